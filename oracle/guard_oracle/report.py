@@ -1,0 +1,364 @@
+"""Structured report restatement (TEST INFRASTRUCTURE ONLY -- the parity oracle).
+
+Restates ``report_all_failed_clauses_for_rules`` / ``simplified_json_from_root``
+(``guard/src/rules/eval_context.rs:1965-2435``), ``FileReport::combine`` (:1630-1640),
+the structured loop ``CommonStructuredReporter::report``
+(``commands/reporters/validate/structured.rs:99-133``) and serde_json's pretty writer
+(``to_writer_pretty``: 2-space indent, ryu floats, struct field order = declaration order).
+"""
+from .errors import GuardError
+from . import pv as P
+from .parser import slice_display, parse_rules
+from . import evaluator as E
+from .loader import load_document
+
+CMP_NAME = {k: k for k in ("Eq", "In", "Gt", "Lt", "Le", "Ge", "Exists", "Empty", "IsString", "IsList",
+                            "IsMap", "IsBool", "IsInt", "IsFloat", "IsNull")}
+
+
+class OMap:
+    """ordered JSON object (serde struct / IndexMap)"""
+    __slots__ = ("items",)
+
+    def __init__(self, items):
+        self.items = items
+
+
+def _ur_json(ur):
+    return OMap([("traversed_to", P.serialize(ur.traversed_to)),
+                 ("remaining_query", ur.remaining_query),
+                 ("reason", ur.reason)])
+
+
+def _pav_json(v):
+    s = P.serialize(v)
+    return OMap([("path", s["path"]), ("value", s["value"])])
+
+
+def _messages(custom, error):
+    return OMap([("custom_message", custom), ("error_message", error)])
+
+
+def _unary_cmp_msg(cmp, neg):
+    table = {
+        "Exists": ("existed", "did not exist"), "Empty": ("was empty", "was not empty"),
+        "IsList": ("was a list ", "was not list"), "IsMap": ("was a struct", "was not struct"),
+        "IsString": ("was a string ", "was not string"), "IsInt": ("was int", "was not int"),
+        "IsBool": ("was bool", "was not bool"), "IsNull": ("was null", "was not null"),
+    }
+    a, b = table.get(cmp, ("was float", "was not float"))
+    return a if neg else b
+
+
+_OP_MSG = {
+    "Eq": ("equal to", "not equal to"), "Le": ("less than equal to", "not less than equal to"),
+    "Lt": ("less than", "not less than"), "Ge": ("greater than equal to", "not greater than equal"),
+    "Gt": ("greater than", "not greater than"), "In": ("in", "not in"),
+}
+
+
+def _qr_display(q):
+    # impl Display for QueryResult (display.rs:109-126)
+    k, v = q
+    if k == "L":
+        return "literal, %s" % P.display(v)
+    if k == "R":
+        return "(resolved, %s)" % P.display(v)
+    return "(unresolved, %s)" % P.display(v.traversed_to)
+
+
+def report_all_failed(checks):
+    clauses = []
+    for cur in checks:
+        c = cur.container
+        if c is None:
+            continue
+        k = c[0]
+        if k == "RuleCheck" and c[2] == E.FAIL:
+            clauses.append(("Rule", OMap([
+                ("name", c[1]), ("metadata", OMap([])),
+                ("messages", _messages(c[3], None)),
+                ("checks", report_all_failed(cur.children))])))
+        elif k == "BlockGuardCheck" and c[1] == E.FAIL:
+            if not cur.children:
+                clauses.append(("Block", OMap([
+                    ("context", cur.context),
+                    ("messages", _messages(None, "query for block clause did not retrieve any value")),
+                    ("unresolved", None)])))
+            else:
+                clauses.extend(report_all_failed(cur.children))
+        elif k == "Disjunction" and c[1] == E.FAIL:
+            clauses.append(("Disjunctions", OMap([("checks", report_all_failed(cur.children))])))
+        elif k in ("GuardClauseBlockCheck", "TypeBlock", "TypeCheck", "WhenCheck") and c[1] == E.FAIL:
+            clauses.extend(report_all_failed(cur.children))
+        elif k == "ClauseValueCheck":
+            cc = c[1]
+            ck = cc[0]
+            if ck == "NoValueForEmptyCheck":
+                custom = (cc[1] or "").replace("\n", ";")
+                err = "Check was not compliant as variable in context [%s] was not empty" % cur.context
+                clauses.append(("Clause", ("Unary", OMap([
+                    ("check", OMap([("UnResolvedContext", cur.context)])),
+                    ("context", cur.context),
+                    ("messages", _messages(custom, err))]))))
+            elif ck == "DependentRule":
+                m = cc[1]
+                err = "Check was not compliant as dependent rule [%s] did not PASS. Context [%s]" % (m["rule"], cur.context)
+                clauses.append(("Clause", ("Unary", OMap([
+                    ("check", OMap([("UnResolvedContext", m["rule"])])),
+                    ("context", cur.context),
+                    ("messages", _messages(m["custom_message"] or "", err))]))))
+            elif ck == "MissingBlockValue":
+                m = cc[1]
+                ur = m["from"][1]
+                err = "Check was not compliant as property [%s] is missing. Value traversed to [%s]" % (
+                    ur.remaining_query, P.display(ur.traversed_to))
+                clauses.append(("Block", OMap([
+                    ("context", cur.context),
+                    ("messages", _messages(m["custom_message"] or "", err)),
+                    ("unresolved", _ur_json(ur))])))
+            elif ck == "Unary":
+                m = cc[1]
+                cmp, neg = m["comparison"]
+                cmp_msg = _unary_cmp_msg(cmp, neg)
+                custom = m["custom_message"] or ""
+                errm = "" if m["message"] is None else "Error = [%s]" % m["message"]
+                frm = m["from"]
+                if frm[0] == "R":
+                    res = frm[1]
+                    msg = "Check was not compliant as property [%s] %s.%s" % (res.path_display(), cmp_msg, errm)
+                    check = OMap([("Resolved", OMap([("value", _pav_json(res)), ("comparison", [cmp, neg])]))])
+                else:
+                    ur = frm[1]
+                    msg = "Check was not compliant as property [%s] is missing. Value traversed to [%s].%s" % (
+                        ur.remaining_query, P.display(ur.traversed_to), errm)
+                    check = OMap([("UnResolved", OMap([("value", _ur_json(ur)), ("comparison", [cmp, neg])]))])
+                clauses.append(("Clause", ("Unary", OMap([
+                    ("check", check), ("context", cur.context), ("messages", _messages(custom, msg))]))))
+            elif ck == "Comparison":
+                m = cc[1]
+                cmp, neg = m["comparison"]
+                custom = m["custom_message"] or ""
+                errm = "" if m["message"] is None else " Error = [%s]" % m["message"]
+                frm = m["from"]
+                if frm[0] == "U":
+                    ur = frm[1]
+                    msg = ("Check was not compliant as property [%s] to compare from is missing. "
+                           "Value traversed to [%s].%s" % (ur.remaining_query, P.display(ur.traversed_to), errm))
+                    clauses.append(("Clause", ("Binary", OMap([
+                        ("context", cur.context), ("messages", _messages(custom, msg)),
+                        ("check", OMap([("UnResolved", OMap([("value", _ur_json(ur)), ("comparison", [cmp, neg])]))]))]))))
+                else:
+                    res = frm[1]
+                    to = m["to"]
+                    if to is None:
+                        continue
+                    if to[0] == "R":
+                        a, b = _OP_MSG[cmp]
+                        msg = "Check was not compliant as property value [%s] %s value [%s].%s" % (
+                            P.display(res), a if neg else b, P.display(to[1]), errm)
+                        clauses.append(("Clause", ("Binary", OMap([
+                            ("context", cur.context), ("messages", _messages(custom, msg)),
+                            ("check", OMap([("Resolved", OMap([("from", _pav_json(res)), ("to", _pav_json(to[1])),
+                                                               ("comparison", [cmp, neg])]))]))]))))
+                    else:
+                        ur = to[1]
+                        msg = ("Check was not compliant as property [%s] to compare to is missing. "
+                               "Value traversed to [%s].%s" % (ur.remaining_query, P.display(ur.traversed_to), errm))
+                        clauses.append(("Clause", ("Binary", OMap([
+                            ("context", cur.context), ("messages", _messages(custom, msg)),
+                            ("check", OMap([("UnResolved", OMap([("value", _ur_json(ur)), ("comparison", [cmp, neg])]))]))]))))
+            elif ck == "InComparison":
+                m = cc[1]
+                frm = m["from"][1]
+                to = m["to"]
+                err = "Check was not compliant as property [%s] was not present in [%s]" % (
+                    frm.path_display(), slice_display(to, _qr_display))
+                clauses.append(("Clause", ("Binary", OMap([
+                    ("context", cur.context),
+                    ("messages", _messages(m["custom_message"], err)),
+                    ("check", OMap([("InResolved", OMap([
+                        ("from", _pav_json(frm)),
+                        ("to", [_pav_json(t[1]) for t in to if t[0] == "R"]),
+                        ("comparison", list(m["comparison"]))]))]))]))))
+    return clauses
+
+
+def _clause_json(c):
+    kind, body = c
+    if kind == "Clause":
+        sub, inner = body
+        return OMap([("Clause", OMap([(sub, _fix(inner))]))])
+    return OMap([(kind, _fix(body))])
+
+
+def _fix(o):
+    if isinstance(o, OMap):
+        return OMap([(k, _fix(v)) for k, v in o.items])
+    if isinstance(o, list):
+        return [_fix_item(x) for x in o]
+    return o
+
+
+def _fix_item(x):
+    if isinstance(x, tuple) and len(x) == 2 and isinstance(x[0], str) and x[0] in (
+            "Rule", "Block", "Disjunctions", "Clause"):
+        return _clause_json(x)
+    return _fix(x)
+
+
+def simplified_json_from_root(root):
+    c = root.container
+    assert c[0] == "FileCheck"
+    passed, skipped = set(), set()
+    for ch in root.children:
+        cc = ch.container
+        if cc is not None and cc[0] == "RuleCheck":
+            if cc[2] == E.PASS:
+                passed.add(cc[1])
+            elif cc[2] == E.SKIP:
+                skipped.add(cc[1])
+    return {"name": c[1], "status": c[2], "not_compliant": report_all_failed(root.children),
+            "not_applicable": skipped, "compliant": passed}
+
+
+def _rust_str_key(s):
+    return s.encode("utf-8", "surrogatepass")
+
+
+def file_report_json(fr):
+    return OMap([("name", fr["name"]), ("metadata", OMap([])), ("status", fr["status"]),
+                 ("not_compliant", [_clause_json(c) for c in fr["not_compliant"]]),
+                 ("not_applicable", sorted(fr["not_applicable"], key=_rust_str_key)),
+                 ("compliant", sorted(fr["compliant"], key=_rust_str_key))])
+
+
+# ---------------------------------------------------------------------------
+# serde_json pretty writer
+# ---------------------------------------------------------------------------
+def _json_str(s):
+    out = ['"']
+    for ch in s:
+        o = ord(ch)
+        if ch == '"':
+            out.append('\\"')
+        elif ch == "\\":
+            out.append("\\\\")
+        elif ch == "\n":
+            out.append("\\n")
+        elif ch == "\r":
+            out.append("\\r")
+        elif ch == "\t":
+            out.append("\\t")
+        elif ch == "\b":
+            out.append("\\b")
+        elif ch == "\f":
+            out.append("\\f")
+        elif o < 0x20:
+            out.append("\\u%04x" % o)
+        else:
+            out.append(ch)
+    out.append('"')
+    return "".join(out)
+
+
+def to_json_pretty(o, indent=0):
+    pad = "  " * indent
+    pad1 = "  " * (indent + 1)
+    if o is None:
+        return "null"
+    if o is True:
+        return "true"
+    if o is False:
+        return "false"
+    if isinstance(o, P.JFloat):
+        return P.ryu_f64(o.v)
+    if isinstance(o, int):
+        return str(o)
+    if isinstance(o, str):
+        return _json_str(o)
+    if isinstance(o, OMap):
+        if not o.items:
+            return "{}"
+        parts = ["%s%s: %s" % (pad1, _json_str(k), to_json_pretty(v, indent + 1)) for k, v in o.items]
+        return "{\n" + ",\n".join(parts) + "\n" + pad + "}"
+    if isinstance(o, dict):
+        return to_json_pretty(OMap(list(o.items())), indent)
+    if isinstance(o, (list, tuple)):
+        if not o:
+            return "[]"
+        parts = ["%s%s" % (pad1, to_json_pretty(v, indent + 1)) for v in o]
+        return "[\n" + ",\n".join(parts) + "\n" + pad + "]"
+    raise TypeError(type(o))
+
+
+# ---------------------------------------------------------------------------
+# drivers
+# ---------------------------------------------------------------------------
+SUCCESS, FAILURE_STATUS, ERROR_STATUS = 0, 19, 5
+
+
+def eval_file_report(rules_file, doc, data_name):
+    root = E.RootScope(rules_file, doc)
+    status = E.eval_rules_file(rules_file, root, data_name)
+    rec = root.recorder.final_event
+    return status, simplified_json_from_root(rec)
+
+
+def validate_structured(rules, data, parsed_docs=None):
+    """``cfn-guard validate --structured -o json -S none`` over in-memory inputs.
+
+    rules: list of (rules_file_name, text); data: list of (data_name, text).
+    Returns (stdout_text, exit_code, stderr_text).  Evaluation errors abort the run with
+    no stdout, exit code -1 (main.rs:35-42)."""
+    exit_code = SUCCESS
+    stderr = []
+    parsed_rules = []
+    for name, text in rules:
+        try:
+            rf = parse_rules(text, name)
+        except GuardError as e:
+            stderr.append("Parsing error handling rule file = %s, Error = %s\n---" % (name, e.display()))
+            exit_code = ERROR_STATUS
+            continue
+        if rf is not None:
+            parsed_rules.append((rf, name))
+    try:
+        docs = parsed_docs if parsed_docs is not None else [(n, load_document(t, n)) for n, t in data]
+        records = []
+        for dname, doc in docs:
+            fr = {"name": dname, "status": E.SKIP, "not_compliant": [], "not_applicable": set(), "compliant": set()}
+            for rf, _ in parsed_rules:
+                st, rep = eval_file_report(rf, doc, dname)
+                if st == E.FAIL:
+                    exit_code = FAILURE_STATUS
+                fr["status"] = E.status_and(fr["status"], rep["status"])
+                fr["not_compliant"].extend(rep["not_compliant"])
+                fr["compliant"] |= rep["compliant"]
+                fr["not_applicable"] |= rep["not_applicable"]
+            records.append(file_report_json(fr))
+        out = to_json_pretty(records)
+    except GuardError as e:
+        return "", -1, "".join(stderr) + "Error occurred %s" % e.display()
+    return out, exit_code, "".join(stderr)
+
+
+def run_checks(data_text, data_name, rules_text, rules_name):
+    """guard-ffi ``run_checks`` (commands/helper.rs:25-87), verbose = false.
+    Returns the pretty FileReport JSON or raises GuardError."""
+    from .loader import load_serde_json
+    try:
+        doc = load_serde_json(data_text)
+    except GuardError:
+        raise
+    except Exception:
+        raise GuardError("Unsupported", "serde_yaml fallback is outside the oracle's scope")
+    rf = parse_rules(rules_text, rules_name)
+    if rf is None:
+        return ""
+    st, rep = eval_file_report(rf, doc, data_name)
+    return to_json_pretty(OMap([
+        ("name", rep["name"]), ("metadata", OMap([])), ("status", rep["status"]),
+        ("not_compliant", [_clause_json(c) for c in rep["not_compliant"]]),
+        ("not_applicable", sorted(rep["not_applicable"], key=_rust_str_key)),
+        ("compliant", sorted(rep["compliant"], key=_rust_str_key))]))
