@@ -1,0 +1,684 @@
+// Document loader (see doc_loader.h for the reference mapping).
+#include "doc_loader.h"
+
+#include <yaml.h>
+
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <unordered_map>
+
+#include "host_format.h"
+
+namespace gg {
+
+// ------------------------------------------------------------ Rust parsing ---
+// `str::parse::<i64>()`
+static bool rust_parse_i64(const std::string& s, int64_t& out) {
+  size_t i = 0, n = s.size();
+  bool neg = false;
+  if (i < n && (s[i] == '+' || s[i] == '-')) { neg = s[i] == '-'; i++; }
+  if (i >= n) return false;
+  unsigned __int128 v = 0;
+  for (; i < n; i++) {
+    if (s[i] < '0' || s[i] > '9') return false;
+    v = v * 10 + (unsigned)(s[i] - '0');
+    if (v > ((unsigned __int128)1 << 63)) return false;
+  }
+  if (!neg && v > (unsigned __int128)INT64_MAX) return false;
+  out = neg ? (int64_t)(-(__int128)v) : (int64_t)v;
+  return true;
+}
+
+// `str::parse::<f64>()` (Rust dec2flt grammar + inf/infinity/nan, case-insensitive)
+static bool rust_parse_f64(const std::string& s, double& out) {
+  size_t i = 0, n = s.size();
+  bool neg = false;
+  if (i < n && (s[i] == '+' || s[i] == '-')) { neg = s[i] == '-'; i++; }
+  std::string rest = s.substr(i);
+  std::string low;
+  for (char c : rest) low.push_back((char)tolower((unsigned char)c));
+  if (low == "inf" || low == "infinity") { out = neg ? -INFINITY : INFINITY; return true; }
+  if (low == "nan") { out = NAN; return true; }
+  size_t j = i, digits = 0;
+  while (j < n && isdigit((unsigned char)s[j])) { j++; digits++; }
+  if (j < n && s[j] == '.') { j++; while (j < n && isdigit((unsigned char)s[j])) { j++; digits++; } }
+  if (digits == 0) return false;
+  if (j < n && (s[j] == 'e' || s[j] == 'E')) {
+    j++;
+    if (j < n && (s[j] == '+' || s[j] == '-')) j++;
+    size_t ed = 0;
+    while (j < n && isdigit((unsigned char)s[j])) { j++; ed++; }
+    if (ed == 0) return false;
+  }
+  if (j != n) return false;
+  out = strtod(s.c_str(), nullptr);
+  return true;
+}
+
+// ------------------------------------------------------------- temp tree ---
+namespace {
+
+struct TN {
+  uint32_t kind = K_NULL;
+  int64_t i = 0;
+  double f = 0;
+  std::string s;
+  bool bad = false;
+  uint32_t line = 0, col = 0;
+  std::vector<uint32_t> kids;
+  std::vector<std::string> keys;
+  std::vector<std::pair<uint32_t, uint32_t>> kmarks;
+};
+
+struct Tree {
+  std::vector<TN> n;
+  uint32_t add(TN&& t) { n.push_back(std::move(t)); return (uint32_t)n.size() - 1; }
+};
+
+const char* kShort[][2] = {
+    {"Ref", "Ref"}, {"GetAtt", "Fn::GetAtt"}, {"Base64", "Fn::Base64"}, {"Sub", "Fn::Sub"},
+    {"GetAZs", "Fn::GetAZs"}, {"ImportValue", "Fn::ImportValue"}, {"Condition", "Condition"},
+    {"RefAll", "Fn::RefAll"}, {"Select", "Fn::Select"}, {"Split", "Fn::Split"}, {"Join", "Fn::Join"},
+    {"FindInMap", "Fn::FindInMap"}, {"And", "Fn::And"}, {"Equals", "Fn::Equals"},
+    {"Contains", "Fn::Contains"}, {"EachMemberIn", "Fn::EachMemberIn"},
+    {"EachMemberEquals", "Fn::EachMemberEquals"}, {"ValueOf", "Fn::ValueOf"}, {"If", "Fn::If"},
+    {"Not", "Fn::Not"}, {"Or", "Fn::Or"}};
+const char* kSingle[] = {"Ref", "Base64", "Sub", "GetAZs", "ImportValue", "GetAtt", "Condition", "RefAll"};
+const char* kSeq[] = {"GetAtt", "Sub", "Select", "Split", "Join", "FindInMap", "And", "Equals", "Contains",
+                      "EachMemberIn", "EachMemberEquals", "ValueOf", "If", "Not", "Or"};
+
+bool in_set(const char* const* set, size_t n, const std::string& s) {
+  for (size_t i = 0; i < n; i++) if (s == set[i]) return true;
+  return false;
+}
+bool is_single(const std::string& s) { return in_set(kSingle, sizeof kSingle / sizeof *kSingle, s); }
+bool is_seq(const std::string& s) { return in_set(kSeq, sizeof kSeq / sizeof *kSeq, s); }
+std::string long_form(const std::string& s) {
+  for (auto& p : kShort) if (s == p[0]) return p[1];
+  return s;
+}
+
+void split_tag(const std::string& tag, std::string& handle, std::string& suffix) {
+  size_t i = 0;
+  while (i < tag.size() && tag[i] == '!') i++;
+  handle = tag.substr(0, i);
+  suffix = tag.substr(i);
+}
+
+const char* TYPE_REF_PREFIX = "tag:yaml.org,2002:";
+
+// loader.rs:62-102 (+ handle_type_ref 227-244, handle_single_value_func_ref 197-211)
+uint32_t scalar_node(Tree& t, const std::string& val, const char* tag, bool plain, uint32_t line, uint32_t col) {
+  TN n; n.line = line; n.col = col;
+  if (tag) {
+    std::string handle, suffix;
+    split_tag(tag, handle, suffix);
+    if (handle == "!") {
+      if (is_single(suffix)) {
+        TN inner; inner.kind = K_STRING; inner.s = val; inner.line = line; inner.col = col;
+        uint32_t ii = t.add(std::move(inner));
+        n.kind = K_MAP; n.keys.push_back(long_form(suffix)); n.kmarks.push_back({line, col}); n.kids.push_back(ii);
+        return t.add(std::move(n));
+      }
+      n.kind = K_STRING; n.s = val; return t.add(std::move(n));
+    }
+    if (suffix.rfind(TYPE_REF_PREFIX, 0) == 0) {
+      if (suffix == "tag:yaml.org,2002:bool") {
+        if (val == "true") { n.kind = K_BOOL; n.i = 1; }
+        else if (val == "false") { n.kind = K_BOOL; n.i = 0; }
+        else { n.kind = K_STRING; n.s = val; }
+      } else if (suffix == "tag:yaml.org,2002:int") {
+        int64_t v;
+        if (rust_parse_i64(val, v)) { n.kind = K_INT; n.i = v; } else { n.bad = true; n.s = val; }
+      } else if (suffix == "tag:yaml.org,2002:float") {
+        double v;
+        if (rust_parse_f64(val, v)) { n.kind = K_FLOAT; n.f = v; } else { n.bad = true; n.s = val; }
+      } else if (suffix == "tag:yaml.org,2002:null") {
+        n.kind = K_NULL;
+      } else { n.kind = K_STRING; n.s = val; }
+      return t.add(std::move(n));
+    }
+    n.kind = K_STRING; n.s = val; return t.add(std::move(n));
+  }
+  if (!plain) { n.kind = K_STRING; n.s = val; return t.add(std::move(n)); }
+  int64_t iv; double fv;
+  if (rust_parse_i64(val, iv)) { n.kind = K_INT; n.i = iv; }
+  else if (rust_parse_f64(val, fv)) { n.kind = K_FLOAT; n.f = fv; }
+  else if (val == "true" || val == "yes" || val == "on" || val == "y") { n.kind = K_BOOL; n.i = 1; }
+  else if (val == "false" || val == "no" || val == "off" || val == "n") { n.kind = K_BOOL; n.i = 0; }
+  else {
+    std::string low;
+    for (char c : val) low.push_back((char)tolower((unsigned char)c));
+    if (low == "~" || low == "null") n.kind = K_NULL;
+    else { n.kind = K_STRING; n.s = val; }
+  }
+  return t.add(std::move(n));
+}
+
+// serde_yaml 0.9 (YAML 1.2 core) plain scalar resolution
+uint32_t serde_yaml_scalar(Tree& t, const std::string& val, bool plain) {
+  TN n;
+  if (!plain) { n.kind = K_STRING; n.s = val; return t.add(std::move(n)); }
+  if (val == "~" || val == "null" || val == "Null" || val == "NULL" || val.empty()) { n.kind = K_NULL; return t.add(std::move(n)); }
+  if (val == "true" || val == "True" || val == "TRUE") { n.kind = K_BOOL; n.i = 1; return t.add(std::move(n)); }
+  if (val == "false" || val == "False" || val == "FALSE") { n.kind = K_BOOL; n.i = 0; return t.add(std::move(n)); }
+  // ints: [-+]?(digits | 0x.. | 0o.. | 0b..)
+  {
+    size_t i = 0; bool neg = false;
+    if (i < val.size() && (val[i] == '+' || val[i] == '-')) { neg = val[i] == '-'; i++; }
+    std::string body = val.substr(i);
+    int base = 10; size_t start = 0;
+    if (body.size() > 2 && body[0] == '0' && (body[1] == 'x' || body[1] == 'o' || body[1] == 'b')) {
+      base = body[1] == 'x' ? 16 : body[1] == 'o' ? 8 : 2; start = 2;
+    }
+    bool ok = start < body.size();
+    unsigned __int128 v = 0; bool overflow = false;
+    for (size_t j = start; j < body.size() && ok; j++) {
+      int d;
+      char c = body[j];
+      if (c >= '0' && c <= '9') d = c - '0';
+      else if (c >= 'a' && c <= 'f') d = c - 'a' + 10;
+      else if (c >= 'A' && c <= 'F') d = c - 'A' + 10;
+      else { ok = false; break; }
+      if (d >= base) { ok = false; break; }
+      v = v * base + d;
+      if (v > ((unsigned __int128)1 << 64)) overflow = true;
+    }
+    if (ok) {
+      n.kind = K_INT;
+      if (!overflow && !neg && v <= (unsigned __int128)INT64_MAX) { n.i = (int64_t)v; return t.add(std::move(n)); }
+      if (!overflow && neg && v <= ((unsigned __int128)1 << 63)) { n.i = (int64_t)(-(__int128)v); return t.add(std::move(n)); }
+      if (!overflow && !neg && v <= (unsigned __int128)UINT64_MAX) { n.i = (int64_t)(uint64_t)v; return t.add(std::move(n)); }
+      n.kind = K_FLOAT; n.f = strtod(val.c_str(), nullptr); return t.add(std::move(n));
+    }
+  }
+  {
+    double fv;
+    std::string low;
+    for (char c : val) low.push_back((char)tolower((unsigned char)c));
+    if (low == ".inf" || low == "+.inf") { n.kind = K_FLOAT; n.f = INFINITY; return t.add(std::move(n)); }
+    if (low == "-.inf") { n.kind = K_FLOAT; n.f = -INFINITY; return t.add(std::move(n)); }
+    if (low == ".nan") { n.kind = K_FLOAT; n.f = NAN; return t.add(std::move(n)); }
+    bool okf = !val.empty() && rust_parse_f64(val, fv) && low.find("inf") == std::string::npos && low.find("nan") == std::string::npos;
+    if (okf) { n.kind = K_FLOAT; n.f = fv; return t.add(std::move(n)); }
+  }
+  n.kind = K_STRING; n.s = val; return t.add(std::move(n));
+}
+
+struct Emitter {
+  DocBatch& b;
+  Tree& t;
+  bool serde;
+  void fill(uint32_t ti, uint32_t slot, uint32_t parent, uint32_t line, uint32_t col) {
+    TN& n = t.n[ti];
+    DNode& d = b.nodes[slot];
+    d.kind = n.kind; d.count = 0; d.a = 0; d.b = 0; d.parent = parent;
+    b.line[slot] = line; b.col[slot] = col;
+    switch (n.kind) {
+      case K_STRING: {
+        d.a = (uint32_t)b.bytes.size(); d.count = (uint32_t)n.s.size();
+        d.b = fnv1a(n.s.data(), n.s.size());
+        b.bytes += n.s;
+        break;
+      }
+      case K_BOOL: d.a = (uint32_t)n.i; break;
+      case K_INT: { uint64_t u = (uint64_t)n.i; d.a = (uint32_t)u; d.b = (uint32_t)(u >> 32); break; }
+      case K_FLOAT: { uint64_t u; memcpy(&u, &n.f, 8); d.a = (uint32_t)u; d.b = (uint32_t)(u >> 32); break; }
+      case K_LIST: {
+        uint32_t cnt = (uint32_t)n.kids.size();
+        uint32_t first = (uint32_t)b.nodes.size();
+        grow(cnt);
+        DNode& dd = b.nodes[slot];
+        dd.a = first; dd.count = cnt;
+        for (uint32_t j = 0; j < cnt; j++) {
+          uint32_t k = t.n[ti].kids[j];
+          const TN& kn = t.n[k];
+          b.nodes[first + j].key_off = NONE; b.nodes[first + j].key_len = 0; b.nodes[first + j].key_hash = 0;
+          fill(k, first + j, slot, serde ? 0 : kn.line, serde ? 0 : kn.col);
+        }
+        break;
+      }
+      case K_MAP: {
+        // IndexMap<String, _>::insert over the (key, mark) entries: first position, last value
+        std::vector<std::string> keys;
+        std::vector<std::pair<uint32_t, uint32_t>> kmarks;
+        std::vector<uint32_t> vals;
+        std::unordered_map<std::string, size_t> pos;
+        for (size_t j = 0; j < t.n[ti].keys.size(); j++) {
+          const std::string& k = t.n[ti].keys[j];
+          auto it = pos.find(k);
+          if (it == pos.end()) {
+            pos[k] = keys.size(); keys.push_back(k); kmarks.push_back(t.n[ti].kmarks[j]); vals.push_back(t.n[ti].kids[j]);
+          } else {
+            vals[it->second] = t.n[ti].kids[j];
+          }
+        }
+        uint32_t cnt = (uint32_t)keys.size();
+        uint32_t first = (uint32_t)b.nodes.size();
+        grow(cnt);
+        DNode& dd = b.nodes[slot];
+        dd.a = first; dd.count = cnt;
+        for (uint32_t j = 0; j < cnt; j++) {
+          DNode& c = b.nodes[first + j];
+          c.key_off = (uint32_t)b.bytes.size(); c.key_len = (uint32_t)keys[j].size();
+          c.key_hash = fnv1a(keys[j].data(), keys[j].size());
+          b.bytes += keys[j];
+          b.kline[first + j] = serde ? 0 : kmarks[j].first;
+          b.kcol[first + j] = serde ? 0 : kmarks[j].second;
+          const TN& kn = t.n[vals[j]];
+          fill(vals[j], first + j, slot, serde ? 0 : kn.line, serde ? 0 : kn.col);
+        }
+        break;
+      }
+      default: break;
+    }
+  }
+  void grow(uint32_t cnt) {
+    size_t s = b.nodes.size() + cnt;
+    b.nodes.resize(s); b.line.resize(s); b.col.resize(s); b.kline.resize(s); b.kcol.resize(s);
+  }
+};
+
+bool check_bad(const Tree& t, uint32_t ti, LoadError& err) {
+  const TN& n = t.n[ti];
+  if (n.bad) {
+    err.kind = "ParseError";
+    err.msg = "Bad Value encountered parsing incoming file Value = " + n.s + ", Loc = L:" + std::to_string(n.line) +
+              ",C:" + std::to_string(n.col);
+    return false;
+  }
+  for (uint32_t k : n.kids) if (!check_bad(t, k, err)) return false;
+  return true;
+}
+
+bool emit_root(DocBatch& b, Tree& t, uint32_t root, const std::string& name, bool serde, LoadError& err) {
+  if (!check_bad(t, root, err)) return false;
+  Emitter e{b, t, serde};
+  uint32_t slot = (uint32_t)b.nodes.size();
+  e.grow(1);
+  b.nodes[slot].key_off = NONE; b.nodes[slot].key_len = 0; b.nodes[slot].key_hash = 0;
+  const TN& r = t.n[root];
+  uint32_t line = 0, col = 0;
+  // root: Path::root() (L0,C0) keeps its location for lists; maps/scalars take their own mark
+  if (!serde && r.kind != K_LIST) { line = r.line; col = r.col; }
+  e.fill(root, slot, NONE, line, col);
+  b.roots.push_back(slot);
+  b.names.push_back(name);
+  return true;
+}
+
+// ------------------------------------------------------ libyaml event loop ---
+struct YamlParser {
+  yaml_parser_t p;
+  bool ok;
+  YamlParser(const char* text, size_t len) {
+    ok = yaml_parser_initialize(&p) != 0;
+    yaml_parser_set_encoding(&p, YAML_UTF8_ENCODING);
+    yaml_parser_set_input_string(&p, (const unsigned char*)text, len);
+  }
+  ~YamlParser() { yaml_parser_delete(&p); }
+};
+
+std::string ev_scalar(const yaml_event_t& ev) {
+  return std::string((const char*)ev.data.scalar.value, ev.data.scalar.length);
+}
+
+// Loader::load (loader.rs:31-60): returns root tree node of the first document
+bool libyaml_load(const char* text, size_t len, Tree& t, uint32_t& root, LoadError& err) {
+  YamlParser yp(text, len);
+  std::vector<uint32_t> stack, last_container;
+  std::vector<std::pair<size_t, std::pair<std::string, std::pair<uint32_t, uint32_t>>>> func_support;
+  for (;;) {
+    yaml_event_t ev;
+    if (yp.p.error != YAML_NO_ERROR || !yaml_parser_parse(&yp.p, &ev)) {
+      err.kind = "ParseError"; err.msg = "error parsing file"; return false;
+    }
+    uint32_t line = (uint32_t)ev.start_mark.line, col = (uint32_t)ev.start_mark.column;
+    bool done = false;
+    switch (ev.type) {
+      case YAML_STREAM_START_EVENT: case YAML_DOCUMENT_START_EVENT: break;
+      case YAML_STREAM_END_EVENT: case YAML_NO_EVENT:
+        // the reference keeps polling after STREAM-END and panics (unimplemented!())
+        yaml_event_delete(&ev);
+        err.kind = "ParseError"; err.msg = "error parsing file"; return false;
+      case YAML_DOCUMENT_END_EVENT:
+        root = stack.back(); done = true; break;
+      case YAML_MAPPING_START_EVENT: {
+        TN n; n.kind = K_MAP; n.line = line; n.col = col;
+        stack.push_back(t.add(std::move(n)));
+        last_container.push_back((uint32_t)stack.size() - 1);
+        break;
+      }
+      case YAML_MAPPING_END_EVENT: {
+        uint32_t idx = last_container.back(); last_container.pop_back();
+        std::vector<uint32_t> kvs(stack.begin() + idx + 1, stack.end());
+        stack.resize(idx + 1);
+        uint32_t m = stack.back();
+        for (size_t j = 0; j + 1 < kvs.size(); j += 2) {
+          const TN& k = t.n[kvs[j]];
+          if (k.kind != K_STRING || k.bad) {
+            yaml_event_delete(&ev);
+            err.kind = "InternalError";
+            err.msg = "non string type detected for key in a map at L:" + std::to_string(k.line) + ",C:" +
+                      std::to_string(k.col) + ", cfn-guard only supports keys that are string types";
+            return false;
+          }
+          // IndexMap<(String, Location)>::insert
+          TN& mm = t.n[m];
+          bool replaced = false;
+          for (size_t q = 0; q < mm.keys.size(); q++) {
+            if (mm.keys[q] == k.s && mm.kmarks[q].first == k.line && mm.kmarks[q].second == k.col) {
+              mm.kids[q] = kvs[j + 1]; replaced = true; break;
+            }
+          }
+          if (!replaced) { mm.keys.push_back(k.s); mm.kmarks.push_back({k.line, k.col}); mm.kids.push_back(kvs[j + 1]); }
+        }
+        break;
+      }
+      case YAML_SEQUENCE_START_EVENT: {
+        if (ev.data.sequence_start.tag) {
+          std::string handle, suffix;
+          split_tag((const char*)ev.data.sequence_start.tag, handle, suffix);
+          if (handle == "!" && is_seq(suffix)) {
+            TN nul; nul.kind = K_NULL; nul.line = line; nul.col = col;
+            uint32_t ni = t.add(std::move(nul));
+            TN m; m.kind = K_MAP; m.line = line; m.col = col;
+            m.keys.push_back(long_form(suffix)); m.kmarks.push_back({line, col}); m.kids.push_back(ni);
+            stack.push_back(t.add(std::move(m)));
+            func_support.push_back({stack.size() - 1, {long_form(suffix), {line, col}}});
+          }
+        }
+        TN n; n.kind = K_LIST; n.line = line; n.col = col;
+        stack.push_back(t.add(std::move(n)));
+        last_container.push_back((uint32_t)stack.size() - 1);
+        break;
+      }
+      case YAML_SEQUENCE_END_EVENT: {
+        uint32_t idx = last_container.back(); last_container.pop_back();
+        std::vector<uint32_t> vals(stack.begin() + idx + 1, stack.end());
+        stack.resize(idx + 1);
+        for (uint32_t v : vals) t.n[stack.back()].kids.push_back(v);
+        if (!func_support.empty() && func_support.back().first + 1 == idx) {
+          auto fs = func_support.back(); func_support.pop_back();
+          uint32_t arr = stack.back(); stack.pop_back();
+          TN& mm = t.n[stack.back()];
+          if (mm.kind == K_MAP) {
+            bool replaced = false;
+            for (size_t q = 0; q < mm.keys.size(); q++) {
+              if (mm.keys[q] == fs.second.first && mm.kmarks[q] == fs.second.second) { mm.kids[q] = arr; replaced = true; break; }
+            }
+            if (!replaced) { mm.keys.push_back(fs.second.first); mm.kmarks.push_back(fs.second.second); mm.kids.push_back(arr); }
+          }
+        }
+        break;
+      }
+      case YAML_SCALAR_EVENT: {
+        std::string v = ev_scalar(ev);
+        stack.push_back(scalar_node(t, v, (const char*)ev.data.scalar.tag,
+                                    ev.data.scalar.style == YAML_PLAIN_SCALAR_STYLE, line, col));
+        break;
+      }
+      case YAML_ALIAS_EVENT:
+        yaml_event_delete(&ev);
+        err.kind = "ParseError"; err.msg = "Guard does not currently support aliases"; return false;
+    }
+    yaml_event_delete(&ev);
+    if (done) return true;
+  }
+}
+
+// serde_yaml Value (YAML 1.2) from libyaml events; tags -> handle_tagged_value (values.rs:455-466)
+bool serde_yaml_load(const char* text, size_t len, Tree& t, uint32_t& root, std::string& msg) {
+  YamlParser yp(text, len);
+  struct Frame { bool map; std::vector<uint32_t> items; std::string tag; };
+  std::vector<Frame> st;
+  st.push_back(Frame{false, {}, ""});
+  for (;;) {
+    yaml_event_t ev;
+    if (yp.p.error != YAML_NO_ERROR || !yaml_parser_parse(&yp.p, &ev)) {
+      msg = yp.p.problem ? yp.p.problem : "error parsing YAML"; return false;
+    }
+    bool done = false;
+    auto wrap_tag = [&](uint32_t node, const std::string& tag) -> uint32_t {
+      size_t bangs = 0;
+      for (char c : tag) if (c == '!') bangs++;
+      if (!tag.empty() && tag[0] == '!' && bangs == 1) {
+        std::string fn = tag.substr(1);
+        if (is_single(fn) || is_seq(fn)) {
+          TN m; m.kind = K_MAP; m.keys.push_back(long_form(fn)); m.kmarks.push_back({0, 0}); m.kids.push_back(node);
+          return t.add(std::move(m));
+        }
+      }
+      return node;
+    };
+    switch (ev.type) {
+      case YAML_SCALAR_EVENT: {
+        std::string v = ev_scalar(ev);
+        const char* tg = (const char*)ev.data.scalar.tag;
+        bool plain = ev.data.scalar.style == YAML_PLAIN_SCALAR_STYLE;
+        uint32_t node;
+        if (tg && tg[0] == '!' && std::string(tg) != "!") {
+          TN s; s.kind = K_STRING; s.s = v;
+          node = wrap_tag(t.add(std::move(s)), tg);
+        } else {
+          node = serde_yaml_scalar(t, v, plain);
+        }
+        st.back().items.push_back(node);
+        break;
+      }
+      case YAML_MAPPING_START_EVENT:
+        st.push_back(Frame{true, {}, ev.data.mapping_start.tag ? (const char*)ev.data.mapping_start.tag : ""});
+        break;
+      case YAML_SEQUENCE_START_EVENT:
+        st.push_back(Frame{false, {}, ev.data.sequence_start.tag ? (const char*)ev.data.sequence_start.tag : ""});
+        break;
+      case YAML_MAPPING_END_EVENT: case YAML_SEQUENCE_END_EVENT: {
+        Frame f = std::move(st.back()); st.pop_back();
+        TN n;
+        if (f.map) {
+          n.kind = K_MAP;
+          for (size_t j = 0; j + 1 < f.items.size(); j += 2) {
+            const TN& k = t.n[f.items[j]];
+            if (k.kind != K_STRING) { yaml_event_delete(&ev); msg = "non string key"; return false; }
+            n.keys.push_back(k.s); n.kmarks.push_back({0, 0}); n.kids.push_back(f.items[j + 1]);
+          }
+        } else {
+          n.kind = K_LIST; n.kids = f.items;
+        }
+        st.back().items.push_back(wrap_tag(t.add(std::move(n)), f.tag));
+        break;
+      }
+      case YAML_ALIAS_EVENT:
+        yaml_event_delete(&ev); msg = "aliases are not supported"; return false;
+      case YAML_DOCUMENT_END_EVENT: done = true; break;
+      case YAML_STREAM_END_EVENT: done = true; break;
+      default: break;
+    }
+    yaml_event_delete(&ev);
+    if (done) break;
+  }
+  if (st.back().items.empty()) { TN n; n.kind = K_NULL; root = t.add(std::move(n)); }
+  else root = st.back().items[0];
+  return true;
+}
+
+// serde_json (preserve_order) strict JSON
+struct JsonP {
+  const char* s; size_t n; size_t i = 0; Tree& t;
+  JsonP(const char* s_, size_t n_, Tree& t_) : s(s_), n(n_), t(t_) {}
+  void ws() { while (i < n && (s[i] == ' ' || s[i] == '\t' || s[i] == '\n' || s[i] == '\r')) i++; }
+  bool str(std::string& out) {
+    if (i >= n || s[i] != '"') return false;
+    i++;
+    while (i < n) {
+      unsigned char c = (unsigned char)s[i];
+      if (c == '"') { i++; return true; }
+      if (c < 0x20) return false;
+      if (c == '\\') {
+        i++;
+        if (i >= n) return false;
+        char e = s[i++];
+        switch (e) {
+          case '"': out.push_back('"'); break;
+          case '\\': out.push_back('\\'); break;
+          case '/': out.push_back('/'); break;
+          case 'b': out.push_back('\b'); break;
+          case 'f': out.push_back('\f'); break;
+          case 'n': out.push_back('\n'); break;
+          case 'r': out.push_back('\r'); break;
+          case 't': out.push_back('\t'); break;
+          case 'u': {
+            auto hex4 = [&](uint32_t& v) -> bool {
+              if (i + 4 > n) return false;
+              v = 0;
+              for (int k = 0; k < 4; k++) {
+                char h = s[i++]; v <<= 4;
+                if (h >= '0' && h <= '9') v |= h - '0';
+                else if (h >= 'a' && h <= 'f') v |= h - 'a' + 10;
+                else if (h >= 'A' && h <= 'F') v |= h - 'A' + 10;
+                else return false;
+              }
+              return true;
+            };
+            uint32_t cp;
+            if (!hex4(cp)) return false;
+            if (cp >= 0xD800 && cp < 0xDC00) {
+              if (i + 2 > n || s[i] != '\\' || s[i + 1] != 'u') return false;
+              i += 2;
+              uint32_t lo;
+              if (!hex4(lo) || lo < 0xDC00 || lo > 0xDFFF) return false;
+              cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
+            } else if (cp >= 0xDC00 && cp <= 0xDFFF) return false;
+            utf8_append(out, cp);
+            break;
+          }
+          default: return false;
+        }
+      } else { out.push_back((char)c); i++; }
+    }
+    return false;
+  }
+  bool value(uint32_t& out, int depth) {
+    if (depth > 128) return false;
+    ws();
+    if (i >= n) return false;
+    char c = s[i];
+    TN node;
+    if (c == '{') {
+      i++; node.kind = K_MAP; ws();
+      if (i < n && s[i] == '}') { i++; out = t.add(std::move(node)); return true; }
+      for (;;) {
+        ws(); std::string k;
+        if (!str(k)) return false;
+        ws(); if (i >= n || s[i] != ':') return false; i++;
+        uint32_t v; if (!value(v, depth + 1)) return false;
+        bool replaced = false;
+        for (size_t q = 0; q < node.keys.size(); q++) if (node.keys[q] == k) { node.kids[q] = v; replaced = true; break; }
+        if (!replaced) { node.keys.push_back(k); node.kmarks.push_back({0, 0}); node.kids.push_back(v); }
+        ws();
+        if (i < n && s[i] == ',') { i++; continue; }
+        if (i < n && s[i] == '}') { i++; break; }
+        return false;
+      }
+      out = t.add(std::move(node)); return true;
+    }
+    if (c == '[') {
+      i++; node.kind = K_LIST; ws();
+      if (i < n && s[i] == ']') { i++; out = t.add(std::move(node)); return true; }
+      for (;;) {
+        uint32_t v; if (!value(v, depth + 1)) return false;
+        node.kids.push_back(v); ws();
+        if (i < n && s[i] == ',') { i++; continue; }
+        if (i < n && s[i] == ']') { i++; break; }
+        return false;
+      }
+      out = t.add(std::move(node)); return true;
+    }
+    if (c == '"') { node.kind = K_STRING; if (!str(node.s)) return false; out = t.add(std::move(node)); return true; }
+    if (!strncmp(s + i, "true", 4) && i + 4 <= n) { i += 4; node.kind = K_BOOL; node.i = 1; out = t.add(std::move(node)); return true; }
+    if (!strncmp(s + i, "false", 5) && i + 5 <= n) { i += 5; node.kind = K_BOOL; node.i = 0; out = t.add(std::move(node)); return true; }
+    if (!strncmp(s + i, "null", 4) && i + 4 <= n) { i += 4; node.kind = K_NULL; out = t.add(std::move(node)); return true; }
+    // number
+    size_t st = i; bool neg = false, isf = false;
+    if (s[i] == '-') { neg = true; i++; }
+    if (i >= n || !isdigit((unsigned char)s[i])) return false;
+    if (s[i] == '0') i++; else while (i < n && isdigit((unsigned char)s[i])) i++;
+    if (i < n && s[i] == '.') { isf = true; i++; if (i >= n || !isdigit((unsigned char)s[i])) return false; while (i < n && isdigit((unsigned char)s[i])) i++; }
+    if (i < n && (s[i] == 'e' || s[i] == 'E')) { isf = true; i++; if (i < n && (s[i] == '+' || s[i] == '-')) i++; if (i >= n || !isdigit((unsigned char)s[i])) return false; while (i < n && isdigit((unsigned char)s[i])) i++; }
+    std::string num(s + st, i - st);
+    if (!isf) {
+      unsigned __int128 v = 0; bool of = false;
+      for (size_t k = neg ? 1 : 0; k < num.size(); k++) { v = v * 10 + (num[k] - '0'); if (v > ((unsigned __int128)1 << 65)) of = true; }
+      if (!of) {
+        if (neg && v <= ((unsigned __int128)1 << 63)) { node.kind = K_INT; node.i = (int64_t)(-(__int128)v); out = t.add(std::move(node)); return true; }
+        if (!neg && v <= (unsigned __int128)UINT64_MAX) { node.kind = K_INT; node.i = (int64_t)(uint64_t)v; out = t.add(std::move(node)); return true; }
+      }
+    }
+    node.kind = K_FLOAT; node.f = strtod(num.c_str(), nullptr);
+    if (std::isinf(node.f)) return false;  // serde_json: number out of range
+    out = t.add(std::move(node)); return true;
+  }
+};
+
+}  // namespace
+
+void DocBatch::clear() {
+  nodes.clear(); bytes.clear(); line.clear(); col.clear(); kline.clear(); kcol.clear(); roots.clear(); names.clear();
+}
+
+std::string DocBatch::path(uint32_t node) const {
+  std::vector<std::string> parts;
+  uint32_t cur = node;
+  while (nodes[cur].parent != NONE) {
+    uint32_t p = nodes[cur].parent;
+    if (nodes[p].kind == K_MAP) parts.push_back(bytes.substr(nodes[cur].key_off, nodes[cur].key_len));
+    else parts.push_back(std::to_string(cur - nodes[p].a));
+    cur = p;
+  }
+  std::string out;
+  for (size_t i = parts.size(); i-- > 0;) { out.push_back('/'); out += parts[i]; }
+  return out;
+}
+
+std::string DocBatch::path_display(uint32_t node) const {
+  return path(node) + "[L:" + std::to_string(line[node]) + ",C:" + std::to_string(col[node]) + "]";
+}
+
+bool load_document(DocBatch& b, const char* text, size_t len, const std::string& name, LoadMode mode, LoadError& err) {
+  Tree t;
+  uint32_t root = 0;
+  if (mode == LOAD_LIBYAML) {
+    std::string tmp(text, len);
+    bool blank = true;
+    for (char c : tmp) if (!isspace((unsigned char)c)) { blank = false; break; }
+    if (blank) {
+      err.kind = "ParseError";
+      err.msg = "Unable to parse a template from data file: " + name + " is empty";
+      return false;
+    }
+    if (!libyaml_load(text, len, t, root, err)) {
+      if (err.kind == "InternalError") { err.kind = "ParseError"; return false; }
+      size_t l = len < 100 ? len : 100;
+      err.kind = "ParseError";
+      err.msg = "Error encountered while parsing data file: " + name + ", data beginning with \n" +
+                std::string(text, l) + "\n ...";
+      return false;
+    }
+    return emit_root(b, t, root, name, false, err);
+  }
+  // serde: JSON first, then YAML (commands/helper.rs:30-42)
+  JsonP jp(text, len, t);
+  bool ok = jp.value(root, 0);
+  if (ok) { jp.ws(); ok = jp.i == len; }
+  if (!ok) {
+    t.n.clear();
+    std::string msg;
+    if (!serde_yaml_load(text, len, t, root, msg)) {
+      err.kind = "YamlError"; err.msg = msg; return false;
+    }
+  }
+  return emit_root(b, t, root, name, true, err);
+}
+
+}  // namespace gg

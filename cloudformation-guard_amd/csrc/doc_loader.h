@@ -1,0 +1,40 @@
+// Document loader: YAML/JSON text -> columnar node arena (host side, then uploaded to HBM).
+//
+// Replaces the reference's document model construction:
+//   Loader::load                       guard/src/rules/libyaml/loader.rs:31-195
+//   PathAwareValue::try_from(Marked)   guard/src/rules/path_value.rs:414-478
+//   build_data_file                    guard/src/commands/validate.rs:760-787
+//   run_checks' serde loader           guard/src/commands/helper.rs:30-42
+// The YAML event stream comes from libyaml 0.2.5 (the reference links unsafe-libyaml 0.2.11,
+// a transpile of the same C library).
+#pragma once
+#include <string>
+#include <vector>
+
+#include "guard_types.h"
+
+namespace gg {
+
+struct DocBatch {
+  std::vector<DNode> nodes;
+  std::string bytes;
+  std::vector<uint32_t> line, col;       // per node mark (PathAwareValue location)
+  std::vector<uint32_t> kline, kcol;     // per map-entry node: its key's mark
+  std::vector<uint32_t> roots;           // per document: root node
+  std::vector<std::string> names;        // per document: data file name
+
+  size_t ndocs() const { return roots.size(); }
+  std::string path(uint32_t node) const;  // JSON pointer ("" for a root)
+  std::string path_display(uint32_t node) const;  // "{pointer}[L:{line},C:{col}]"
+  void clear();
+};
+
+enum LoadMode { LOAD_LIBYAML = 0, LOAD_SERDE = 1 };
+
+struct LoadError { std::string kind, msg; };
+
+// Appends one document; returns false and fills err on failure (batch unchanged).
+bool load_document(DocBatch& b, const char* text, size_t len, const std::string& name,
+                   LoadMode mode, LoadError& err);
+
+}  // namespace gg

@@ -1,0 +1,64 @@
+// Device-side evaluator state shared by the kernel TU and the host launcher.
+#pragma once
+#include <stdint.h>
+
+#include "guard_types.h"
+
+namespace gg {
+
+struct DevProg {
+  const PStr* strs;
+  const PPart* parts;
+  const PQuery* queries;
+  const PClause* clauses;
+  const PRange2* conjs;
+  const PRange2* disjs;
+  const uint32_t* clause_refs;
+  const uint32_t* disj_refs;
+  const PBlock* blocks;
+  const PLet* lets;
+  const PRule* rules;
+  const PRange2* name_rules;
+  const uint32_t* name_rule_ids;
+  const PFunc* funcs;
+  const PParamRule* params;
+  const uint32_t* param_vars;
+  const uint32_t* alts;
+  const PRegex* regex;
+  const uint16_t* dfa;
+  const DNode* lit_nodes;
+  const DRange* lit_ranges;
+  const char* bytes;
+  uint32_t root_block;
+  uint32_t top_first;     // first top-level rule id
+  uint32_t n_top;         // number of top-level rules
+  uint32_t n_slots;
+  uint32_t n_rules_total;
+};
+
+struct DevBatch {
+  const DNode* nodes;
+  const char* bytes;
+  const uint32_t* roots;   // per doc
+  uint32_t ndocs;
+};
+
+struct LaunchArgs {
+  DevBatch docs;
+  const DevProg* progs;    // per rules file
+  uint32_t nfiles;
+  uint32_t ntiles;         // ndocs * nfiles (tile = doc * nfiles + file)
+  uint32_t tile_base;      // first tile index of this launch
+  uint8_t* heaps;          // per wave slot scratch
+  uint32_t heap_bytes;
+  uint32_t nslots;         // number of wave slots (= grid size)
+  TileOut* tiles;          // [ntiles]
+  uint8_t* rule_status;    // [ntiles * max_top] 0 PASS 1 FAIL 2 SKIP
+  uint32_t max_top;
+  Rec* recs;               // global record arena
+  uint32_t rec_cap;
+  uint32_t* rec_cursor;    // atomic bump
+  uint32_t* tile_cursor;   // atomic work queue
+};
+
+}  // namespace gg
