@@ -1,0 +1,71 @@
+"""Builds libcfnguard_mi355x.so in-tree (hipcc, --offload-arch=gfx950).
+
+The library holds the host loader/compiler/reporter (C++) and the HIP evaluation kernel; it
+links libyaml 0.2.5 (the reference's YAML engine, via unsafe-libyaml) from /opt/conda/lib.
+"""
+import os
+import shutil
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+OUT = os.path.join(HERE, "libcfnguard_mi355x.so")
+OBJ = os.path.join(HERE, "build")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+YAML_INC = "/opt/conda/include"
+YAML_LIB = "/opt/conda/lib"
+
+HOST_SRCS = ["doc_loader.cpp", "rules_parser.cpp", "regex_dfa.cpp", "cruet.cpp", "compiler.cpp", "reporter.cpp"]
+HIP_SRCS = ["eval_kernel.hip", "capi.cpp"]
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-I" + YAML_INC, "-Wno-unused-result"]
+
+
+def _needs(src, obj, deps):
+    if not os.path.exists(obj):
+        return True
+    t = os.path.getmtime(obj)
+    return any(os.path.getmtime(d) > t for d in [src] + deps)
+
+
+def build(verbose=False):
+    os.makedirs(OBJ, exist_ok=True)
+    headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    headers.append(os.path.join(HERE, "..", "include", "cfn_guard_mi355x.h"))
+    jobs = []
+    for s in HOST_SRCS + HIP_SRCS:
+        src = os.path.join(CSRC, s)
+        obj = os.path.join(OBJ, s.replace(".cpp", ".o").replace(".hip", ".o"))
+        if _needs(src, obj, headers):
+            cmd = [HIPCC, "--offload-arch=gfx950"] + FLAGS + ["-c", src, "-o", obj]
+            jobs.append((s, cmd))
+
+    def run(job):
+        name, cmd = job
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError("compile failed: %s\n%s" % (name, r.stderr[-4000:]))
+        return name
+
+    with ThreadPoolExecutor(max_workers=min(8, max(1, len(jobs)))) as ex:
+        for name in ex.map(run, jobs):
+            if verbose:
+                print("compiled", name)
+    objs = [os.path.join(OBJ, s.replace(".cpp", ".o").replace(".hip", ".o")) for s in HOST_SRCS + HIP_SRCS]
+    if jobs or not os.path.exists(OUT):
+        # libyaml is loaded from the package directory ($ORIGIN): an rpath to /opt/conda/lib would
+        # also pull conda's older libstdc++ in front of the one libamdhip64 needs
+        local_yaml = os.path.join(HERE, "libyaml-0.so.2")
+        shutil.copyfile(os.path.join(YAML_LIB, "libyaml-0.so.2"), local_yaml)
+        cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC"] + objs + [
+            "-o", OUT, local_yaml, "-Wl,-rpath,$ORIGIN", "-lpthread"]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError("link failed:\n" + r.stderr[-4000:])
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(verbose=True))
+    sys.exit(0)

@@ -1,0 +1,548 @@
+// C ABI + HIP runtime for the MI355X evaluator.
+//
+// Drop-in boundary (guard-ffi/src/lib.rs:32-47, guard-ffi/example/cfn_guard.h):
+//   char* cfn_guard_run_checks(validate_input_t data, validate_input_t rules, _Bool verbose, extern_err_t* err)
+//   void  cfn_guard_free_string(char*)
+// plus a batched entry point (`validate --structured -o json` over many documents and rules files)
+// and a session API used by bench.py / tests (documents resident in HBM across evaluations).
+//
+// There is no CPU evaluation path: every evaluation launches guard_eval_kernel on the GPU, and the
+// library reports an explicit error when no HIP device is present.
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/cfn_guard_mi355x.h"
+#include "doc_loader.h"
+#include "eval_device.h"
+#include "program.h"
+#include "reporter.h"
+
+namespace gg {
+__global__ void guard_eval_kernel(LaunchArgs A);
+}
+
+using namespace gg;
+
+namespace {
+
+char* dup_str(const std::string& s) {
+  char* p = (char*)malloc(s.size() + 1);
+  memcpy(p, s.data(), s.size());
+  p[s.size()] = 0;
+  return p;
+}
+
+int32_t ffi_code(const std::string& kind) {
+  static const char* names[] = {"", "JsonError", "YamlError", "FormatError", "IoError", "ParseError", "RegexError",
+                                "MissingProperty", "MissingVariable", "MultipleValues", "IncompatibleRetrievalError",
+                                "IncompatibleError", "NotComparable", "ConversionError", "Errors", "RetrievalError",
+                                "MissingValue", "FileNotFoundError", "IllegalArguments"};
+  for (int i = 1; i < 19; i++) if (kind == names[i]) return i;
+  if (kind == "XMLError") return 20;
+  return -1;   // InternalError / unsupported: ffi-support's panic code
+}
+
+void set_err(extern_err_t* err, int32_t code, const std::string& msg) {
+  if (!err) return;
+  err->code = code;
+  err->message = code ? dup_str(msg) : nullptr;
+}
+
+#define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { throw std::runtime_error(std::string("HIP: ") + hipGetErrorString(e_) + " at " #x); } } while (0)
+
+struct DeviceState {
+  std::mutex mu;
+  bool ready = false;
+  int device = 0;
+  int ncu = 256;
+  std::string error;
+  hipStream_t stream = nullptr;
+  bool init(int dev) {
+    if (ready) return true;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) { error = "no HIP device available (the MI355X path has no CPU fallback)"; return false; }
+    if (dev >= n) dev = 0;
+    device = dev;
+    if (hipSetDevice(dev) != hipSuccess) { error = "hipSetDevice failed"; return false; }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) == hipSuccess) ncu = prop.multiProcessorCount;
+    hipDeviceSetLimit(hipLimitStackSize, 16384);
+    if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) { error = "stream creation failed"; return false; }
+    ready = true;
+    return true;
+  }
+};
+DeviceState g_dev;
+
+template <class T>
+struct DBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  void alloc(size_t count) {
+    release();
+    n = count;
+    if (count) HIPCHK(hipMalloc((void**)&p, count * sizeof(T)));
+  }
+  void upload(const T* src, size_t count, hipStream_t s) {
+    alloc(count);
+    if (count) HIPCHK(hipMemcpyAsync(p, src, count * sizeof(T), hipMemcpyHostToDevice, s));
+  }
+  void release() { if (p) hipFree(p); p = nullptr; n = 0; }
+  ~DBuf() { release(); }
+};
+
+struct GpuProgram {
+  Program prog;
+  DBuf<uint32_t> blob;
+  DevProg dp{};
+  void upload(hipStream_t s) {
+    blob.upload(prog.blob.data(), prog.blob.size(), s);
+    const uint32_t* b = blob.p;
+    const ProgHeader& h = prog.hdr;
+    dp.strs = (const PStr*)(b + h.off_strs);
+    dp.parts = (const PPart*)(b + h.off_parts);
+    dp.queries = (const PQuery*)(b + h.off_queries);
+    dp.clauses = (const PClause*)(b + h.off_clauses);
+    dp.conjs = (const PRange2*)(b + h.off_conjs);
+    dp.disjs = (const PRange2*)(b + h.off_disjs);
+    dp.clause_refs = b + h.off_clause_refs;
+    dp.disj_refs = b + h.off_disj_refs;
+    dp.blocks = (const PBlock*)(b + h.off_blocks);
+    dp.lets = (const PLet*)(b + h.off_lets);
+    dp.rules = (const PRule*)(b + h.off_rules);
+    dp.name_rules = (const PRange2*)(b + h.off_name_rules);
+    dp.name_rule_ids = b + h.off_name_rule_ids;
+    dp.funcs = (const PFunc*)(b + h.off_funcs);
+    dp.params = (const PParamRule*)(b + h.off_params);
+    dp.param_vars = b + h.off_param_vars;
+    dp.alts = b + h.off_alts;
+    dp.regex = (const PRegex*)(b + h.off_regex);
+    dp.dfa = (const uint16_t*)(b + h.off_dfa);
+    dp.lit_nodes = (const DNode*)(b + h.off_lit_nodes);
+    dp.lit_ranges = (const DRange*)(b + h.off_lit_ranges);
+    dp.bytes = (const char*)(b + h.off_bytes);
+    dp.root_block = h.root_block;
+    dp.top_first = prog.blob[sizeof(ProgHeader) / 4];
+    dp.n_top = prog.blob[sizeof(ProgHeader) / 4 + 1];
+    dp.n_slots = h.n_name_slots;
+    dp.n_rules_total = h.n_rules;
+  }
+};
+
+}  // namespace
+
+// ------------------------------------------------------------------ session ---
+struct gg_session {
+  DocBatch docs;
+  std::vector<std::unique_ptr<GpuProgram>> progs;
+  std::vector<std::string> parse_errors;   // rules files that failed to parse (exit code 5)
+  // device residency
+  DBuf<DNode> d_nodes;
+  DBuf<char> d_bytes;
+  DBuf<uint32_t> d_roots;
+  DBuf<DevProg> d_progs;
+  DBuf<uint8_t> d_heaps;
+  DBuf<TileOut> d_tiles;
+  DBuf<uint8_t> d_rule_status;
+  DBuf<Rec> d_recs;
+  DBuf<uint32_t> d_counters;
+  bool uploaded = false;
+  uint32_t max_top = 1;
+  uint32_t nslots = 0;
+  uint32_t heap_bytes = 512 * 1024;
+  size_t rec_cap = 0;
+  // results
+  std::vector<TileOut> tiles;
+  std::vector<uint8_t> rule_status;
+  std::vector<Rec> recs;
+  bool evaluated = false;
+  double last_kernel_ms = 0;
+  std::string last_error;
+};
+
+namespace {
+
+bool ensure_device(std::string& why) {
+  std::lock_guard<std::mutex> lk(g_dev.mu);
+  if (!g_dev.init(0)) { why = g_dev.error; return false; }
+  return true;
+}
+
+void session_upload(gg_session* s) {
+  hipStream_t st = g_dev.stream;
+  s->d_nodes.upload(s->docs.nodes.data(), s->docs.nodes.size(), st);
+  s->d_bytes.upload(s->docs.bytes.data(), s->docs.bytes.size() ? s->docs.bytes.size() : 1, st);
+  s->d_roots.upload(s->docs.roots.data(), s->docs.roots.size(), st);
+  std::vector<DevProg> dps;
+  s->max_top = 1;
+  for (auto& p : s->progs) {
+    p->upload(st);
+    dps.push_back(p->dp);
+    s->max_top = std::max<uint32_t>(s->max_top, p->dp.n_top);
+  }
+  s->d_progs.upload(dps.data(), dps.size(), st);
+  size_t ntiles = s->docs.ndocs() * s->progs.size();
+  uint32_t slots = (uint32_t)std::min<size_t>(std::max<size_t>(ntiles, 1), (size_t)g_dev.ncu * 8);
+  s->nslots = slots;
+  s->d_heaps.alloc((size_t)slots * s->heap_bytes);
+  s->d_tiles.alloc(std::max<size_t>(ntiles, 1));
+  s->d_rule_status.alloc(std::max<size_t>(ntiles * s->max_top, 1));
+  s->rec_cap = std::min<size_t>(std::max<size_t>(ntiles * 48, 4096), (size_t)96 * 1024 * 1024);
+  s->d_recs.alloc(s->rec_cap);
+  s->d_counters.alloc(16);
+  HIPCHK(hipStreamSynchronize(st));
+  s->uploaded = true;
+}
+
+// runs the kernel over all tiles; returns kernel milliseconds (HIP events on the launch stream)
+double session_run(gg_session* s, bool fetch) {
+  hipStream_t st = g_dev.stream;
+  uint32_t ntiles = (uint32_t)(s->docs.ndocs() * s->progs.size());
+  HIPCHK(hipMemsetAsync(s->d_counters.p, 0, 16 * sizeof(uint32_t), st));
+  LaunchArgs A{};
+  A.docs.nodes = s->d_nodes.p; A.docs.bytes = s->d_bytes.p; A.docs.roots = s->d_roots.p; A.docs.ndocs = (uint32_t)s->docs.ndocs();
+  A.progs = s->d_progs.p; A.nfiles = (uint32_t)s->progs.size();
+  A.ntiles = ntiles; A.tile_base = 0;
+  A.heaps = s->d_heaps.p; A.heap_bytes = s->heap_bytes; A.nslots = s->nslots;
+  A.tiles = s->d_tiles.p; A.rule_status = s->d_rule_status.p; A.max_top = s->max_top;
+  A.recs = s->d_recs.p; A.rec_cap = (uint32_t)s->rec_cap;
+  A.rec_cursor = s->d_counters.p; A.tile_cursor = s->d_counters.p + 1;
+  hipEvent_t e0, e1;
+  HIPCHK(hipEventCreate(&e0));
+  HIPCHK(hipEventCreate(&e1));
+  HIPCHK(hipEventRecord(e0, st));
+  if (ntiles) hipLaunchKernelGGL(guard_eval_kernel, dim3(s->nslots), dim3(64), 0, st, A);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(e1, st));
+  HIPCHK(hipEventSynchronize(e1));
+  float ms = 0;
+  HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  s->last_kernel_ms = ms;
+  if (fetch) {
+    s->tiles.resize(ntiles);
+    s->rule_status.resize((size_t)ntiles * s->max_top);
+    uint32_t nrec = 0;
+    HIPCHK(hipMemcpy(&nrec, s->d_counters.p, 4, hipMemcpyDeviceToHost));
+    if (nrec > s->rec_cap) nrec = (uint32_t)s->rec_cap;
+    s->recs.resize(nrec);
+    if (ntiles) {
+      HIPCHK(hipMemcpy(s->tiles.data(), s->d_tiles.p, ntiles * sizeof(TileOut), hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(s->rule_status.data(), s->d_rule_status.p, s->rule_status.size(), hipMemcpyDeviceToHost));
+    }
+    if (nrec) HIPCHK(hipMemcpy(s->recs.data(), s->d_recs.p, nrec * sizeof(Rec), hipMemcpyDeviceToHost));
+    s->evaluated = true;
+  }
+  return ms;
+}
+
+// structured JSON over (docs x programs); returns false + err for an aborting error
+bool session_report(gg_session* s, std::string& out, int32_t& exit_code, ReportError& err) {
+  exit_code = s->parse_errors.empty() ? 0 : 5;
+  std::vector<const Program*> progs;
+  for (auto& p : s->progs) progs.push_back(&p->prog);
+  size_t nf = progs.size();
+  // the first tile in (doc, rules-file) order that raised an error aborts the run (structured.rs:110)
+  for (size_t t = 0; t < s->tiles.size(); t++) {
+    if (s->tiles[t].err) {
+      tile_error(s->docs, *progs[t % nf], s->tiles[t], err);
+      exit_code = -1;
+      return false;
+    }
+  }
+  out.clear();
+  size_t nd = s->docs.ndocs();
+  if (nd == 0) { out = "[]"; return true; }
+  out += "[\n";
+  std::vector<TileResult> trs(nf);
+  for (size_t d = 0; d < nd; d++) {
+    std::vector<const TileResult*> tp;
+    for (size_t f = 0; f < nf; f++) {
+      size_t t = d * nf + f;
+      TileResult& tr = trs[f];
+      tr.out = s->tiles[t];
+      tr.rule_status.assign(s->rule_status.begin() + t * s->max_top, s->rule_status.begin() + t * s->max_top + s->max_top);
+      tr.recs.assign(s->recs.begin() + tr.out.rec_off, s->recs.begin() + tr.out.rec_off + tr.out.rec_n);
+      if (tr.out.status == ST_FAIL) exit_code = exit_code == 5 ? 5 : 19;
+      tp.push_back(&tr);
+    }
+    out.append(2, ' ');
+    if (!report_document(s->docs, (uint32_t)d, progs, tp, 1, out, err)) { exit_code = -1; return false; }
+    if (d + 1 < nd) out += ",";
+    out += "\n";
+  }
+  out += "]";
+  // validate.rs: exit code 19 when any rules file FAILed (structured.rs:110-112), 5 on parse errors
+  if (exit_code != 5) {
+    bool anyfail = false;
+    for (auto& t : s->tiles) if (t.status == ST_FAIL) anyfail = true;
+    exit_code = anyfail ? 19 : 0;
+  } else {
+    // parse error keeps exit code 5 unless a FAIL overrides it (StructuredReporter sets 19)
+    for (auto& t : s->tiles) if (t.status == ST_FAIL) exit_code = 19;
+  }
+  return true;
+}
+
+void merge_batch(DocBatch& dst, const DocBatch& src) {
+  uint32_t nbase = (uint32_t)dst.nodes.size();
+  uint32_t bbase = (uint32_t)dst.bytes.size();
+  dst.bytes += src.bytes;
+  for (size_t i = 0; i < src.nodes.size(); i++) {
+    DNode n = src.nodes[i];
+    if (n.kind == K_LIST || n.kind == K_MAP) n.a += nbase;
+    else if (n.kind == K_STRING) n.a += bbase;
+    if (n.key_off != NONE) n.key_off += bbase;
+    if (n.parent != NONE) n.parent += nbase;
+    dst.nodes.push_back(n);
+  }
+  dst.line.insert(dst.line.end(), src.line.begin(), src.line.end());
+  dst.col.insert(dst.col.end(), src.col.begin(), src.col.end());
+  dst.kline.insert(dst.kline.end(), src.kline.begin(), src.kline.end());
+  dst.kcol.insert(dst.kcol.end(), src.kcol.begin(), src.kcol.end());
+  for (uint32_t r : src.roots) dst.roots.push_back(r + nbase);
+  dst.names.insert(dst.names.end(), src.names.begin(), src.names.end());
+}
+
+bool add_rules(gg_session* s, const std::string& text, const std::string& name, std::string& perr) {
+  RulesFile rf;
+  bool empty = false;
+  std::string msg;
+  if (!parse_rules_file(text, name, rf, empty, msg)) { perr = msg; return false; }
+  if (empty) return true;
+  auto gp = std::make_unique<GpuProgram>();
+  std::string cerr;
+  if (!compile_program(rf, name, gp->prog, cerr)) { perr = cerr; return false; }
+  s->progs.push_back(std::move(gp));
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+void cfn_guard_free_string(char* s) { free(s); }
+
+char* cfn_guard_run_checks(validate_input_t data, validate_input_t rules, bool verbose, extern_err_t* err) {
+  set_err(err, 0, "");
+  if (verbose) {
+    set_err(err, -1, "unsupported on MI355X path: verbose EventRecord tree output (SURVEY.md 8f row 4)");
+    return nullptr;
+  }
+  try {
+    std::string why;
+    if (!ensure_device(why)) { set_err(err, -1, why); return nullptr; }
+    gg_session s;
+    std::string dname = data.file_name ? data.file_name : "";
+    LoadError le;
+    const char* text = data.content ? data.content : "";
+    if (!load_document(s.docs, text, strlen(text), dname, LOAD_SERDE, le)) {
+      if (le.kind == "YamlError") set_err(err, 2, error_display("YamlError", le.msg));
+      else set_err(err, 5, error_display("ParseError", "Unable to process data in file " + dname + ", Error " + error_display(le.kind, le.msg) + ","));
+      return nullptr;
+    }
+    std::string rname = rules.file_name ? rules.file_name : "";
+    std::string perr;
+    const char* rtext = rules.content ? rules.content : "";
+    RulesFile rf;
+    bool empty = false;
+    if (!parse_rules_file(rtext, rname, rf, empty, perr)) { set_err(err, 5, error_display("ParseError", perr)); return nullptr; }
+    if (empty) return dup_str("");
+    auto gp = std::make_unique<GpuProgram>();
+    if (!compile_program(rf, rname, gp->prog, perr)) { set_err(err, 5, error_display("ParseError", perr)); return nullptr; }
+    s.progs.push_back(std::move(gp));
+    session_upload(&s);
+    session_run(&s, true);
+    if (s.tiles[0].err) {
+      ReportError re;
+      tile_error(s.docs, s.progs[0]->prog, s.tiles[0], re);
+      set_err(err, ffi_code(re.kind), error_display(re.kind, re.msg));
+      return nullptr;
+    }
+    TileResult tr;
+    tr.out = s.tiles[0];
+    tr.rule_status.assign(s.rule_status.begin(), s.rule_status.begin() + s.max_top);
+    tr.recs.assign(s.recs.begin() + tr.out.rec_off, s.recs.begin() + tr.out.rec_off + tr.out.rec_n);
+    std::string out;
+    ReportError re;
+    std::vector<const Program*> progs{&s.progs[0]->prog};
+    std::vector<const TileResult*> tp{&tr};
+    if (!report_document(s.docs, 0, progs, tp, 0, out, re)) {
+      set_err(err, ffi_code(re.kind), error_display(re.kind, re.msg));
+      return nullptr;
+    }
+    return dup_str(out);
+  } catch (std::exception& e) {
+    set_err(err, -1, e.what());
+    return nullptr;
+  }
+}
+
+char* cfn_guard_validate_batch(const validate_input_t* docs, size_t n_docs, const validate_input_t* rules, size_t n_rules,
+                               int32_t* exit_code, extern_err_t* err) {
+  set_err(err, 0, "");
+  if (exit_code) *exit_code = 0;
+  try {
+    std::string why;
+    if (!ensure_device(why)) { set_err(err, -1, why); if (exit_code) *exit_code = -1; return nullptr; }
+    gg_session s;
+    for (size_t i = 0; i < n_rules; i++) {
+      std::string perr;
+      std::string name = rules[i].file_name ? rules[i].file_name : "";
+      if (!add_rules(&s, rules[i].content ? rules[i].content : "", name, perr))
+        s.parse_errors.push_back("Parsing error handling rule file = " + name + ", Error = " + error_display("ParseError", perr) + "\n---");
+    }
+    for (size_t i = 0; i < n_docs; i++) {
+      LoadError le;
+      const char* t = docs[i].content ? docs[i].content : "";
+      if (!load_document(s.docs, t, strlen(t), docs[i].file_name ? docs[i].file_name : "", LOAD_LIBYAML, le)) {
+        set_err(err, ffi_code(le.kind), error_display(le.kind, le.msg));
+        if (exit_code) *exit_code = -1;
+        return nullptr;
+      }
+    }
+    session_upload(&s);
+    session_run(&s, true);
+    std::string out;
+    int32_t code = 0;
+    ReportError re;
+    if (!session_report(&s, out, code, re)) {
+      set_err(err, ffi_code(re.kind), error_display(re.kind, re.msg));
+      if (exit_code) *exit_code = -1;
+      return nullptr;
+    }
+    if (exit_code) *exit_code = code;
+    return dup_str(out);
+  } catch (std::exception& e) {
+    set_err(err, -1, e.what());
+    if (exit_code) *exit_code = -1;
+    return nullptr;
+  }
+}
+
+// ------------------------------------------------------------- session API ---
+gg_session* gg_session_new(void) { return new gg_session(); }
+void gg_session_free(gg_session* s) { delete s; }
+
+int32_t gg_session_add_rules(gg_session* s, const char* text, const char* name, extern_err_t* err) {
+  set_err(err, 0, "");
+  std::string perr;
+  if (!add_rules(s, text ? text : "", name ? name : "", perr)) {
+    s->parse_errors.push_back(perr);
+    set_err(err, 5, error_display("ParseError", perr));
+    return 5;
+  }
+  s->uploaded = false;
+  return 0;
+}
+
+int32_t gg_session_add_docs(gg_session* s, const char* const* texts, const size_t* lens, const char* const* names, size_t n,
+                            int32_t mode, int32_t nthreads, extern_err_t* err) {
+  set_err(err, 0, "");
+  if (nthreads < 1) nthreads = 1;
+  std::vector<DocBatch> parts(nthreads);
+  std::vector<LoadError> errs(nthreads);
+  std::vector<int> failed(nthreads, -1);
+  auto work = [&](int t) {
+    size_t lo = n * t / nthreads, hi = n * (t + 1) / nthreads;
+    for (size_t i = lo; i < hi; i++) {
+      if (!load_document(parts[t], texts[i], lens[i], names ? names[i] : std::string(), (LoadMode)mode, errs[t])) { failed[t] = (int)i; return; }
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 0; t < nthreads; t++) th.emplace_back(work, t);
+  for (auto& x : th) x.join();
+  for (int t = 0; t < nthreads; t++) {
+    if (failed[t] >= 0) { set_err(err, ffi_code(errs[t].kind), error_display(errs[t].kind, errs[t].msg)); return 5; }
+  }
+  for (int t = 0; t < nthreads; t++) merge_batch(s->docs, parts[t]);
+  s->uploaded = false;
+  return 0;
+}
+
+int32_t gg_session_upload(gg_session* s, extern_err_t* err) {
+  set_err(err, 0, "");
+  try {
+    std::string why;
+    if (!ensure_device(why)) { set_err(err, -1, why); return -1; }
+    session_upload(s);
+    return 0;
+  } catch (std::exception& e) { set_err(err, -1, e.what()); return -1; }
+}
+
+// Runs `iters` evaluations of every (doc, rules-file) tile; fills per-iteration kernel ms.
+int32_t gg_session_eval(gg_session* s, int32_t iters, double* ms_out, extern_err_t* err) {
+  set_err(err, 0, "");
+  try {
+    std::string why;
+    if (!ensure_device(why)) { set_err(err, -1, why); return -1; }
+    if (!s->uploaded) session_upload(s);
+    for (int32_t i = 0; i < iters; i++) {
+      double ms = session_run(s, i == iters - 1);
+      if (ms_out) ms_out[i] = ms;
+    }
+    return 0;
+  } catch (std::exception& e) { set_err(err, -1, e.what()); return -1; }
+}
+
+char* gg_session_report(gg_session* s, int32_t* exit_code, extern_err_t* err) {
+  set_err(err, 0, "");
+  if (!s->evaluated) { set_err(err, -1, "session not evaluated"); return nullptr; }
+  std::string out;
+  int32_t code = 0;
+  ReportError re;
+  if (!session_report(s, out, code, re)) {
+    if (exit_code) *exit_code = -1;
+    set_err(err, ffi_code(re.kind), error_display(re.kind, re.msg));
+    return nullptr;
+  }
+  if (exit_code) *exit_code = code;
+  return dup_str(out);
+}
+
+// statistics: 0 ndocs, 1 nfiles, 2 nodes, 3 string bytes, 4 tiles FAIL, 5 tiles PASS, 6 tiles SKIP,
+// 7 tiles with error, 8 records, 9 device arena bytes (nodes + strings + roots), 10 first error code
+int64_t gg_session_stat(gg_session* s, int32_t what) {
+  switch (what) {
+    case 0: return (int64_t)s->docs.ndocs();
+    case 1: return (int64_t)s->progs.size();
+    case 2: return (int64_t)s->docs.nodes.size();
+    case 3: return (int64_t)s->docs.bytes.size();
+    case 4: case 5: case 6: {
+      uint32_t want = what == 4 ? ST_FAIL : what == 5 ? ST_PASS : ST_SKIP;
+      int64_t c = 0;
+      for (auto& t : s->tiles) if (!t.err && t.status == want) c++;
+      return c;
+    }
+    case 7: { int64_t c = 0; for (auto& t : s->tiles) if (t.err) c++; return c; }
+    case 8: return (int64_t)s->recs.size();
+    case 9: return (int64_t)(s->docs.nodes.size() * sizeof(DNode) + s->docs.bytes.size() + s->docs.roots.size() * 4);
+    case 10: for (auto& t : s->tiles) if (t.err) return t.err; return 0;
+    default: return -1;
+  }
+}
+
+// per-tile status (0 PASS 1 FAIL 2 SKIP, 3 error) into out[ndocs * nfiles]
+int32_t gg_session_tile_status(gg_session* s, uint8_t* out, size_t n) {
+  for (size_t i = 0; i < n && i < s->tiles.size(); i++) out[i] = s->tiles[i].err ? 3 : (uint8_t)s->tiles[i].status;
+  return 0;
+}
+
+double gg_session_last_kernel_ms(gg_session* s) { return s->last_kernel_ms; }
+
+int32_t gg_device_available(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+}  // extern "C"

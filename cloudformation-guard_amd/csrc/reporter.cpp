@@ -1,0 +1,623 @@
+// Device records -> structured JSON (see reporter.h).
+#include "reporter.h"
+
+#include <algorithm>
+#include <cstring>
+#include <set>
+
+#include "host_format.h"
+
+namespace gg {
+
+namespace {
+
+struct J {
+  enum T { Null, Bool, Raw, Str, Arr, Obj } t = Null;
+  std::string s;
+  bool b = false;
+  std::vector<J> a;
+  std::vector<std::pair<std::string, J>> o;
+  static J null() { return J(); }
+  static J str(const std::string& v) { J j; j.t = Str; j.s = v; return j; }
+  static J raw(const std::string& v) { J j; j.t = Raw; j.s = v; return j; }
+  static J boolean(bool v) { J j; j.t = Bool; j.b = v; return j; }
+  static J arr() { J j; j.t = Arr; return j; }
+  static J obj() { J j; j.t = Obj; return j; }
+  J& add(const std::string& k, J v) { o.push_back({k, std::move(v)}); return *this; }
+  J& push(J v) { a.push_back(std::move(v)); return *this; }
+};
+
+void pretty(const J& j, int indent, std::string& out) {
+  switch (j.t) {
+    case J::Null: out += "null"; return;
+    case J::Bool: out += j.b ? "true" : "false"; return;
+    case J::Raw: out += j.s; return;
+    case J::Str: json_escape_into(out, j.s.data(), j.s.size()); return;
+    case J::Arr: {
+      if (j.a.empty()) { out += "[]"; return; }
+      out += "[\n";
+      for (size_t i = 0; i < j.a.size(); i++) {
+        out.append((indent + 1) * 2, ' ');
+        pretty(j.a[i], indent + 1, out);
+        if (i + 1 < j.a.size()) out += ",";
+        out += "\n";
+      }
+      out.append(indent * 2, ' ');
+      out += "]";
+      return;
+    }
+    case J::Obj: {
+      if (j.o.empty()) { out += "{}"; return; }
+      out += "{\n";
+      for (size_t i = 0; i < j.o.size(); i++) {
+        out.append((indent + 1) * 2, ' ');
+        json_escape_into(out, j.o[i].first.data(), j.o[i].first.size());
+        out += ": ";
+        pretty(j.o[i].second, indent + 1, out);
+        if (i + 1 < j.o.size()) out += ",";
+        out += "\n";
+      }
+      out.append(indent * 2, ' ');
+      out += "}";
+      return;
+    }
+  }
+}
+
+const char* type_info(uint32_t k) {
+  switch (k) {
+    case K_NULL: return "null";
+    case K_STRING: return "String";
+    case K_REGEX: return "Regex";
+    case K_BOOL: return "bool";
+    case K_INT: return "int";
+    case K_FLOAT: return "float";
+    case K_CHAR: return "char";
+    case K_LIST: return "array";
+    case K_MAP: return "map";
+    case K_RANGE_INT: return "range(int, int)";
+    case K_RANGE_FLOAT: return "range(float, float)";
+    default: return "range(char, char)";
+  }
+}
+
+struct Fatal { std::string kind, msg; };
+
+struct R {
+  const DocBatch& docs;
+  const Program& prog;
+  bool serde;
+
+  const DocBatch& B(uint32_t ref) const { return (ref & LIT_BIT) ? prog.lit : docs; }
+  uint32_t I(uint32_t ref) const { return ref & ~LIT_BIT; }
+  const DNode& N(uint32_t ref) const { return B(ref).nodes[I(ref)]; }
+  std::string str(uint32_t ref) const { const DNode& n = N(ref); return B(ref).bytes.substr(n.a, n.count); }
+  std::string key(uint32_t ref) const { const DNode& n = N(ref); return B(ref).bytes.substr(n.key_off, n.key_len); }
+  uint32_t child(uint32_t ref, uint32_t j) const { return (ref & LIT_BIT) | (N(ref).a + j); }
+  std::string path(uint32_t ref) const { return B(ref).path(I(ref)); }
+  uint32_t line(uint32_t ref) const { return B(ref).line[I(ref)]; }
+  uint32_t col(uint32_t ref) const { return B(ref).col[I(ref)]; }
+  std::string loc(uint32_t l, uint32_t c) const { return "[L:" + std::to_string(l) + ",C:" + std::to_string(c) + "]"; }
+  std::string path_display(uint32_t ref) const { return path(ref) + loc(line(ref), col(ref)); }
+  int64_t ival(const DNode& n) const { return (int64_t)(((uint64_t)n.b << 32) | n.a); }
+  double fval(const DNode& n) const { uint64_t u = ((uint64_t)n.b << 32) | n.a; double d; memcpy(&d, &u, 8); return d; }
+
+  std::string range_str(const DNode& n) const {
+    const DRange& r = prog.ranges[n.a];
+    std::string lo, hi;
+    if (n.kind == K_RANGE_INT) { lo = std::to_string((int64_t)r.lo); hi = std::to_string((int64_t)r.hi); }
+    else if (n.kind == K_RANGE_FLOAT) { double a, b; memcpy(&a, &r.lo, 8); memcpy(&b, &r.hi, 8); lo = rust_display_f64(a); hi = rust_display_f64(b); }
+    else { utf8_append(lo, (uint32_t)r.lo); utf8_append(hi, (uint32_t)r.hi); }
+    return std::string(r.incl & 1 ? "[" : "(") + lo + "," + hi + (r.incl & 2 ? "]" : ")");
+  }
+
+  J value_json(uint32_t ref) const {
+    const DNode& n = N(ref);
+    switch (n.kind) {
+      case K_NULL: return J::null();
+      case K_STRING: return J::str(str(ref));
+      case K_REGEX: return J::str("/" + str(ref) + "/");
+      case K_BOOL: return J::boolean(n.a != 0);
+      case K_INT: return J::raw(std::to_string(ival(n)));
+      case K_FLOAT: {
+        double d = fval(n);
+        if (std::isnan(d) || std::isinf(d))
+          throw Fatal{"IncompatibleError", "Could not convert float " + rust_display_f64(d) + " to serde::Value::Number"};
+        return J::raw(ryu_f64(d));
+      }
+      case K_CHAR: { std::string s; utf8_append(s, n.a); return J::str(s); }
+      case K_LIST: { J a = J::arr(); for (uint32_t j = 0; j < n.count; j++) a.push(value_json(child(ref, j))); return a; }
+      case K_MAP: { J o = J::obj(); for (uint32_t j = 0; j < n.count; j++) { uint32_t c = child(ref, j); o.add(key(c), value_json(c)); } return o; }
+      default: return J::str(range_str(n));
+    }
+  }
+
+  std::string value_only(uint32_t ref) const {
+    const DNode& n = N(ref);
+    switch (n.kind) {
+      case K_NULL: return "\"NULL\"";
+      case K_STRING: return "\"" + str(ref) + "\"";
+      case K_REGEX: return "\"/" + str(ref) + "/\"";
+      case K_BOOL: return n.a ? "true" : "false";
+      case K_INT: return std::to_string(ival(n));
+      case K_FLOAT: return rust_display_f64(fval(n));
+      case K_CHAR: { std::string s = "'"; utf8_append(s, n.a); return s + "'"; }
+      case K_LIST: {
+        std::string s = "[";
+        for (uint32_t j = 0; j < n.count; j++) { if (j) s += ","; s += value_only(child(ref, j)); }
+        return s + "]";
+      }
+      case K_MAP: {
+        std::string s = "{";
+        for (uint32_t j = 0; j < n.count; j++) { if (j) s += ","; uint32_t c = child(ref, j); s += "\"" + key(c) + "\":" + value_only(c); }
+        return s + "}";
+      }
+      default: return range_str(n);
+    }
+  }
+
+  std::string dbg_path(const std::string& p, uint32_t l, uint32_t c) const {
+    return "Path(" + rust_debug_str(p) + ", Location { line: " + std::to_string(l) + ", col: " + std::to_string(c) + " })";
+  }
+
+  std::string debug(uint32_t ref) const {
+    const DNode& n = N(ref);
+    std::string p = dbg_path(path(ref), line(ref), col(ref));
+    switch (n.kind) {
+      case K_NULL: return "Null(" + p + ")";
+      case K_STRING: return "String((" + p + ", " + rust_debug_str(str(ref)) + "))";
+      case K_REGEX: return "Regex((" + p + ", " + rust_debug_str(str(ref)) + "))";
+      case K_BOOL: return std::string("Bool((") + p + ", " + (n.a ? "true" : "false") + "))";
+      case K_INT: return "Int((" + p + ", " + std::to_string(ival(n)) + "))";
+      case K_FLOAT: return "Float((" + p + ", " + rust_debug_f64(fval(n)) + "))";
+      case K_CHAR: { std::string s; utf8_append(s, n.a); return "Char((" + p + ", '" + s + "'))"; }
+      case K_LIST: {
+        std::string s = "List((" + p + ", [";
+        for (uint32_t j = 0; j < n.count; j++) { if (j) s += ", "; s += debug(child(ref, j)); }
+        return s + "]))";
+      }
+      case K_MAP: {
+        std::string keys, vals;
+        std::string mp = path(ref);
+        for (uint32_t j = 0; j < n.count; j++) {
+          uint32_t c = child(ref, j);
+          std::string k = key(c);
+          if (j) { keys += ", "; vals += ", "; }
+          // MapValue.keys: libyaml mode -> parent path at the key mark; serde mode -> path/key at L0,C0
+          bool lit = (ref & LIT_BIT) != 0;
+          if (serde || lit) keys += "String((" + dbg_path(mp + "/" + k, 0, 0) + ", " + rust_debug_str(k) + "))";
+          else keys += "String((" + dbg_path(mp, B(c).kline[I(c)], B(c).kcol[I(c)]) + ", " + rust_debug_str(k) + "))";
+          vals += rust_debug_str(k) + ": " + debug(c);
+        }
+        return "Map((" + p + ", MapValue { keys: [" + keys + "], values: {" + vals + "} }))";
+      }
+      default: {
+        const DRange& r = prog.ranges[n.a];
+        std::string lo, hi;
+        const char* nm = n.kind == K_RANGE_INT ? "RangeInt" : n.kind == K_RANGE_FLOAT ? "RangeFloat" : "RangeChar";
+        if (n.kind == K_RANGE_INT) { lo = std::to_string((int64_t)r.lo); hi = std::to_string((int64_t)r.hi); }
+        else if (n.kind == K_RANGE_FLOAT) { double a, b; memcpy(&a, &r.lo, 8); memcpy(&b, &r.hi, 8); lo = rust_debug_f64(a); hi = rust_debug_f64(b); }
+        else { std::string a, b; utf8_append(a, (uint32_t)r.lo); utf8_append(b, (uint32_t)r.hi); lo = "'" + a + "'"; hi = "'" + b + "'"; }
+        return std::string(nm) + "((" + p + ", RangeType { upper: " + hi + ", lower: " + lo + ", inclusive: " + std::to_string(r.incl) + " }))";
+      }
+    }
+  }
+
+  // QR helpers ------------------------------------------------------------
+  bool is_synth(const QR& q) const { return (q.meta & 3u) == QR_SYNTH_INT; }
+  std::string q_path(const QR& q) const { return is_synth(q) ? (q.node == NONE ? "" : path(q.node)) : path(q.node); }
+  std::string q_path_display(const QR& q) const {
+    if (is_synth(q)) return q.node == NONE ? "[L:0,C:0]" : path_display(q.node);
+    return path_display(q.node);
+  }
+  int64_t synth_val(const QR& q) const { return (int64_t)(((uint64_t)q.aux << 32) | q.uref); }
+  J pav_json(const QR& q) const {
+    J o = J::obj();
+    o.add("path", J::str(q_path(q)));
+    o.add("value", is_synth(q) ? J::raw(std::to_string(synth_val(q))) : value_json(q.node));
+    return o;
+  }
+  std::string pav_display(const QR& q) const {
+    if (is_synth(q)) return "Path=" + q_path_display(q) + " Value=" + std::to_string(synth_val(q));
+    return "Path=" + path_display(q.node) + " Value=" + value_only(q.node);
+  }
+
+  std::string reason(const QR& q) const {
+    uint32_t code = (q.meta >> 8) & 0xFF;
+    uint32_t qid = q.uref >> 12;
+    uint32_t step = q.uref & 0xFFF;
+    uint32_t cur = q.node;
+    const auto& parts = prog.queries[qid];
+    const DNode& n = N(cur);
+    switch (code) {
+      case R_INDEX_OOB: {
+        std::string els;
+        for (uint32_t j = 0; j < n.count; j++) { if (j) els += ", "; els += debug(child(cur, j)); }
+        return "Array Index out of bounds for path = " + path_display(cur) + " on index = " + std::to_string((int32_t)q.aux) +
+               " inside Array = [" + els + "], remaining query = " + slice_display(parts, 0);
+      }
+      case R_NO_MORE_ENTRIES:
+        return "No more entries for value at path = " + path_display(cur) + " on type = " + type_info(n.kind) + " ";
+      case R_KEY_INDEX_NOT_ARRAY:
+        return "Attempting to retrieve from index " + std::to_string((int32_t)q.aux) + " but type is not an array at path " + path_display(cur);
+      case R_LOCATE_KEY:
+        return "Could not locate key = " + str(q.aux) + " inside struct at path = " + path_display(cur);
+      case R_LOCATE_KEY_LIST:
+        return "Could not locate key = " + str(q.aux) + " inside struct at path = " + path_display(q.aux);
+      case R_KEY_NOT_FOUND:
+        return "Could not find key " + parts[step].key + " inside struct at path " + path_display(cur);
+      case R_NOT_STRUCT:
+        return "Attempting to retrieve from key " + parts[step].key + " but type is not an struct type at path " +
+               path_display(cur) + ", Type = " + type_info(n.kind) + ", Value = " + debug(cur);
+      case R_INDEX_NOT_ARRAY:
+        return "Attempting to retrieve from index " + std::to_string(parts[step].index) + " but type is not an array at path " +
+               path_display(cur) + ", type " + type_info(n.kind);
+      case R_FILTER_NOT_STRUCT:
+        return std::string("Filter on value type that was not a struct or array ") + type_info(n.kind) + " " + path_display(cur);
+      default:
+        return "";
+    }
+  }
+  std::string remaining(const QR& q) const { return prog.query_remaining(q.uref >> 12, q.uref & 0xFFF); }
+
+  J unresolved_json(const QR& q) const {
+    J o = J::obj();
+    J t = J::obj();
+    t.add("path", J::str(path(q.node)));
+    t.add("value", value_json(q.node));
+    o.add("traversed_to", t);
+    o.add("remaining_query", J::str(remaining(q)));
+    o.add("reason", J::str(reason(q)));
+    return o;
+  }
+  std::string unresolved_display(const QR& q) const { return "Path=" + path_display(q.node) + " Value=" + value_only(q.node); }
+
+  static J messages(const J& custom, const J& error) {
+    J m = J::obj(); m.add("custom_message", custom); m.add("error_message", error); return m;
+  }
+  J comparison(uint32_t op, bool neg) const {
+    static const char* names[] = {"Eq", "In", "Gt", "Lt", "Le", "Ge", "Exists", "Empty", "IsString", "IsList", "IsMap",
+                                  "IsBool", "IsInt", "IsFloat", "IsNull"};
+    J a = J::arr(); a.push(J::str(names[op])); a.push(J::boolean(neg)); return a;
+  }
+  std::string custom(const PClause& pc) const { return pc.e == NONE ? "" : prog.msgs[pc.e]; }
+  J custom_opt(const PClause& pc) const { return pc.e == NONE ? J::null() : J::str(prog.msgs[pc.e]); }
+};
+
+const char* unary_msg(uint32_t op, bool neg) {
+  switch (op) {
+    case OP_EXISTS: return neg ? "existed" : "did not exist";
+    case OP_EMPTY: return neg ? "was empty" : "was not empty";
+    case OP_IS_LIST: return neg ? "was a list " : "was not list";
+    case OP_IS_MAP: return neg ? "was a struct" : "was not struct";
+    case OP_IS_STRING: return neg ? "was a string " : "was not string";
+    case OP_IS_INT: return neg ? "was int" : "was not int";
+    case OP_IS_BOOL: return neg ? "was bool" : "was not bool";
+    case OP_IS_NULL: return neg ? "was null" : "was not null";
+    default: return neg ? "was float" : "was not float";
+  }
+}
+
+const char* op_msg(uint32_t op, bool neg) {
+  switch (op) {
+    case OP_EQ: return neg ? "equal to" : "not equal to";
+    case OP_LE: return neg ? "less than equal to" : "not less than equal to";
+    case OP_LT: return neg ? "less than" : "not less than";
+    case OP_GE: return neg ? "greater than equal to" : "not greater than equal";
+    case OP_GT: return neg ? "greater than" : "not greater than";
+    default: return neg ? "in" : "not in";
+  }
+}
+
+struct Walker {
+  const R& r;
+  const std::vector<Rec>& recs;
+  size_t i = 0;
+
+  J clause_wrap(const char* kind, J inner) {
+    J o = J::obj(); o.add(kind, std::move(inner)); return o;
+  }
+
+  // parse records until a closing record (or end); returns list of ClauseReport JSON
+  J items(uint32_t close_kind) {
+    J list = J::arr();
+    while (i < recs.size()) {
+      const Rec& rc = recs[i];
+      if (rc.kind == close_kind) { i++; return list; }
+      i++;
+      switch (rc.kind) {
+        case REC_RULE_OPEN: {
+          J checks = items(REC_RULE_CLOSE);
+          J rule = J::obj();
+          rule.add("name", J::str(r.prog.rule_names[rc.clause]));
+          rule.add("metadata", J::obj());
+          rule.add("messages", R::messages(rc.x == NONE ? J::null() : J::str(r.prog.msgs[rc.x]), J::null()));
+          rule.add("checks", std::move(checks));
+          list.push(clause_wrap("Rule", std::move(rule)));
+          break;
+        }
+        case REC_DISJ_OPEN: {
+          J checks = items(REC_DISJ_CLOSE);
+          J d = J::obj(); d.add("checks", std::move(checks));
+          list.push(clause_wrap("Disjunctions", std::move(d)));
+          break;
+        }
+        case REC_BLOCK_EMPTY: {
+          const PClause& pc = r.prog.clauses[rc.clause];
+          J b = J::obj();
+          b.add("context", J::str(r.prog.ctx[pc.d]));
+          b.add("messages", R::messages(J::null(), J::str("query for block clause did not retrieve any value")));
+          b.add("unresolved", J::null());
+          list.push(clause_wrap("Block", std::move(b)));
+          break;
+        }
+        case REC_MISSING_BLOCK_VALUE: {
+          const PClause& pc = r.prog.clauses[rc.clause];
+          std::string err = "Check was not compliant as property [" + r.remaining(rc.from) + "] is missing. Value traversed to [" +
+                            r.unresolved_display(rc.from) + "]";
+          J b = J::obj();
+          b.add("context", J::str(r.prog.ctx[pc.f]));
+          b.add("messages", R::messages(J::str(""), J::str(err)));
+          b.add("unresolved", r.unresolved_json(rc.from));
+          list.push(clause_wrap("Block", std::move(b)));
+          break;
+        }
+        case REC_UNARY: {
+          const PClause& pc = r.prog.clauses[rc.clause];
+          uint32_t op = pc.flags & 15u;
+          bool neg = (pc.flags >> 4) & 1u;
+          std::string ctx = r.prog.ctx[pc.d];
+          J check = J::obj();
+          std::string msg;
+          if ((rc.from.meta & 3u) == QR_UNRESOLVED) {
+            msg = "Check was not compliant as property [" + r.remaining(rc.from) + "] is missing. Value traversed to [" +
+                  r.unresolved_display(rc.from) + "].";
+            J u = J::obj(); u.add("value", r.unresolved_json(rc.from)); u.add("comparison", r.comparison(op, neg));
+            check.add("UnResolved", std::move(u));
+          } else {
+            msg = "Check was not compliant as property [" + r.q_path_display(rc.from) + "] " + unary_msg(op, neg) + ".";
+            J u = J::obj(); u.add("value", r.pav_json(rc.from)); u.add("comparison", r.comparison(op, neg));
+            check.add("Resolved", std::move(u));
+          }
+          J un = J::obj();
+          un.add("check", std::move(check));
+          un.add("context", J::str(ctx));
+          un.add("messages", R::messages(J::str(r.custom(pc)), J::str(msg)));
+          list.push(clause_wrap("Clause", clause_wrap("Unary", std::move(un))));
+          break;
+        }
+        case REC_NOVALUE_EMPTY: {
+          const PClause& pc = r.prog.clauses[rc.clause];
+          std::string ctx = r.prog.ctx[pc.d];
+          std::string cm = r.custom(pc);
+          for (auto& ch : cm) if (ch == '\n') ch = ';';
+          J check = J::obj(); check.add("UnResolvedContext", J::str(ctx));
+          J un = J::obj();
+          un.add("check", std::move(check));
+          un.add("context", J::str(ctx));
+          un.add("messages", R::messages(J::str(cm), J::str("Check was not compliant as variable in context [" + ctx + "] was not empty")));
+          list.push(clause_wrap("Clause", clause_wrap("Unary", std::move(un))));
+          break;
+        }
+        case REC_DEPENDENT_RULE: {
+          const PClause& pc = r.prog.clauses[rc.clause];
+          std::string ctx = r.prog.ctx[pc.d];
+          std::string rule = r.prog.ctx[pc.f];
+          J check = J::obj(); check.add("UnResolvedContext", J::str(rule));
+          J un = J::obj();
+          un.add("messages", R::messages(J::str(r.custom(pc)),
+                                         J::str("Check was not compliant as dependent rule [" + rule + "] did not PASS. Context [" + ctx + "]")));
+          un.add("context", J::str(ctx));
+          un.add("check", std::move(check));
+          // field order: UnaryReport = check, context, messages
+          J ordered = J::obj();
+          ordered.add("check", un.o[2].second);
+          ordered.add("context", un.o[1].second);
+          ordered.add("messages", un.o[0].second);
+          list.push(clause_wrap("Clause", clause_wrap("Unary", std::move(ordered))));
+          break;
+        }
+        case REC_CMP: {
+          const PClause& pc = r.prog.clauses[rc.clause];
+          uint32_t op = pc.flags & 15u;
+          bool neg = (pc.flags >> 4) & 1u;
+          std::string ctx = r.prog.ctx[pc.d];
+          std::string errm;
+          if (rc.x) {
+            std::string reason;
+            if (rc.x == NC_TYPES) reason = std::string("PathAwareValues are not comparable ") + type_info(rc.y >> 8) + ", " + type_info(rc.y & 0xFF);
+            else if (rc.x == NC_FLOAT) reason = "Float values are not comparable";
+            else if (rc.x == NC_STRING_IN) reason = "Type not comparable, " + r.pav_display(rc.from) + ", " + r.pav_display(rc.to);
+            else reason = "Can not compare type " + r.pav_display(rc.from) + ", " + r.pav_display(rc.to);
+            errm = " Error = [" + reason + "]";
+          }
+          J bin = J::obj();
+          bin.add("context", J::str(ctx));
+          if ((rc.from.meta & 3u) == QR_UNRESOLVED) {
+            std::string msg = "Check was not compliant as property [" + r.remaining(rc.from) +
+                              "] to compare from is missing. Value traversed to [" + r.unresolved_display(rc.from) + "]." + errm;
+            bin.add("messages", R::messages(J::str(r.custom(pc)), J::str(msg)));
+            J u = J::obj(); u.add("value", r.unresolved_json(rc.from)); u.add("comparison", r.comparison(op, neg));
+            J check = J::obj(); check.add("UnResolved", std::move(u));
+            bin.add("check", std::move(check));
+          } else {
+            if (rc.to.meta == 0xFFFFFFFFu) break;   // `to` absent: nothing reported (eval_context.rs:2283)
+            if ((rc.to.meta & 3u) == QR_UNRESOLVED) {
+              std::string msg = "Check was not compliant as property [" + r.remaining(rc.to) +
+                                "] to compare to is missing. Value traversed to [" + r.unresolved_display(rc.to) + "]." + errm;
+              bin.add("messages", R::messages(J::str(r.custom(pc)), J::str(msg)));
+              J u = J::obj(); u.add("value", r.unresolved_json(rc.to)); u.add("comparison", r.comparison(op, neg));
+              J check = J::obj(); check.add("UnResolved", std::move(u));
+              bin.add("check", std::move(check));
+            } else {
+              std::string msg = "Check was not compliant as property value [" + r.pav_display(rc.from) + "] " + op_msg(op, neg) +
+                                " value [" + r.pav_display(rc.to) + "]." + errm;
+              bin.add("messages", R::messages(J::str(r.custom(pc)), J::str(msg)));
+              J rr = J::obj(); rr.add("from", r.pav_json(rc.from)); rr.add("to", r.pav_json(rc.to)); rr.add("comparison", r.comparison(op, neg));
+              J check = J::obj(); check.add("Resolved", std::move(rr));
+              bin.add("check", std::move(check));
+            }
+          }
+          list.push(clause_wrap("Clause", clause_wrap("Binary", std::move(bin))));
+          break;
+        }
+        case REC_IN: {
+          const PClause& pc = r.prog.clauses[rc.clause];
+          uint32_t op = pc.flags & 15u;
+          bool neg = (pc.flags >> 4) & 1u;
+          std::vector<QR> to;
+          uint32_t n = rc.x;
+          while (to.size() < n && i < recs.size() && recs[i].kind == REC_LIST) {
+            to.push_back(recs[i].from);
+            if (to.size() < n) to.push_back(recs[i].to);
+            i++;
+          }
+          std::string sd;
+          for (size_t k = 0; k < to.size(); k++) {
+            std::string item = "(resolved, " + r.pav_display(to[k]) + ")";
+            sd = k ? sd + "." + item : item;
+          }
+          std::string fixed;
+          for (size_t k = 0; k < sd.size(); k++) { if (sd[k] == '.' && k + 1 < sd.size() && sd[k + 1] == '[') continue; fixed.push_back(sd[k]); }
+          std::string err = "Check was not compliant as property [" + r.q_path_display(rc.from) + "] was not present in [" + fixed + "]";
+          J bin = J::obj();
+          bin.add("context", J::str(r.prog.ctx[pc.d]));
+          bin.add("messages", R::messages(r.custom_opt(pc), J::str(err)));
+          J inr = J::obj();
+          inr.add("from", r.pav_json(rc.from));
+          J arr = J::arr();
+          for (auto& t : to) arr.push(r.pav_json(t));
+          inr.add("to", std::move(arr));
+          inr.add("comparison", r.comparison(op, neg));
+          J check = J::obj(); check.add("InResolved", std::move(inr));
+          bin.add("check", std::move(check));
+          list.push(clause_wrap("Clause", clause_wrap("Binary", std::move(bin))));
+          break;
+        }
+        default:
+          break;
+      }
+    }
+    return list;
+  }
+};
+
+std::string status_str(uint32_t s) { return s == ST_PASS ? "PASS" : s == ST_FAIL ? "FAIL" : "SKIP"; }
+uint32_t status_and(uint32_t a, uint32_t b) {
+  if (a == ST_FAIL) return ST_FAIL;
+  if (a == ST_PASS) return b == ST_FAIL ? ST_FAIL : ST_PASS;
+  return b;
+}
+
+}  // namespace
+
+std::string error_display(const std::string& kind, const std::string& msg) {
+  if (kind == "ParseError") return "Parser Error when parsing `" + msg + "`";
+  if (kind == "MissingValue") return "There was no variable or value object to resolve. Error = `" + msg + "`";
+  if (kind == "IncompatibleError") return "Types or variable assignments are incompatible `" + msg + "`";
+  if (kind == "NotComparable") return "Comparing incoming context with literals or dynamic results wasn't possible `" + msg + "`";
+  if (kind == "YamlError") return "Error parsing incoming YAML context " + msg;
+  if (kind == "JsonError") return "Error parsing incoming JSON context " + msg;
+  return msg;
+}
+
+void tile_error(const DocBatch& docs, const Program& prog, const TileOut& t, ReportError& err) {
+  err.set = true;
+  R r{docs, prog, false};
+  switch (t.err) {
+    case E_EMPTY_INCOMPATIBLE:
+      err.kind = "IncompatibleError";
+      err.msg = std::string("Attempting EMPTY operation on type ") + type_info(t.err_b) + " that does not support it at " + r.path_display(t.err_a);
+      break;
+    case E_TYPEBLOCK_UNRESOLVED:
+      err.kind = "MissingValue";
+      err.msg = "Unable to resolve type block query: " + prog.ctx[prog.clauses[t.err_a].f];
+      break;
+    case E_VAR_MISSING:
+      err.kind = "MissingValue";
+      err.msg = "Could not resolve variable by name " + prog.var_names[t.err_a] + " across scopes";
+      break;
+    case E_RULE_MISSING: {
+      err.kind = "MissingValue";
+      std::string names;
+      for (size_t i = 0; i < prog.slot_names.size(); i++) { if (i) names += ", "; names += rust_debug_str(prog.slot_names[i]); }
+      err.msg = "Rule " + prog.ctx[prog.clauses[t.err_a].f] + " by that name does not exist, Rule Names = [" + names + "]";
+      break;
+    }
+    case E_PARAM_MISSING: {
+      err.kind = "MissingValue";
+      std::string names;
+      for (size_t i = 0; i < prog.param_rule_names.size(); i++) { if (i) names += ", "; names += rust_debug_str(prog.param_rule_names[i]); }
+      err.msg = "Parameterized Rule with name " + prog.ctx[prog.clauses[t.err_a].f] + " was not found, candidate [" + names + "]";
+      break;
+    }
+    case E_PARAM_ARITY:
+      err.kind = "IncompatibleError";
+      err.msg = "Arity mismatch for called parameter rule " + prog.ctx[prog.clauses[t.err_a].f] + ", expected " +
+                std::to_string(t.err_b) + ", got " + std::to_string(prog.clauses[t.err_a].c);
+      break;
+    case E_INTERP_NON_STRING:
+      err.kind = "NotComparable";
+      err.msg = "Variable projections inside Query are returning a non-string value for key";
+      break;
+    case E_INTERP_QUERY:
+      err.kind = "IncompatibleError";
+      err.msg = "This type of query based variable interpolation is not supported";
+      break;
+    case E_REGEX_UNSUPPORTED:
+      err.kind = "Unsupported";
+      err.msg = "unsupported on MI355X path: regex /" + prog.regex_src[t.err_a] + "/ (" +
+                (prog.regex[t.err_a].unsupported ? prog.regex[t.err_a].why : std::string("Unicode-dependent class on non-ASCII input")) + ")";
+      break;
+    case E_HEAP: err.kind = "Unsupported"; err.msg = "MI355X path: per-tile scratch heap exhausted"; break;
+    case E_RECORDS: err.kind = "Unsupported"; err.msg = "MI355X path: failure-record buffer exhausted"; break;
+    case E_DEPTH: err.kind = "Unsupported"; err.msg = "MI355X path: evaluation depth limit exceeded"; break;
+    default: {
+      static const char* why[] = {"", "variable captures", "filter after this query part", "traversal of a synthesized value",
+                                  "join index out of bounds report", "unresolved join keys report", "map key filters (KEYS)",
+                                  "functions other than count()", "clause kind"};
+      err.kind = "Unsupported";
+      err.msg = std::string("unsupported on MI355X path: ") + (t.err_a < 9 ? why[t.err_a] : "construct");
+    }
+  }
+}
+
+bool report_document(const DocBatch& docs, uint32_t doc, const std::vector<const Program*>& progs,
+                     const std::vector<const TileResult*>& tiles, int indent, std::string& out, ReportError& err) {
+  try {
+    uint32_t status = ST_SKIP;
+    J not_compliant = J::arr();
+    std::set<std::string> pass, skip;
+    for (size_t f = 0; f < progs.size(); f++) {
+      const Program& P = *progs[f];
+      const TileResult& T = *tiles[f];
+      if (T.out.err) { tile_error(docs, P, T.out, err); return false; }
+      R r{docs, P, false};
+      Walker w{r, T.recs};
+      J items = w.items(0xFFFFFFFFu);
+      for (auto& it : items.a) not_compliant.push(std::move(it));
+      status = status_and(status, T.out.status);
+      for (uint32_t k = 0; k < P.n_rules; k++) {
+        const std::string& nm = P.rule_names[P.rule_names.size() - P.n_rules + k];
+        if (T.rule_status[k] == ST_PASS) pass.insert(nm);
+        else if (T.rule_status[k] == ST_SKIP) skip.insert(nm);
+      }
+    }
+    J fr = J::obj();
+    fr.add("name", J::str(docs.names[doc]));
+    fr.add("metadata", J::obj());
+    fr.add("status", J::str(status_str(status)));
+    fr.add("not_compliant", std::move(not_compliant));
+    J na = J::arr(); for (auto& s : skip) na.push(J::str(s));
+    J co = J::arr(); for (auto& s : pass) co.push(J::str(s));
+    fr.add("not_applicable", std::move(na));
+    fr.add("compliant", std::move(co));
+    pretty(fr, indent, out);
+    return true;
+  } catch (Fatal& f) {
+    err.set = true; err.kind = f.kind; err.msg = f.msg;
+    return false;
+  }
+}
+
+}  // namespace gg

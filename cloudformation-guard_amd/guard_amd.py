@@ -1,0 +1,182 @@
+"""Python host binding (ctypes) for libcfnguard_mi355x.so.
+
+Mirrors the reference's operator interface for the evaluation path:
+  * ``run_checks(data, data_name, rules, rules_name)``  <- guard-ffi ``cfn_guard_run_checks``
+    (guard-ffi/src/lib.rs:32-45 -> guard/src/commands/helper.rs:25-87)
+  * ``validate_structured(rules, data)``                <- ``cfn-guard validate --structured -o json``
+    (guard/src/commands/validate.rs:391-403, reporters/validate/structured.rs:99-133)
+  * ``Session``                                          batched evaluation with HBM-resident documents
+
+Every call evaluates on the GPU (HIP kernel).  If the shared library has not been built, or no
+HIP device is present, calls raise -- there is no CPU fallback.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libcfnguard_mi355x.so")
+
+
+class ExternError(ctypes.Structure):
+    _fields_ = [("code", ctypes.c_int32), ("message", ctypes.c_void_p)]
+
+
+class ValidateInput(ctypes.Structure):
+    _fields_ = [("content", ctypes.c_char_p), ("file_name", ctypes.c_char_p)]
+
+
+class GuardError(Exception):
+    def __init__(self, code, message):
+        Exception.__init__(self, message)
+        self.code = code
+        self.message = message
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError("libcfnguard_mi355x.so is not built (run __graft_entry__.build()); "
+                           "the MI355X path has no CPU fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    L.cfn_guard_run_checks.argtypes = [ValidateInput, ValidateInput, ctypes.c_bool, ctypes.POINTER(ExternError)]
+    L.cfn_guard_run_checks.restype = ctypes.c_void_p
+    L.cfn_guard_free_string.argtypes = [ctypes.c_void_p]
+    L.cfn_guard_free_string.restype = None
+    L.cfn_guard_validate_batch.argtypes = [ctypes.POINTER(ValidateInput), ctypes.c_size_t, ctypes.POINTER(ValidateInput),
+                                           ctypes.c_size_t, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ExternError)]
+    L.cfn_guard_validate_batch.restype = ctypes.c_void_p
+    L.gg_session_new.restype = ctypes.c_void_p
+    L.gg_session_free.argtypes = [ctypes.c_void_p]
+    L.gg_session_add_rules.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(ExternError)]
+    L.gg_session_add_docs.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_size_t),
+                                      ctypes.POINTER(ctypes.c_char_p), ctypes.c_size_t, ctypes.c_int32, ctypes.c_int32,
+                                      ctypes.POINTER(ExternError)]
+    L.gg_session_upload.argtypes = [ctypes.c_void_p, ctypes.POINTER(ExternError)]
+    L.gg_session_eval.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ExternError)]
+    L.gg_session_report.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ExternError)]
+    L.gg_session_report.restype = ctypes.c_void_p
+    L.gg_session_stat.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+    L.gg_session_stat.restype = ctypes.c_int64
+    L.gg_session_tile_status.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+    L.gg_session_last_kernel_ms.argtypes = [ctypes.c_void_p]
+    L.gg_session_last_kernel_ms.restype = ctypes.c_double
+    L.gg_device_available.restype = ctypes.c_int32
+    _lib = L
+    return L
+
+
+def _take_string(p):
+    if not p:
+        return None
+    s = ctypes.string_at(p).decode("utf-8")
+    lib().cfn_guard_free_string(p)
+    return s
+
+
+def _raise(err):
+    msg = _take_string(err.message) or ""
+    raise GuardError(err.code, msg)
+
+
+def _b(s):
+    return s.encode("utf-8") if isinstance(s, str) else s
+
+
+def run_checks(data, data_name, rules, rules_name, verbose=False):
+    """guard-ffi run_checks: one document x one rules file -> pretty FileReport JSON."""
+    err = ExternError()
+    p = lib().cfn_guard_run_checks(ValidateInput(_b(data), _b(data_name)), ValidateInput(_b(rules), _b(rules_name)),
+                                   verbose, ctypes.byref(err))
+    if err.code != 0:
+        _raise(err)
+    return _take_string(p)
+
+
+def validate_structured(rules, data):
+    """rules: [(name, text)], data: [(name, text)] -> (stdout_json, exit_code).
+    Raises GuardError for an evaluation error (the CLI prints it to stderr, exit -1)."""
+    R = (ValidateInput * max(1, len(rules)))(*[ValidateInput(_b(t), _b(n)) for n, t in rules])
+    D = (ValidateInput * max(1, len(data)))(*[ValidateInput(_b(t), _b(n)) for n, t in data])
+    code = ctypes.c_int32(0)
+    err = ExternError()
+    p = lib().cfn_guard_validate_batch(D, len(data), R, len(rules), ctypes.byref(code), ctypes.byref(err))
+    if err.code != 0:
+        _raise(err)
+    return _take_string(p), code.value
+
+
+class Session:
+    """Documents and compiled rules resident in HBM; repeated evaluations for benchmarking."""
+
+    def __init__(self):
+        self.s = lib().gg_session_new()
+
+    def close(self):
+        if self.s:
+            lib().gg_session_free(self.s)
+            self.s = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def add_rules(self, text, name):
+        err = ExternError()
+        lib().gg_session_add_rules(self.s, _b(text), _b(name), ctypes.byref(err))
+        if err.code != 0:
+            _raise(err)
+
+    def add_docs(self, texts, names=None, mode=0, threads=8):
+        n = len(texts)
+        bufs = [_b(t) for t in texts]
+        T = (ctypes.c_char_p * n)(*bufs)
+        Ls = (ctypes.c_size_t * n)(*[len(b) for b in bufs])
+        N = (ctypes.c_char_p * n)(*[_b(x) for x in (names or ["" for _ in range(n)])])
+        err = ExternError()
+        lib().gg_session_add_docs(self.s, T, Ls, N, n, mode, threads, ctypes.byref(err))
+        if err.code != 0:
+            _raise(err)
+
+    def upload(self):
+        err = ExternError()
+        lib().gg_session_upload(self.s, ctypes.byref(err))
+        if err.code != 0:
+            _raise(err)
+
+    def eval(self, iters=1):
+        ms = (ctypes.c_double * max(1, iters))()
+        err = ExternError()
+        lib().gg_session_eval(self.s, iters, ms, ctypes.byref(err))
+        if err.code != 0:
+            _raise(err)
+        return list(ms)
+
+    def report(self):
+        code = ctypes.c_int32(0)
+        err = ExternError()
+        p = lib().gg_session_report(self.s, ctypes.byref(code), ctypes.byref(err))
+        if err.code != 0:
+            _raise(err)
+        return _take_string(p), code.value
+
+    def stat(self, what):
+        return lib().gg_session_stat(self.s, what)
+
+    def tile_status(self, n):
+        buf = (ctypes.c_uint8 * n)()
+        lib().gg_session_tile_status(self.s, buf, n)
+        return bytes(buf)
+
+    STAT = {"ndocs": 0, "nfiles": 1, "nodes": 2, "bytes": 3, "fail": 4, "pass": 5, "skip": 6, "errors": 7,
+            "records": 8, "arena_bytes": 9, "first_error": 10}
+
+
+def device_available():
+    return lib().gg_device_available() > 0

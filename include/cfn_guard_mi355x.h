@@ -1,0 +1,65 @@
+/* C ABI of the MI355X batch evaluator for AWS CloudFormation Guard rules.
+ *
+ * Drop-in for guard-ffi (reference: guard-ffi/src/lib.rs:32-47, guard-ffi/src/types.rs:4-8,
+ * guard-ffi/example/cfn_guard.h): same struct layouts, same error codes
+ * (guard-ffi/src/errors.rs:12-38), same JSON bytes for non-verbose calls.
+ * All entry points evaluate on the GPU; without a HIP device they fail with code -1.
+ */
+#ifndef CFN_GUARD_MI355X_H
+#define CFN_GUARD_MI355X_H
+
+#include <stdbool.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* guard-ffi/example/cfn_guard.h: extern_err_t (ffi-support ExternError) */
+typedef struct {
+  int32_t code;
+  char *message;
+} extern_err_t;
+
+/* guard-ffi/example/cfn_guard.h / src/types.rs:4-8 FfiValidateInput */
+typedef struct {
+  const char *content;
+  const char *file_name;
+} validate_input_t;
+
+/* Replaces guard-ffi `cfn_guard_run_checks` (guard-ffi/src/lib.rs:32-45 -> run_checks,
+ * guard/src/commands/helper.rs:25-87): one document x one rules file, pretty FileReport JSON.
+ * verbose == true (EventRecord tree) is reported as unsupported (code -1). */
+char *cfn_guard_run_checks(validate_input_t data, validate_input_t rules, bool verbose, extern_err_t *err);
+
+/* Replaces guard-ffi `cfn_guard_free_string` (guard-ffi/src/lib.rs:47). NULL is a no-op. */
+void cfn_guard_free_string(char *s);
+
+/* Batched `cfn-guard validate --structured -o json -S none` (guard/src/commands/validate.rs:391-403,
+ * commands/reporters/validate/structured.rs:99-133): n_docs documents x n_rules rules files.
+ * *exit_code receives 0 / 19 / 5 / -1 like the CLI (commands/mod.rs:69-73, main.rs:35-42). */
+char *cfn_guard_validate_batch(const validate_input_t *docs, size_t n_docs, const validate_input_t *rules,
+                               size_t n_rules, int32_t *exit_code, extern_err_t *err);
+
+/* ---- session API (documents resident in HBM across evaluations; used by bench.py/tests) ---- */
+typedef struct gg_session gg_session;
+gg_session *gg_session_new(void);
+void gg_session_free(gg_session *s);
+int32_t gg_session_add_rules(gg_session *s, const char *text, const char *name, extern_err_t *err);
+/* mode 0: libyaml loader (CLI path, marks); mode 1: serde loader (FFI path) */
+int32_t gg_session_add_docs(gg_session *s, const char *const *texts, const size_t *lens, const char *const *names,
+                            size_t n, int32_t mode, int32_t nthreads, extern_err_t *err);
+int32_t gg_session_upload(gg_session *s, extern_err_t *err);
+int32_t gg_session_eval(gg_session *s, int32_t iters, double *ms_out, extern_err_t *err);
+char *gg_session_report(gg_session *s, int32_t *exit_code, extern_err_t *err);
+int64_t gg_session_stat(gg_session *s, int32_t what);
+int32_t gg_session_tile_status(gg_session *s, uint8_t *out, size_t n);
+double gg_session_last_kernel_ms(gg_session *s);
+int32_t gg_device_available(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif
