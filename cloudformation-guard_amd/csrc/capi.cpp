@@ -310,6 +310,7 @@ void merge_batch(DocBatch& dst, const DocBatch& src) {
   dst.kline.insert(dst.kline.end(), src.kline.begin(), src.kline.end());
   dst.kcol.insert(dst.kcol.end(), src.kcol.begin(), src.kcol.end());
   for (uint32_t r : src.roots) dst.roots.push_back(r + nbase);
+  if (src.serde) dst.serde = true;
   dst.names.insert(dst.names.end(), src.names.begin(), src.names.end());
 }
 

@@ -210,7 +210,16 @@ struct Compiler {
         case QueryPart::AllValues: pp.kind = P_ALL_VALUES; pp.a = qp.has_name ? var(qp.key) : NONE; break;
         case QueryPart::AllIndices: pp.kind = P_ALL_INDICES; pp.a = qp.has_name ? var(qp.key) : NONE; break;
         case QueryPart::Filter: pp.kind = P_FILTER; pp.a = conj(*qp.filter); pp.b = qp.has_name ? var(qp.key) : NONE; break;
-        case QueryPart::MapKeyFilter: pp.kind = P_MAP_KEY_FILTER; break;
+        case QueryPart::MapKeyFilter: {
+          // MapKeyFilterClause (exprs.rs:183-187): rhs literal | query (rooted at the map) | function
+          pp.kind = P_MAP_KEY_FILTER;
+          const LetValue& w = *qp.mk_with;
+          if (w.k == LetValue::Value) { pp.a = RHS_LITERAL; pp.b = literal(w.value); }
+          else if (w.k == LetValue::Access) { pp.a = RHS_QUERY; pp.b = query(w.access); }
+          else { pp.a = RHS_FUNC; pp.b = func(*w.func); }
+          pp.c = op_id(qp.mk_op) | (qp.mk_not ? 1u << 4 : 0) | (qp.has_name ? 1u << 8 : 0);
+          break;
+        }
       }
       local.push_back(pp);
     }

@@ -625,6 +625,7 @@ struct JsonP {
 
 void DocBatch::clear() {
   nodes.clear(); bytes.clear(); line.clear(); col.clear(); kline.clear(); kcol.clear(); roots.clear(); names.clear();
+  serde = false;
 }
 
 std::string DocBatch::path(uint32_t node) const {
@@ -678,6 +679,7 @@ bool load_document(DocBatch& b, const char* text, size_t len, const std::string&
       err.kind = "YamlError"; err.msg = msg; return false;
     }
   }
+  b.serde = true;
   return emit_root(b, t, root, name, true, err);
 }
 

@@ -22,6 +22,7 @@ struct DocBatch {
   std::vector<uint32_t> kline, kcol;     // per map-entry node: its key's mark
   std::vector<uint32_t> roots;           // per document: root node
   std::vector<std::string> names;        // per document: data file name
+  bool serde = false;                    // loaded by the serde (FFI) loader: key paths differ
 
   size_t ndocs() const { return roots.size(); }
   std::string path(uint32_t node) const;  // JSON pointer ("" for a root)

@@ -26,6 +26,7 @@ namespace gg {
 #define DEVN __device__ __attribute__((noinline))
 
 static const uint32_t SYN_BIT = 0x40000000u;
+static const uint32_t KEY_BIT = 0x20000000u;
 static const uint32_t FRAMES_BYTES = 16384;
 static const uint32_t RECS_BYTES = 65536;
 static const uint32_t MAX_DEPTH = 48;
@@ -102,6 +103,14 @@ DEV DNode node(const Ctx& c, uint32_t ref) {
   if (ref & SYN_BIT) {
     const uint32_t* s = (const uint32_t*)(c.heap + c.syn_off) + 4 * (ref & 0xFFFFu);
     DNode d; d.kind = K_INT; d.count = 0; d.a = s[1]; d.b = s[2]; d.key_off = NONE; d.key_len = 0; d.key_hash = 0; d.parent = NONE;
+    return d;
+  }
+  if (ref & KEY_BIT) {
+    // the key of a map entry as a String value (MapValue.keys, path_value.rs:459-466)
+    uint32_t e = ref & ~KEY_BIT;
+    DNode en = (e & LIT_BIT) ? c.P->lit_nodes[e & ~LIT_BIT] : c.dn[e];
+    DNode d; d.kind = K_STRING; d.count = en.key_len; d.a = en.key_off; d.b = en.key_hash;
+    d.key_off = NONE; d.key_len = 0; d.key_hash = 0; d.parent = NONE;
     return d;
   }
   if (ref & LIT_BIT) return c.P->lit_nodes[ref & ~LIT_BIT];
@@ -357,6 +366,123 @@ DEVN bool pv_eq(Ctx& c, uint32_t ra, uint32_t rb, uint32_t depth) {
 // ---------------------------------------------------------- query engine ---
 DEV uint32_t qpart_index(const Ctx& c, uint32_t qid, uint32_t qi) { return c.P->queries[qid].first + qi; }
 
+DEV Rec mk_rec(uint32_t kind, uint32_t clause);
+DEV void rec_push(Ctx& c, const Rec& r);
+
+// in_cmp(not_in) (eval.rs:540-566): 1 true, 0 false, -1 NotComparable
+DEVN int in_cmp(Ctx& c, uint32_t l, uint32_t r, bool not_in) {
+  DNode a = node(c, l), b = node(c, r);
+  if (a.kind == K_STRING && b.kind == K_STRING) {
+    const char* hay = bytes_of(c, r) + b.a;
+    const char* nd = bytes_of(c, l) + a.a;
+    bool found = a.count == 0;
+    for (uint32_t i = 0; !found && i + a.count <= b.count; i++) found = bytes_eq(hay + i, nd, a.count);
+    return (found != not_in) ? 1 : 0;
+  }
+  if (b.kind == K_LIST) {
+    bool found = false;
+    for (uint32_t i = 0; i < b.count; i++) {
+      Cmp x = compare_eq(c, l, child(r, b, i), 0);
+      if (x.status) return -1;
+      if (x.ord == 0) found = true;
+    }
+    return (found != not_in) ? 1 : 0;
+  }
+  Cmp x = compare_eq(c, l, r, 0);
+  if (x.status) return -1;
+  return ((x.ord == 0) != not_in) ? 1 : 0;
+}
+
+// MapKeyFilter step (eval_context.rs:830-922): real_binary_operation over the map's keys with
+// context "" (records leak into the enclosing clause, exactly as in the reference)
+DEVN void map_key_filter(Ctx& c, uint32_t qi, uint32_t qid, uint32_t cur, const DNode& cn, uint32_t resolver,
+                         uint32_t conv, const PPart& part) {
+  const uint32_t m0 = c.tmp;
+  View rhs;
+  if (part.a == RHS_LITERAL) {
+    rhs.off = alloc_tmp(c, 16); rhs.n = 1;
+    if (c.err) return;
+    *qra(c, rhs.off) = mk_qr(part.b, QR_LITERAL);
+  } else if (part.a == RHS_QUERY) {
+    uint32_t start = c.tmp;
+    query_retrieval(c, 0, part.b, cur, resolver, conv);
+    rhs.off = start; rhs.n = (c.tmp - start) / 16;
+  } else {
+    rhs = resolve_function(c, part.b, resolver);
+  }
+  if (c.err) return;
+  uint32_t op = part.c & 15u;
+  bool neg = (part.c >> 4) & 1u;
+  if (op == OP_EQ && rhs.n > 1) op = OP_IN;
+  uint32_t yop = op | (neg ? 16u : 0u) | 0x100u;
+  uint32_t sel_off = alloc_tmp(c, (cn.count ? cn.count : 1) * 4);
+  uint32_t items_off = alloc_tmp(c, (rhs.n ? rhs.n : 1) * 16);
+  if (c.err) return;
+  uint32_t nsel = 0;
+  for (uint32_t j = 0; j < cn.count && !c.err; j++) {
+    uint32_t entry = child(cur, cn, j);
+    uint32_t kref = KEY_BIT | entry;
+    if (op == OP_IN) {
+      bool found = false;
+      for (uint32_t i = 0; i < rhs.n && !c.err; i++) {
+        QR r = *qra(c, rhs.off + i * 16);
+        if (qkind(r) == QR_UNRESOLVED) { *qra(c, items_off + i * 16) = r; continue; }
+        uint32_t rr = r.node;
+        int res = in_cmp(c, kref, rr, neg);
+        if (res < 0 && qkind(r) == QR_LITERAL) {
+          DNode rn = node(c, rr);
+          if (rn.kind == K_LIST && rn.count == 1) { rr = child(rr, rn, 0); res = in_cmp(c, kref, rr, neg); }
+        }
+        *qra(c, items_off + i * 16) = mk_qr(rr, QR_RESOLVED);
+        if (res == 1) found = true;
+      }
+      if (c.err) break;
+      c.rec_created++;
+      if (found) { u32a(c, sel_off)[nsel++] = entry; continue; }
+      if (!c.suppress) {
+        Rec rc = mk_rec(REC_IN, NONE);
+        rc.from = mk_qr(kref, QR_RESOLVED); rc.x = rhs.n; rc.y = yop;
+        rec_push(c, rc);
+        for (uint32_t i = 0; i < rhs.n; i += 2) {
+          Rec l = mk_rec(REC_LIST, NONE);
+          l.from = *qra(c, items_off + i * 16);
+          if (i + 1 < rhs.n) l.to = *qra(c, items_off + (i + 1) * 16);
+          rec_push(c, l);
+        }
+      }
+    } else {
+      for (uint32_t i = 0; i < rhs.n && !c.err; i++) {
+        QR r = *qra(c, rhs.off + i * 16);
+        c.rec_created++;
+        Rec rc = mk_rec(REC_CMP, NONE);
+        rc.from = mk_qr(kref, QR_RESOLVED); rc.y = yop;
+        if (qkind(r) == QR_UNRESOLVED) { rc.to = r; rec_push(c, rc); continue; }
+        uint32_t rr = r.node;
+        Cmp x = compare_eq(c, kref, rr, 0);
+        if (x.status && qkind(r) == QR_LITERAL) {
+          DNode rn = node(c, rr);
+          if (rn.kind == K_LIST && rn.count == 1) { rr = child(rr, rn, 0); x = compare_eq(c, kref, rr, 0); }
+        }
+        if (c.err) break;
+        bool ok = x.status == 0 && ((x.ord == 0) != neg);
+        if (ok) { u32a(c, sel_off)[nsel++] = entry; continue; }
+        rc.to = mk_qr(rr, QR_RESOLVED);
+        rec_push(c, rc);
+      }
+    }
+  }
+  uint32_t res0 = c.tmp;
+  for (uint32_t k = 0; k < nsel && !c.err; k++) query_retrieval(c, qi + 1, qid, u32a(c, sel_off)[k], resolver, conv);
+  if (c.err) return;
+  // results must stay contiguous for the caller: slide them over the temporaries
+  // (every lane copies everything in the same order, so each lane only reads its own writes)
+  uint32_t n = (c.tmp - res0) / 4;
+  uint32_t* dst = u32a(c, m0);
+  const uint32_t* src = u32a(c, res0);
+  for (uint32_t i = 0; i < n; i++) dst[i] = src[i];
+  c.tmp = m0 + n * 4;
+}
+
 DEVN void query_retrieval(Ctx& c, uint32_t qi, uint32_t qid, uint32_t cur, uint32_t resolver, uint32_t conv) {
   CHK(c);
   if (++c.depth > MAX_DEPTH * 4) { fail(c, E_DEPTH); c.depth--; return; }
@@ -560,6 +686,9 @@ DEVN void query_retrieval(Ctx& c, uint32_t qi, uint32_t qid, uint32_t cur, uint3
       break;
     }
     case P_MAP_KEY_FILTER:
+      if (cn.kind != K_MAP) { qr_push(c, mk_unres(cur, R_MAPFILTER_NOT_STRUCT, qid, qi, 0)); break; }
+      map_key_filter(c, qi, qid, cur, cn, resolver, conv, part);
+      break;
     default:
       fail(c, E_UNSUPPORTED, 6);
       break;

@@ -88,15 +88,39 @@ struct R {
   const Program& prog;
   bool serde;
 
+  static const uint32_t KEY_BIT = 0x20000000u;   // "the key of map entry X" (MapValue.keys)
   const DocBatch& B(uint32_t ref) const { return (ref & LIT_BIT) ? prog.lit : docs; }
-  uint32_t I(uint32_t ref) const { return ref & ~LIT_BIT; }
-  const DNode& N(uint32_t ref) const { return B(ref).nodes[I(ref)]; }
-  std::string str(uint32_t ref) const { const DNode& n = N(ref); return B(ref).bytes.substr(n.a, n.count); }
-  std::string key(uint32_t ref) const { const DNode& n = N(ref); return B(ref).bytes.substr(n.key_off, n.key_len); }
+  uint32_t I(uint32_t ref) const { return ref & ~(LIT_BIT | KEY_BIT); }
+  bool is_key(uint32_t ref) const { return (ref & KEY_BIT) != 0; }
+  // key refs read as a String node whose bytes are the entry's key
+  DNode key_node(uint32_t ref) const {
+    const DNode& e = B(ref).nodes[I(ref)];
+    DNode d; d.kind = K_STRING; d.count = e.key_len; d.a = e.key_off; d.b = e.key_hash;
+    d.key_off = NONE; d.key_len = 0; d.key_hash = 0; d.parent = NONE;
+    return d;
+  }
+  DNode N(uint32_t ref) const { return is_key(ref) ? key_node(ref) : B(ref).nodes[I(ref)]; }
+  std::string str(uint32_t ref) const { DNode n = N(ref); return B(ref).bytes.substr(n.a, n.count); }
+  std::string key(uint32_t ref) const { DNode n = N(ref); return B(ref).bytes.substr(n.key_off, n.key_len); }
   uint32_t child(uint32_t ref, uint32_t j) const { return (ref & LIT_BIT) | (N(ref).a + j); }
-  std::string path(uint32_t ref) const { return B(ref).path(I(ref)); }
-  uint32_t line(uint32_t ref) const { return B(ref).line[I(ref)]; }
-  uint32_t col(uint32_t ref) const { return B(ref).col[I(ref)]; }
+  // key PV paths: libyaml loader -> the map's path at the key mark (path_value.rs:467-470);
+  // serde loader / rule literals -> map path + "/key" at the map's (0,0) location (:391-395)
+  bool key_serde(uint32_t ref) const { return (ref & LIT_BIT) || docs.serde; }
+  uint32_t parent_of(uint32_t ref) const { return B(ref).nodes[I(ref)].parent; }
+  std::string path(uint32_t ref) const {
+    if (!is_key(ref)) return B(ref).path(I(ref));
+    std::string mp = B(ref).path(parent_of(ref));
+    if (key_serde(ref)) { const DNode& e = B(ref).nodes[I(ref)]; return mp + "/" + B(ref).bytes.substr(e.key_off, e.key_len); }
+    return mp;
+  }
+  uint32_t line(uint32_t ref) const {
+    if (!is_key(ref)) return B(ref).line[I(ref)];
+    return key_serde(ref) ? 0 : B(ref).kline[I(ref)];
+  }
+  uint32_t col(uint32_t ref) const {
+    if (!is_key(ref)) return B(ref).col[I(ref)];
+    return key_serde(ref) ? 0 : B(ref).kcol[I(ref)];
+  }
   std::string loc(uint32_t l, uint32_t c) const { return "[L:" + std::to_string(l) + ",C:" + std::to_string(c) + "]"; }
   std::string path_display(uint32_t ref) const { return path(ref) + loc(line(ref), col(ref)); }
   int64_t ival(const DNode& n) const { return (int64_t)(((uint64_t)n.b << 32) | n.a); }
@@ -418,10 +442,14 @@ struct Walker {
           break;
         }
         case REC_CMP: {
-          const PClause& pc = r.prog.clauses[rc.clause];
-          uint32_t op = pc.flags & 15u;
-          bool neg = (pc.flags >> 4) & 1u;
-          std::string ctx = r.prog.ctx[pc.d];
+          // clause == NONE: a map-key-filter comparison (real_binary_operation, eval.rs:976-1075):
+          // context "", no custom message, comparison carried in rc.y
+          bool mk = rc.clause == NONE;
+          const PClause* pcp = mk ? nullptr : &r.prog.clauses[rc.clause];
+          uint32_t op = mk ? (rc.y & 15u) : (pcp->flags & 15u);
+          bool neg = mk ? ((rc.y >> 4) & 1u) : ((pcp->flags >> 4) & 1u);
+          std::string ctx = mk ? std::string() : r.prog.ctx[pcp->d];
+          std::string cust = mk ? std::string() : r.custom(*pcp);
           std::string errm;
           if (rc.x) {
             std::string reason;
@@ -436,7 +464,7 @@ struct Walker {
           if ((rc.from.meta & 3u) == QR_UNRESOLVED) {
             std::string msg = "Check was not compliant as property [" + r.remaining(rc.from) +
                               "] to compare from is missing. Value traversed to [" + r.unresolved_display(rc.from) + "]." + errm;
-            bin.add("messages", R::messages(J::str(r.custom(pc)), J::str(msg)));
+            bin.add("messages", R::messages(J::str(cust), J::str(msg)));
             J u = J::obj(); u.add("value", r.unresolved_json(rc.from)); u.add("comparison", r.comparison(op, neg));
             J check = J::obj(); check.add("UnResolved", std::move(u));
             bin.add("check", std::move(check));
@@ -445,14 +473,14 @@ struct Walker {
             if ((rc.to.meta & 3u) == QR_UNRESOLVED) {
               std::string msg = "Check was not compliant as property [" + r.remaining(rc.to) +
                                 "] to compare to is missing. Value traversed to [" + r.unresolved_display(rc.to) + "]." + errm;
-              bin.add("messages", R::messages(J::str(r.custom(pc)), J::str(msg)));
+              bin.add("messages", R::messages(J::str(cust), J::str(msg)));
               J u = J::obj(); u.add("value", r.unresolved_json(rc.to)); u.add("comparison", r.comparison(op, neg));
               J check = J::obj(); check.add("UnResolved", std::move(u));
               bin.add("check", std::move(check));
             } else {
               std::string msg = "Check was not compliant as property value [" + r.pav_display(rc.from) + "] " + op_msg(op, neg) +
                                 " value [" + r.pav_display(rc.to) + "]." + errm;
-              bin.add("messages", R::messages(J::str(r.custom(pc)), J::str(msg)));
+              bin.add("messages", R::messages(J::str(cust), J::str(msg)));
               J rr = J::obj(); rr.add("from", r.pav_json(rc.from)); rr.add("to", r.pav_json(rc.to)); rr.add("comparison", r.comparison(op, neg));
               J check = J::obj(); check.add("Resolved", std::move(rr));
               bin.add("check", std::move(check));
@@ -462,9 +490,10 @@ struct Walker {
           break;
         }
         case REC_IN: {
-          const PClause& pc = r.prog.clauses[rc.clause];
-          uint32_t op = pc.flags & 15u;
-          bool neg = (pc.flags >> 4) & 1u;
+          bool mk = rc.clause == NONE;
+          const PClause* pcp = mk ? nullptr : &r.prog.clauses[rc.clause];
+          uint32_t op = mk ? (rc.y & 15u) : (pcp->flags & 15u);
+          bool neg = mk ? ((rc.y >> 4) & 1u) : ((pcp->flags >> 4) & 1u);
           std::vector<QR> to;
           uint32_t n = rc.x;
           while (to.size() < n && i < recs.size() && recs[i].kind == REC_LIST) {
@@ -474,19 +503,20 @@ struct Walker {
           }
           std::string sd;
           for (size_t k = 0; k < to.size(); k++) {
-            std::string item = "(resolved, " + r.pav_display(to[k]) + ")";
+            std::string item = (to[k].meta & 3u) == QR_UNRESOLVED ? "(unresolved, " + r.unresolved_display(to[k]) + ")"
+                                                                  : "(resolved, " + r.pav_display(to[k]) + ")";
             sd = k ? sd + "." + item : item;
           }
           std::string fixed;
           for (size_t k = 0; k < sd.size(); k++) { if (sd[k] == '.' && k + 1 < sd.size() && sd[k + 1] == '[') continue; fixed.push_back(sd[k]); }
           std::string err = "Check was not compliant as property [" + r.q_path_display(rc.from) + "] was not present in [" + fixed + "]";
           J bin = J::obj();
-          bin.add("context", J::str(r.prog.ctx[pc.d]));
-          bin.add("messages", R::messages(r.custom_opt(pc), J::str(err)));
+          bin.add("context", J::str(mk ? std::string() : r.prog.ctx[pcp->d]));
+          bin.add("messages", R::messages(mk ? J::null() : r.custom_opt(*pcp), J::str(err)));
           J inr = J::obj();
           inr.add("from", r.pav_json(rc.from));
           J arr = J::arr();
-          for (auto& t : to) arr.push(r.pav_json(t));
+          for (auto& t : to) if ((t.meta & 3u) != QR_UNRESOLVED) arr.push(r.pav_json(t));
           inr.add("to", std::move(arr));
           inr.add("comparison", r.comparison(op, neg));
           J check = J::obj(); check.add("InResolved", std::move(inr));
@@ -523,7 +553,7 @@ std::string error_display(const std::string& kind, const std::string& msg) {
 
 void tile_error(const DocBatch& docs, const Program& prog, const TileOut& t, ReportError& err) {
   err.set = true;
-  R r{docs, prog, false};
+  R r{docs, prog, docs.serde};
   switch (t.err) {
     case E_EMPTY_INCOMPATIBLE:
       err.kind = "IncompatibleError";
@@ -592,7 +622,7 @@ bool report_document(const DocBatch& docs, uint32_t doc, const std::vector<const
       const Program& P = *progs[f];
       const TileResult& T = *tiles[f];
       if (T.out.err) { tile_error(docs, P, T.out, err); return false; }
-      R r{docs, P, false};
+      R r{docs, P, docs.serde};
       Walker w{r, T.recs};
       J items = w.items(0xFFFFFFFFu);
       for (auto& it : items.a) not_compliant.push(std::move(it));
