@@ -17,7 +17,8 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 YAML_INC = "/opt/conda/include"
 YAML_LIB = "/opt/conda/lib"
 
-HOST_SRCS = ["doc_loader.cpp", "rules_parser.cpp", "regex_dfa.cpp", "cruet.cpp", "compiler.cpp", "reporter.cpp"]
+HOST_SRCS = ["doc_loader.cpp", "rules_parser.cpp", "regex_dfa.cpp", "cruet.cpp", "compiler.cpp", "reporter.cpp",
+             "synth_corpus.cpp"]
 HIP_SRCS = ["eval_kernel.hip", "capi.cpp"]
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-I" + YAML_INC, "-Wno-unused-result"]
 

@@ -24,9 +24,12 @@
 #include "eval_device.h"
 #include "program.h"
 #include "reporter.h"
+#include "synth_corpus.h"
 
 namespace gg {
 __global__ void guard_eval_kernel(LaunchArgs A);
+__global__ void rule_count_kernel(const TileOut* tiles, const uint8_t* rule_status, const DevProg* progs, uint32_t nfiles,
+                                  uint32_t ntiles, uint32_t max_top, unsigned long long* counts);
 }
 
 using namespace gg;
@@ -154,6 +157,15 @@ struct gg_session {
   DBuf<uint8_t> d_rule_status;
   DBuf<Rec> d_recs;
   DBuf<uint32_t> d_counters;
+  DBuf<unsigned long long> d_counts;   // per (file, top rule) x {PASS, FAIL, SKIP, error}
+  size_t ncounts = 0;
+  hipStream_t stream = nullptr;        // caller stream (e.g. torch's current stream); null = library stream
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;   // brackets of the most recent launch (= evq[nq - 1])
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> evq;   // one pair per launch since the last drain
+  size_t nq = 0;
+  unsigned long long* ext_counts = nullptr;   // caller-owned device tally buffer (RCCL all-reduce)
+  bool launched = false;
+  std::vector<unsigned long long> counts;
   bool uploaded = false;
   uint32_t max_top = 1;
   uint32_t nslots = 0;
@@ -198,15 +210,23 @@ void session_upload(gg_session* s) {
   s->rec_cap = std::min<size_t>(std::max<size_t>(ntiles * 48, 4096), (size_t)96 * 1024 * 1024);
   s->d_recs.alloc(s->rec_cap);
   s->d_counters.alloc(16);
+  s->ncounts = s->progs.size() * (s->max_top + 1) * 4;
+  if (s->ncounts * sizeof(uint32_t) > 60 * 1024)
+    throw std::runtime_error("too many (rules file x rule) tallies for one LDS block; split the rules files across sessions");
+  s->d_counts.alloc(std::max<size_t>(s->ncounts, 1));
   HIPCHK(hipStreamSynchronize(st));
   s->uploaded = true;
 }
 
-// runs the kernel over all tiles; returns kernel milliseconds (HIP events on the launch stream)
-double session_run(gg_session* s, bool fetch) {
-  hipStream_t st = g_dev.stream;
+hipStream_t session_stream(gg_session* s) { return s->stream ? s->stream : g_dev.stream; }
+
+// enqueues one evaluation of every tile (and the per-rule tally) on the session stream; no host sync
+void session_launch(gg_session* s) {
+  hipStream_t st = session_stream(s);
   uint32_t ntiles = (uint32_t)(s->docs.ndocs() * s->progs.size());
   HIPCHK(hipMemsetAsync(s->d_counters.p, 0, 16 * sizeof(uint32_t), st));
+  unsigned long long* counts = s->ext_counts ? s->ext_counts : s->d_counts.p;
+  HIPCHK(hipMemsetAsync(counts, 0, s->ncounts * sizeof(unsigned long long), st));
   LaunchArgs A{};
   A.docs.nodes = s->d_nodes.p; A.docs.bytes = s->d_bytes.p; A.docs.roots = s->d_roots.p; A.docs.ndocs = (uint32_t)s->docs.ndocs();
   A.progs = s->d_progs.p; A.nfiles = (uint32_t)s->progs.size();
@@ -215,33 +235,86 @@ double session_run(gg_session* s, bool fetch) {
   A.tiles = s->d_tiles.p; A.rule_status = s->d_rule_status.p; A.max_top = s->max_top;
   A.recs = s->d_recs.p; A.rec_cap = (uint32_t)s->rec_cap;
   A.rec_cursor = s->d_counters.p; A.tile_cursor = s->d_counters.p + 1;
-  hipEvent_t e0, e1;
-  HIPCHK(hipEventCreate(&e0));
-  HIPCHK(hipEventCreate(&e1));
-  HIPCHK(hipEventRecord(e0, st));
-  if (ntiles) hipLaunchKernelGGL(guard_eval_kernel, dim3(s->nslots), dim3(64), 0, st, A);
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipEventRecord(e1, st));
-  HIPCHK(hipEventSynchronize(e1));
-  float ms = 0;
-  HIPCHK(hipEventElapsedTime(&ms, e0, e1));
-  hipEventDestroy(e0);
-  hipEventDestroy(e1);
-  s->last_kernel_ms = ms;
-  if (fetch) {
-    s->tiles.resize(ntiles);
-    s->rule_status.resize((size_t)ntiles * s->max_top);
-    uint32_t nrec = 0;
-    HIPCHK(hipMemcpy(&nrec, s->d_counters.p, 4, hipMemcpyDeviceToHost));
-    if (nrec > s->rec_cap) nrec = (uint32_t)s->rec_cap;
-    s->recs.resize(nrec);
-    if (ntiles) {
-      HIPCHK(hipMemcpy(s->tiles.data(), s->d_tiles.p, ntiles * sizeof(TileOut), hipMemcpyDeviceToHost));
-      HIPCHK(hipMemcpy(s->rule_status.data(), s->d_rule_status.p, s->rule_status.size(), hipMemcpyDeviceToHost));
-    }
-    if (nrec) HIPCHK(hipMemcpy(s->recs.data(), s->d_recs.p, nrec * sizeof(Rec), hipMemcpyDeviceToHost));
-    s->evaluated = true;
+  if (!ntiles) return;
+  if (s->nq == s->evq.size()) {
+    std::pair<hipEvent_t, hipEvent_t> pr;
+    HIPCHK(hipEventCreate(&pr.first));
+    HIPCHK(hipEventCreate(&pr.second));
+    s->evq.push_back(pr);
   }
+  s->ev0 = s->evq[s->nq].first; s->ev1 = s->evq[s->nq].second; s->nq++;
+  HIPCHK(hipEventRecord(s->ev0, st));
+  hipLaunchKernelGGL(guard_eval_kernel, dim3(s->nslots), dim3(64), 0, st, A);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(s->ev1, st));
+  uint32_t cblocks = std::min<uint32_t>((ntiles + 255) / 256, g_dev.ncu * 4);
+  hipLaunchKernelGGL(rule_count_kernel, dim3(cblocks), dim3(256), s->ncounts * sizeof(uint32_t), st, s->d_tiles.p,
+                     s->d_rule_status.p, s->d_progs.p, A.nfiles, ntiles, s->max_top, counts);
+  HIPCHK(hipGetLastError());
+  s->launched = true;
+}
+
+// waits for the last launch; returns the evaluation kernel's milliseconds (HIP events on its stream)
+double session_wait(gg_session* s) {
+  if (!s->launched) return 0;
+  HIPCHK(hipEventSynchronize(s->ev1));
+  float ms = 0;
+  HIPCHK(hipEventElapsedTime(&ms, s->ev0, s->ev1));
+  s->last_kernel_ms = ms;
+  return ms;
+}
+
+// kernel ms of every launch since the last drain (synchronises on the last one)
+size_t session_drain(gg_session* s, double* out, size_t cap) {
+  size_t n = s->nq;
+  if (n) HIPCHK(hipEventSynchronize(s->evq[n - 1].second));
+  for (size_t i = 0; i < n; i++) {
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, s->evq[i].first, s->evq[i].second));
+    if (i < cap && out) out[i] = ms;
+  }
+  s->nq = 0;
+  return n;
+}
+
+// total records the last launch wanted to publish (may exceed rec_cap)
+uint32_t session_records_wanted(gg_session* s) {
+  uint32_t nrec = 0;
+  HIPCHK(hipMemcpy(&nrec, s->d_counters.p, 4, hipMemcpyDeviceToHost));
+  return nrec;
+}
+
+void session_fetch(gg_session* s) {
+  uint32_t ntiles = (uint32_t)(s->docs.ndocs() * s->progs.size());
+  s->tiles.resize(ntiles);
+  s->rule_status.resize((size_t)ntiles * s->max_top);
+  uint32_t nrec = session_records_wanted(s);
+  if (nrec > s->rec_cap) nrec = (uint32_t)s->rec_cap;
+  s->recs.resize(nrec);
+  if (ntiles) {
+    HIPCHK(hipMemcpy(s->tiles.data(), s->d_tiles.p, ntiles * sizeof(TileOut), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(s->rule_status.data(), s->d_rule_status.p, s->rule_status.size(), hipMemcpyDeviceToHost));
+  }
+  if (nrec) HIPCHK(hipMemcpy(s->recs.data(), s->d_recs.p, nrec * sizeof(Rec), hipMemcpyDeviceToHost));
+  s->counts.resize(s->ncounts);
+  HIPCHK(hipMemcpy(s->counts.data(), s->ext_counts ? s->ext_counts : s->d_counts.p, s->ncounts * sizeof(unsigned long long),
+                   hipMemcpyDeviceToHost));
+  s->evaluated = true;
+}
+
+// one complete evaluation; grows the record arena and re-runs when the first pass overflowed it
+double session_run(gg_session* s, bool fetch) {
+  session_launch(s);
+  double ms = session_wait(s);
+  uint32_t want = session_records_wanted(s);
+  if (want > s->rec_cap) {
+    s->rec_cap = std::min<size_t>((size_t)want + want / 8 + 1024, (size_t)0xFFFFFFF0u);
+    s->d_recs.alloc(s->rec_cap);
+    session_launch(s);
+    ms = session_wait(s);
+  }
+  if (fetch) session_fetch(s);
+  session_drain(s, nullptr, 0);
   return ms;
 }
 
@@ -293,25 +366,60 @@ bool session_report(gg_session* s, std::string& out, int32_t& exit_code, ReportE
   return true;
 }
 
-void merge_batch(DocBatch& dst, const DocBatch& src) {
-  uint32_t nbase = (uint32_t)dst.nodes.size();
-  uint32_t bbase = (uint32_t)dst.bytes.size();
-  dst.bytes += src.bytes;
-  for (size_t i = 0; i < src.nodes.size(); i++) {
-    DNode n = src.nodes[i];
-    if (n.kind == K_LIST || n.kind == K_MAP) n.a += nbase;
-    else if (n.kind == K_STRING) n.a += bbase;
-    if (n.key_off != NONE) n.key_off += bbase;
-    if (n.parent != NONE) n.parent += nbase;
-    dst.nodes.push_back(n);
+// Appends per-thread batches to dst: sizes first, one resize, then each part is copied and
+// rebased by its own thread (the arena of a 1M-template corpus is tens of GB).
+void merge_batches(DocBatch& dst, std::vector<DocBatch>& parts) {
+  size_t np = parts.size();
+  std::vector<size_t> nbase(np + 1), bbase(np + 1), rbase(np + 1);
+  nbase[0] = dst.nodes.size(); bbase[0] = dst.bytes.size(); rbase[0] = dst.roots.size();
+  for (size_t t = 0; t < np; t++) {
+    nbase[t + 1] = nbase[t] + parts[t].nodes.size();
+    bbase[t + 1] = bbase[t] + parts[t].bytes.size();
+    rbase[t + 1] = rbase[t] + parts[t].roots.size();
   }
-  dst.line.insert(dst.line.end(), src.line.begin(), src.line.end());
-  dst.col.insert(dst.col.end(), src.col.begin(), src.col.end());
-  dst.kline.insert(dst.kline.end(), src.kline.begin(), src.kline.end());
-  dst.kcol.insert(dst.kcol.end(), src.kcol.begin(), src.kcol.end());
-  for (uint32_t r : src.roots) dst.roots.push_back(r + nbase);
-  if (src.serde) dst.serde = true;
-  dst.names.insert(dst.names.end(), src.names.begin(), src.names.end());
+  if (bbase[np] > kMaxPoolBytes || nbase[np] > kMaxPoolBytes)
+    throw std::runtime_error("document batch is full (u32 arena offsets); evaluate it and start a new batch");
+  dst.nodes.resize(nbase[np]); dst.line.resize(nbase[np]); dst.col.resize(nbase[np]);
+  dst.kline.resize(nbase[np]); dst.kcol.resize(nbase[np]);
+  dst.bytes.resize(bbase[np]);
+  dst.roots.resize(rbase[np]);
+  for (auto& p : parts) if (p.serde) dst.serde = true;
+  auto work = [&](size_t t) {
+    const DocBatch& src = parts[t];
+    uint32_t nb = (uint32_t)nbase[t], bb = (uint32_t)bbase[t];
+    DNode* out = dst.nodes.data() + nb;
+    for (size_t i = 0; i < src.nodes.size(); i++) {
+      DNode n = src.nodes[i];
+      if (n.kind == K_LIST || n.kind == K_MAP) n.a += nb;
+      else if (n.kind == K_STRING) n.a += bb;
+      if (n.key_off != NONE) n.key_off += bb;
+      if (n.parent != NONE) n.parent += nb;
+      out[i] = n;
+    }
+    size_t nn = src.nodes.size() * sizeof(uint32_t);
+    if (nn) {
+      memcpy(dst.line.data() + nb, src.line.data(), nn);
+      memcpy(dst.col.data() + nb, src.col.data(), nn);
+      memcpy(dst.kline.data() + nb, src.kline.data(), nn);
+      memcpy(dst.kcol.data() + nb, src.kcol.data(), nn);
+    }
+    if (!src.bytes.empty()) memcpy(&dst.bytes[bb], src.bytes.data(), src.bytes.size());
+    for (size_t r = 0; r < src.roots.size(); r++) dst.roots[rbase[t] + r] = src.roots[r] + nb;
+  };
+  std::vector<std::thread> th;
+  for (size_t t = 1; t < np; t++) th.emplace_back(work, t);
+  if (np) work(0);
+  for (auto& x : th) x.join();
+  for (auto& p : parts) {
+    dst.names.insert(dst.names.end(), std::make_move_iterator(p.names.begin()), std::make_move_iterator(p.names.end()));
+    p = DocBatch();
+  }
+}
+
+void merge_batch(DocBatch& dst, DocBatch& src) {
+  std::vector<DocBatch> one(1);
+  one[0] = std::move(src);
+  merge_batches(dst, one);
 }
 
 bool add_rules(gg_session* s, const std::string& text, const std::string& name, std::string& perr) {
@@ -432,7 +540,53 @@ char* cfn_guard_validate_batch(const validate_input_t* docs, size_t n_docs, cons
 
 // ------------------------------------------------------------- session API ---
 gg_session* gg_session_new(void) { return new gg_session(); }
-void gg_session_free(gg_session* s) { delete s; }
+void gg_session_free(gg_session* s) {
+  if (!s) return;
+  for (auto& pr : s->evq) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
+  delete s;
+}
+
+void gg_session_set_stream(gg_session* s, void* stream) { s->stream = (hipStream_t)stream; }
+
+int32_t gg_session_launch(gg_session* s, extern_err_t* err) {
+  set_err(err, 0, "");
+  try {
+    std::string why;
+    if (!ensure_device(why)) { set_err(err, -1, why); return -1; }
+    if (!s->uploaded) session_upload(s);
+    session_launch(s);
+    return 0;
+  } catch (std::exception& e) { set_err(err, -1, e.what()); return -1; }
+}
+
+double gg_session_wait(gg_session* s, extern_err_t* err) {
+  set_err(err, 0, "");
+  try { return session_wait(s); } catch (std::exception& e) { set_err(err, -1, e.what()); return -1; }
+}
+
+int32_t gg_session_fetch(gg_session* s, extern_err_t* err) {
+  set_err(err, 0, "");
+  try {
+    session_wait(s);
+    if (session_records_wanted(s) > s->rec_cap) { set_err(err, -1, "record arena overflow: run gg_session_eval first"); return -1; }
+    session_fetch(s);
+    return 0;
+  } catch (std::exception& e) { set_err(err, -1, e.what()); return -1; }
+}
+
+size_t gg_session_ncounts(gg_session* s) { return s->ncounts; }
+void* gg_session_counts_device(gg_session* s) { return s->ext_counts ? (void*)s->ext_counts : (void*)s->d_counts.p; }
+void gg_session_bind_counts(gg_session* s, void* dev, size_t n) {
+  s->ext_counts = (dev && n >= s->ncounts) ? (unsigned long long*)dev : nullptr;
+}
+size_t gg_session_drain_kernel_ms(gg_session* s, double* out, size_t cap, extern_err_t* err) {
+  set_err(err, 0, "");
+  try { return session_drain(s, out, cap); } catch (std::exception& e) { set_err(err, -1, e.what()); return 0; }
+}
+int32_t gg_session_counts(gg_session* s, uint64_t* out, size_t n) {
+  for (size_t i = 0; i < n && i < s->counts.size(); i++) out[i] = s->counts[i];
+  return 0;
+}
 
 int32_t gg_session_add_rules(gg_session* s, const char* text, const char* name, extern_err_t* err) {
   set_err(err, 0, "");
@@ -465,9 +619,52 @@ int32_t gg_session_add_docs(gg_session* s, const char* const* texts, const size_
   for (int t = 0; t < nthreads; t++) {
     if (failed[t] >= 0) { set_err(err, ffi_code(errs[t].kind), error_display(errs[t].kind, errs[t].msg)); return 5; }
   }
-  for (int t = 0; t < nthreads; t++) merge_batch(s->docs, parts[t]);
+  try {
+    merge_batches(s->docs, parts);
+  } catch (std::exception& e) { set_err(err, -1, e.what()); return -1; }
   s->uploaded = false;
   return 0;
+}
+
+int32_t gg_loader_selfcheck(const char* text, size_t len) { return loader_selfcheck(text, len); }
+
+size_t gg_synth_cfn_doc(uint64_t index, int32_t n_resources, char* buf, size_t cap) {
+  std::string t;
+  cfn_synth_doc(index, n_resources, t);
+  if (buf && cap) {
+    size_t n = std::min(cap - 1, t.size());
+    memcpy(buf, t.data(), n);
+    buf[n] = 0;
+  }
+  return t.size();
+}
+
+int32_t gg_session_add_synthetic(gg_session* s, uint64_t first, size_t n, int32_t n_resources, int32_t nthreads,
+                                 extern_err_t* err) {
+  set_err(err, 0, "");
+  try {
+    if (nthreads < 1) nthreads = 1;
+    std::vector<DocBatch> parts(nthreads);
+    std::vector<LoadError> errs(nthreads);
+    std::vector<int> failed(nthreads, 0);
+    auto work = [&](int t) {
+      size_t lo = n * t / nthreads, hi = n * (t + 1) / nthreads;
+      std::string text;
+      for (size_t i = lo; i < hi; i++) {
+        cfn_synth_doc(first + i, n_resources, text);
+        if (!load_document(parts[t], text.data(), text.size(), "synthetic-" + std::to_string(first + i) + ".json",
+                           LOAD_LIBYAML, errs[t])) { failed[t] = 1; return; }
+      }
+    };
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthreads; t++) th.emplace_back(work, t);
+    for (auto& x : th) x.join();
+    for (int t = 0; t < nthreads; t++)
+      if (failed[t]) { set_err(err, ffi_code(errs[t].kind), error_display(errs[t].kind, errs[t].msg)); return 5; }
+    merge_batches(s->docs, parts);
+    s->uploaded = false;
+    return 0;
+  } catch (std::exception& e) { set_err(err, -1, e.what()); return -1; }
 }
 
 int32_t gg_session_upload(gg_session* s, extern_err_t* err) {
@@ -511,7 +708,8 @@ char* gg_session_report(gg_session* s, int32_t* exit_code, extern_err_t* err) {
 }
 
 // statistics: 0 ndocs, 1 nfiles, 2 nodes, 3 string bytes, 4 tiles FAIL, 5 tiles PASS, 6 tiles SKIP,
-// 7 tiles with error, 8 records, 9 device arena bytes (nodes + strings + roots), 10 first error code
+// 7 tiles with error, 8 records, 9 device arena bytes (nodes + strings + roots), 10 first error code,
+// 11 record bytes of the last fetch, 12 record capacity, 13 max top rules per file, 14 wave slots, 15 heap bytes/slot
 int64_t gg_session_stat(gg_session* s, int32_t what) {
   switch (what) {
     case 0: return (int64_t)s->docs.ndocs();
@@ -528,6 +726,11 @@ int64_t gg_session_stat(gg_session* s, int32_t what) {
     case 8: return (int64_t)s->recs.size();
     case 9: return (int64_t)(s->docs.nodes.size() * sizeof(DNode) + s->docs.bytes.size() + s->docs.roots.size() * 4);
     case 10: for (auto& t : s->tiles) if (t.err) return t.err; return 0;
+    case 11: return (int64_t)s->recs.size() * (int64_t)sizeof(Rec);
+    case 12: return (int64_t)s->rec_cap;
+    case 13: return (int64_t)s->max_top;
+    case 14: return (int64_t)s->nslots;
+    case 15: return (int64_t)s->heap_bytes;
     default: return -1;
   }
 }

@@ -3,6 +3,7 @@
 
 #include <yaml.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -217,9 +218,9 @@ struct Emitter {
     b.line[slot] = line; b.col[slot] = col;
     switch (n.kind) {
       case K_STRING: {
-        d.a = (uint32_t)b.bytes.size(); d.count = (uint32_t)n.s.size();
+        d.count = (uint32_t)n.s.size();
         d.b = fnv1a(n.s.data(), n.s.size());
-        b.bytes += n.s;
+        d.a = b.intern(n.s.data(), d.count, d.b);
         break;
       }
       case K_BOOL: d.a = (uint32_t)n.i; break;
@@ -261,9 +262,9 @@ struct Emitter {
         dd.a = first; dd.count = cnt;
         for (uint32_t j = 0; j < cnt; j++) {
           DNode& c = b.nodes[first + j];
-          c.key_off = (uint32_t)b.bytes.size(); c.key_len = (uint32_t)keys[j].size();
+          c.key_len = (uint32_t)keys[j].size();
           c.key_hash = fnv1a(keys[j].data(), keys[j].size());
-          b.bytes += keys[j];
+          c.key_off = b.intern(keys[j].data(), c.key_len, c.key_hash);
           b.kline[first + j] = serde ? 0 : kmarks[j].first;
           b.kcol[first + j] = serde ? 0 : kmarks[j].second;
           const TN& kn = t.n[vals[j]];
@@ -624,8 +625,34 @@ struct JsonP {
 }  // namespace
 
 void DocBatch::clear() {
+  islots.clear(); ilen.clear(); iused = 0;
   nodes.clear(); bytes.clear(); line.clear(); col.clear(); kline.clear(); kcol.clear(); roots.clear(); names.clear();
   serde = false;
+}
+
+uint32_t DocBatch::intern(const char* p, uint32_t n, uint32_t hash) {
+  if ((iused + 1) * 2 > islots.size()) {
+    size_t cap = islots.empty() ? 4096 : islots.size() * 2;
+    std::vector<uint32_t> ns(cap, 0), nl(cap, 0);
+    for (size_t i = 0; i < islots.size(); i++) {
+      if (!islots[i]) continue;
+      uint32_t off = islots[i] - 1, len = ilen[i];
+      size_t h = fnv1a(bytes.data() + off, len) & (cap - 1);
+      while (ns[h]) h = (h + 1) & (cap - 1);
+      ns[h] = islots[i]; nl[h] = len;
+    }
+    islots.swap(ns); ilen.swap(nl);
+  }
+  size_t mask = islots.size() - 1;
+  size_t h = hash & mask;
+  while (islots[h]) {
+    if (ilen[h] == n && memcmp(bytes.data() + islots[h] - 1, p, n) == 0) return islots[h] - 1;
+    h = (h + 1) & mask;
+  }
+  uint32_t off = (uint32_t)bytes.size();
+  bytes.append(p, n);
+  islots[h] = off + 1; ilen[h] = n; iused++;
+  return off;
 }
 
 std::string DocBatch::path(uint32_t node) const {
@@ -646,13 +673,287 @@ std::string DocBatch::path_display(uint32_t node) const {
   return path(node) + "[L:" + std::to_string(line[node]) + ",C:" + std::to_string(col[node]) + "]";
 }
 
+
+bool g_json_fast = true;
+
+// ------------------------------------------------------ JSON fast path ---
+// Most corpora (CloudFormation JSON, Terraform plan JSON, Config CIs) are strict JSON.  For such a
+// document libyaml produces a flow-style event stream whose marks are (line, column) of each
+// token's first character and whose plain scalars are exactly the JSON number/true/false/null
+// tokens.  This path parses that subset directly into the arena -- same node layout as Emitter
+// (each container's children contiguous, blocks in DFS pre-order), same marks, same scalar typing
+// -- and returns "not handled" for anything outside the subset it can prove identical: non-ASCII
+// or control bytes, tabs/CR, surrogate \u escapes, duplicate keys, a key whose ':' is not on the
+// same line within 1000 characters (libyaml simple-key rules), non-container roots, nesting
+// deeper than 256.  Unhandled documents take the libyaml path, so results never depend on which
+// path ran (tests/test_loader_cpu.py compares both on the corpora).
+namespace {
+
+struct JsonFast {
+  const char* s;
+  size_t n;
+  size_t i = 0;
+  uint32_t line = 0;
+  size_t line_start = 0;
+  std::vector<uint32_t> counts;   // pass 1: child count per container, pre-order
+  size_t ci = 0;
+  std::string sbuf;
+  std::vector<uint32_t> khash;    // pass 1 duplicate-key scratch
+
+  JsonFast(const char* t, size_t len) : s(t), n(len) {}
+
+  void ws() {
+    while (i < n) {
+      char c = s[i];
+      if (c == ' ') i++;
+      else if (c == '\n') { i++; line++; line_start = i; }
+      else break;
+    }
+  }
+  uint32_t col() const { return (uint32_t)(i - line_start); }
+
+  // string token at s[i] == '"'; decodes into sbuf when `decode`
+  bool str(bool decode) {
+    i++;
+    if (decode) sbuf.clear();
+    for (;;) {
+      if (i >= n) return false;
+      unsigned char c = (unsigned char)s[i];
+      if (c == '"') { i++; return true; }
+      if (c < 0x20 || c > 0x7E) return false;
+      if (c != '\\') {
+        size_t j = i;
+        while (j < n && s[j] != '"' && s[j] != '\\' && (unsigned char)s[j] >= 0x20 && (unsigned char)s[j] <= 0x7E) j++;
+        if (decode) sbuf.append(s + i, j - i);
+        i = j;
+        continue;
+      }
+      if (i + 1 >= n) return false;
+      char e = s[i + 1];
+      char out;
+      switch (e) {
+        case '"': out = '"'; break;
+        case '\\': out = '\\'; break;
+        case '/': out = '/'; break;
+        case 'b': out = '\b'; break;
+        case 'f': out = '\f'; break;
+        case 'n': out = '\n'; break;
+        case 'r': out = '\r'; break;
+        case 't': out = '\t'; break;
+        case 'u': {
+          if (i + 6 > n) return false;
+          uint32_t cp = 0;
+          for (int k = 0; k < 4; k++) {
+            char h = s[i + 2 + k];
+            cp <<= 4;
+            if (h >= '0' && h <= '9') cp |= (uint32_t)(h - '0');
+            else if (h >= 'a' && h <= 'f') cp |= (uint32_t)(h - 'a' + 10);
+            else if (h >= 'A' && h <= 'F') cp |= (uint32_t)(h - 'A' + 10);
+            else return false;
+          }
+          if (cp >= 0xD800 && cp <= 0xDFFF) return false;
+          if (decode) utf8_append(sbuf, cp);
+          i += 6;
+          continue;
+        }
+        default: return false;
+      }
+      if (decode) sbuf.push_back(out);
+      i += 2;
+    }
+  }
+
+  // plain token (JSON number / true / false / null): returns its length, 0 if not one
+  size_t plain_len() const {
+    size_t j = i;
+    if (j < n && (s[j] == 't' || s[j] == 'f' || s[j] == 'n')) {
+      static const char* words[] = {"true", "false", "null"};
+      for (const char* w : words) {
+        size_t L = strlen(w);
+        if (j + L <= n && memcmp(s + j, w, L) == 0) return L;
+      }
+      return 0;
+    }
+    if (j < n && s[j] == '-') j++;
+    if (j >= n) return 0;
+    if (s[j] == '0') j++;
+    else if (s[j] >= '1' && s[j] <= '9') { while (j < n && isdigit((unsigned char)s[j])) j++; }
+    else return 0;
+    if (j < n && s[j] == '.') {
+      j++;
+      size_t d = j;
+      while (j < n && isdigit((unsigned char)s[j])) j++;
+      if (j == d) return 0;
+    }
+    if (j < n && (s[j] == 'e' || s[j] == 'E')) {
+      j++;
+      if (j < n && (s[j] == '+' || s[j] == '-')) j++;
+      size_t d = j;
+      while (j < n && isdigit((unsigned char)s[j])) j++;
+      if (j == d) return 0;
+    }
+    return j - i;
+  }
+  bool after_plain_ok(size_t j) const {
+    return j >= n || s[j] == ' ' || s[j] == '\n' || s[j] == ',' || s[j] == ']' || s[j] == '}';
+  }
+
+  // pass 1: validate the subset and record container sizes
+  bool v1(int depth) {
+    if (depth > 256 || i >= n) return false;
+    char c = s[i];
+    if (c == '"') return str(false);
+    if (c == '{' || c == '[') {
+      bool map = c == '{';
+      size_t slot = counts.size();
+      counts.push_back(0);
+      i++;
+      ws();
+      char close = map ? '}' : ']';
+      if (i < n && s[i] == close) { i++; return true; }
+      uint32_t cnt = 0;
+      size_t kbase = khash.size();
+      for (;;) {
+        if (map) {
+          if (i >= n || s[i] != '"') return false;
+          size_t kstart = i;
+          uint32_t kline = line;
+          if (!str(true)) return false;
+          uint32_t h = fnv1a(sbuf.data(), sbuf.size());
+          if (khash.size() - kbase <= 64)
+            for (size_t q = kbase; q < khash.size(); q++) if (khash[q] == h) return false;  // possible duplicate
+          khash.push_back(h);
+          while (i < n && s[i] == ' ') i++;
+          if (i >= n || s[i] != ':' || line != kline || i - kstart > 1000) return false;
+          i++;
+          ws();
+        }
+        if (!v1(depth + 1)) return false;
+        cnt++;
+        ws();
+        if (i < n && s[i] == ',') { i++; ws(); continue; }
+        if (i < n && s[i] == close) { i++; break; }
+        return false;
+      }
+      if (khash.size() - kbase > 64) {
+        std::sort(khash.begin() + kbase, khash.end());
+        for (size_t q = kbase + 1; q < khash.size(); q++) if (khash[q] == khash[q - 1]) return false;
+      }
+      khash.resize(kbase);
+      counts[slot] = cnt;
+      return true;
+    }
+    size_t L = plain_len();
+    if (!L || !after_plain_ok(i + L)) return false;
+    i += L;
+    return true;
+  }
+
+  // pass 2: emit into the arena; `slot` already allocated by the parent
+  void v2(DocBatch& b, uint32_t slot, uint32_t parent) {
+    DNode& d = b.nodes[slot];
+    d.parent = parent;
+    d.count = 0; d.a = 0; d.b = 0;
+    char c = s[i];
+    if (c == '"') {
+      str(true);
+      d.kind = K_STRING;
+      d.count = (uint32_t)sbuf.size();
+      d.b = fnv1a(sbuf.data(), sbuf.size());
+      d.a = b.intern(sbuf.data(), d.count, d.b);
+      return;
+    }
+    if (c == '{' || c == '[') {
+      bool map = c == '{';
+      uint32_t cnt = counts[ci++];
+      uint32_t first = (uint32_t)b.nodes.size();
+      size_t sz = first + (size_t)cnt;
+      b.nodes.resize(sz); b.line.resize(sz); b.col.resize(sz); b.kline.resize(sz); b.kcol.resize(sz);
+      DNode& dd = b.nodes[slot];
+      dd.kind = map ? K_MAP : K_LIST;
+      dd.a = first; dd.count = cnt;
+      i++;
+      ws();
+      for (uint32_t j = 0; j < cnt; j++) {
+        uint32_t cs = first + j;
+        if (map) {
+          uint32_t kl = line, kc = col();
+          str(true);
+          DNode& e = b.nodes[cs];
+          e.key_len = (uint32_t)sbuf.size();
+          e.key_hash = fnv1a(sbuf.data(), sbuf.size());
+          e.key_off = b.intern(sbuf.data(), e.key_len, e.key_hash);
+          b.kline[cs] = kl; b.kcol[cs] = kc;
+          while (s[i] == ' ') i++;
+          i++;  // ':'
+          ws();
+        } else {
+          DNode& e = b.nodes[cs];
+          e.key_off = NONE; e.key_len = 0; e.key_hash = 0;
+          b.kline[cs] = 0; b.kcol[cs] = 0;
+        }
+        b.line[cs] = line; b.col[cs] = col();
+        v2(b, cs, slot);
+        ws();
+        i++;  // ',' or the closing bracket
+        ws();
+      }
+      if (!cnt) i++;   // empty container: closing bracket (pass 1 skipped whitespace the same way)
+      return;
+    }
+    size_t L = plain_len();
+    std::string tok(s + i, L);
+    i += L;
+    int64_t iv; double fv;
+    if (tok == "true") { d.kind = K_BOOL; d.a = 1; }
+    else if (tok == "false") { d.kind = K_BOOL; d.a = 0; }
+    else if (tok == "null") { d.kind = K_NULL; }
+    else if (rust_parse_i64(tok, iv)) { d.kind = K_INT; uint64_t u = (uint64_t)iv; d.a = (uint32_t)u; d.b = (uint32_t)(u >> 32); }
+    else { rust_parse_f64(tok, fv); d.kind = K_FLOAT; uint64_t u; memcpy(&u, &fv, 8); d.a = (uint32_t)u; d.b = (uint32_t)(u >> 32); }
+  }
+};
+
+}  // namespace
+
+// returns true when the document was loaded by the fast path; false leaves `b` unchanged
+static bool load_json_fast(DocBatch& b, const char* text, size_t len, const std::string& name) {
+  JsonFast p(text, len);
+  p.ws();
+  if (p.i >= len || (text[p.i] != '{' && text[p.i] != '[')) return false;
+  size_t start = p.i;
+  uint32_t sline = p.line, scol = p.col();
+  size_t sls = p.line_start;
+  if (!p.v1(0)) return false;
+  p.ws();
+  if (p.i != len) return false;
+  // pass 2
+  p.i = start; p.line = sline; p.line_start = sls; p.ci = 0;
+  uint32_t slot = (uint32_t)b.nodes.size();
+  size_t sz = slot + 1;
+  b.nodes.resize(sz); b.line.resize(sz); b.col.resize(sz); b.kline.resize(sz); b.kcol.resize(sz);
+  b.nodes[slot].key_off = NONE; b.nodes[slot].key_len = 0; b.nodes[slot].key_hash = 0;
+  bool list = text[start] == '[';
+  b.line[slot] = list ? 0 : sline; b.col[slot] = list ? 0 : scol;   // emit_root: lists keep Path::root()'s (0,0)
+  b.kline[slot] = 0; b.kcol[slot] = 0;
+  p.v2(b, slot, NONE);
+  b.roots.push_back(slot);
+  b.names.push_back(name);
+  return true;
+}
+
 bool load_document(DocBatch& b, const char* text, size_t len, const std::string& name, LoadMode mode, LoadError& err) {
   Tree t;
   uint32_t root = 0;
+  // u32 arena offsets: refuse a document that could push the pool or node count past the cap
+  if (b.bytes.size() + len > kMaxPoolBytes || b.nodes.size() + len + 1 > kMaxPoolBytes) {
+    err.kind = "IncompatibleError";
+    err.msg = "document batch is full (u32 arena offsets); evaluate it and start a new batch";
+    return false;
+  }
   if (mode == LOAD_LIBYAML) {
-    std::string tmp(text, len);
+    if (g_json_fast && load_json_fast(b, text, len, name)) return true;
     bool blank = true;
-    for (char c : tmp) if (!isspace((unsigned char)c)) { blank = false; break; }
+    for (size_t k = 0; k < len; k++) if (!isspace((unsigned char)text[k])) { blank = false; break; }
     if (blank) {
       err.kind = "ParseError";
       err.msg = "Unable to parse a template from data file: " + name + " is empty";
@@ -681,6 +982,23 @@ bool load_document(DocBatch& b, const char* text, size_t len, const std::string&
   }
   b.serde = true;
   return emit_root(b, t, root, name, true, err);
+}
+
+// test hook: 1 when the fast path accepts `text` and builds exactly the libyaml path's arena,
+// 0 when they differ, -1 when the fast path declines (or libyaml fails)
+int loader_selfcheck(const char* text, size_t len) {
+  DocBatch a, b;
+  LoadError e;
+  if (!load_json_fast(a, text, len, "x")) return -1;
+  bool saved = g_json_fast;
+  g_json_fast = false;
+  bool ok = load_document(b, text, len, "x", LOAD_LIBYAML, e);
+  g_json_fast = saved;
+  if (!ok) return -1;
+  if (a.nodes.size() != b.nodes.size() || a.bytes != b.bytes || a.roots != b.roots || a.line != b.line ||
+      a.col != b.col || a.kline != b.kline || a.kcol != b.kcol)
+    return 0;
+  return memcmp(a.nodes.data(), b.nodes.data(), a.nodes.size() * sizeof(DNode)) == 0 ? 1 : 0;
 }
 
 }  // namespace gg

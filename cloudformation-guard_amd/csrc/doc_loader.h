@@ -23,6 +23,13 @@ struct DocBatch {
   std::vector<uint32_t> roots;           // per document: root node
   std::vector<std::string> names;        // per document: data file name
   bool serde = false;                    // loaded by the serde (FFI) loader: key paths differ
+  // string pool interning: map keys and string scalars repeat heavily across templates
+  // ("Properties", "Type", "AWS::S3::Bucket"), so each distinct string is stored once per batch.
+  // Offsets are u32: a batch's pool is capped at kMaxPoolBytes (load_document fails beyond it).
+  std::vector<uint32_t> islots;          // open addressing: pool offset + 1 (0 = empty)
+  std::vector<uint32_t> ilen;            // parallel to islots: string length
+  size_t iused = 0;
+  uint32_t intern(const char* p, uint32_t n, uint32_t hash);
 
   size_t ndocs() const { return roots.size(); }
   std::string path(uint32_t node) const;  // JSON pointer ("" for a root)
@@ -30,9 +37,15 @@ struct DocBatch {
   void clear();
 };
 
+constexpr size_t kMaxPoolBytes = 0xF0000000u;
+
 enum LoadMode { LOAD_LIBYAML = 0, LOAD_SERDE = 1 };
 
 struct LoadError { std::string kind, msg; };
+
+// strict-JSON documents skip libyaml (identical arena; see doc_loader.cpp); tests switch it off
+extern bool g_json_fast;
+int loader_selfcheck(const char* text, size_t len);
 
 // Appends one document; returns false and fills err on failure (batch unchanged).
 bool load_document(DocBatch& b, const char* text, size_t len, const std::string& name,

@@ -1608,3 +1608,33 @@ __global__ void __launch_bounds__(64) guard_eval_kernel(LaunchArgs A) {
 }
 
 }  // namespace gg
+
+namespace gg {
+
+// Per-(rules file, top rule) PASS/FAIL/SKIP tallies over every tile of one evaluation, plus a
+// per-file line (index max_top) holding file statuses and errored tiles (status slot 3).
+// counts[((file * (max_top + 1) + rule) * 4) + status]; the same buffer is what the multi-GPU
+// path all-reduces over RCCL.  LDS-privatised so global atomics are per block.
+__global__ void __launch_bounds__(256) rule_count_kernel(const TileOut* tiles, const uint8_t* rule_status,
+                                                          const DevProg* progs, uint32_t nfiles, uint32_t ntiles,
+                                                          uint32_t max_top, unsigned long long* counts) {
+  extern __shared__ uint32_t lds_counts[];
+  const uint32_t ncount = nfiles * (max_top + 1) * 4;
+  for (uint32_t i = threadIdx.x; i < ncount; i += blockDim.x) lds_counts[i] = 0;
+  __syncthreads();
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < ntiles; t += gridDim.x * blockDim.x) {
+    uint32_t file = t % nfiles;
+    TileOut o = tiles[t];
+    uint32_t base = file * (max_top + 1) * 4;
+    if (o.err) { atomicAdd(&lds_counts[base + max_top * 4 + 3], 1u); continue; }
+    atomicAdd(&lds_counts[base + max_top * 4 + o.status], 1u);
+    uint32_t ntop = progs[file].n_top;
+    const uint8_t* rs = rule_status + (size_t)t * max_top;
+    for (uint32_t r = 0; r < ntop; r++) atomicAdd(&lds_counts[base + r * 4 + rs[r]], 1u);
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < ncount; i += blockDim.x)
+    if (lds_counts[i]) atomicAdd(&counts[i], (unsigned long long)lds_counts[i]);
+}
+
+}  // namespace gg

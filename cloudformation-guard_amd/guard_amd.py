@@ -66,6 +66,25 @@ def lib():
     L.gg_session_last_kernel_ms.argtypes = [ctypes.c_void_p]
     L.gg_session_last_kernel_ms.restype = ctypes.c_double
     L.gg_device_available.restype = ctypes.c_int32
+    L.gg_session_set_stream.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    L.gg_session_set_stream.restype = None
+    L.gg_session_launch.argtypes = [ctypes.c_void_p, ctypes.POINTER(ExternError)]
+    L.gg_session_wait.argtypes = [ctypes.c_void_p, ctypes.POINTER(ExternError)]
+    L.gg_session_wait.restype = ctypes.c_double
+    L.gg_session_fetch.argtypes = [ctypes.c_void_p, ctypes.POINTER(ExternError)]
+    L.gg_session_ncounts.argtypes = [ctypes.c_void_p]
+    L.gg_session_ncounts.restype = ctypes.c_size_t
+    L.gg_session_counts_device.argtypes = [ctypes.c_void_p]
+    L.gg_session_counts_device.restype = ctypes.c_void_p
+    L.gg_session_counts.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+    L.gg_session_bind_counts.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+    L.gg_session_bind_counts.restype = None
+    L.gg_session_drain_kernel_ms.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ExternError)]
+    L.gg_session_drain_kernel_ms.restype = ctypes.c_size_t
+    L.gg_synth_cfn_doc.argtypes = [ctypes.c_uint64, ctypes.c_int32, ctypes.c_char_p, ctypes.c_size_t]
+    L.gg_synth_cfn_doc.restype = ctypes.c_size_t
+    L.gg_session_add_synthetic.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_int32,
+                                           ctypes.c_int32, ctypes.POINTER(ExternError)]
     _lib = L
     return L
 
@@ -174,8 +193,66 @@ class Session:
         lib().gg_session_tile_status(self.s, buf, n)
         return bytes(buf)
 
+    def add_synthetic(self, first, n, n_resources=50, threads=8):
+        """Appends synthetic templates first..first+n-1 (synth.cfn_doc), generated and loaded natively."""
+        err = ExternError()
+        lib().gg_session_add_synthetic(self.s, first, n, n_resources, threads, ctypes.byref(err))
+        if err.code != 0:
+            _raise(err)
+
+    def set_stream(self, stream_handle):
+        lib().gg_session_set_stream(self.s, ctypes.c_void_p(stream_handle))
+
+    def _call(self, fn):
+        err = ExternError()
+        r = fn(self.s, ctypes.byref(err))
+        if err.code != 0:
+            _raise(err)
+        return r
+
+    def launch(self):
+        self._call(lib().gg_session_launch)
+
+    def wait(self):
+        return self._call(lib().gg_session_wait)
+
+    def fetch(self):
+        self._call(lib().gg_session_fetch)
+
+    def ncounts(self):
+        return lib().gg_session_ncounts(self.s)
+
+    def counts_device_ptr(self):
+        return lib().gg_session_counts_device(self.s)
+
+    def bind_counts(self, dev_ptr, n):
+        lib().gg_session_bind_counts(self.s, ctypes.c_void_p(dev_ptr), n)
+
+    def drain_kernel_ms(self, cap=4096):
+        buf = (ctypes.c_double * cap)()
+        err = ExternError()
+        n = lib().gg_session_drain_kernel_ms(self.s, buf, cap, ctypes.byref(err))
+        if err.code != 0:
+            _raise(err)
+        return list(buf)[:min(n, cap)]
+
+    def counts(self):
+        n = self.ncounts()
+        buf = (ctypes.c_uint64 * max(1, n))()
+        lib().gg_session_counts(self.s, buf, n)
+        return list(buf)[:n]
+
     STAT = {"ndocs": 0, "nfiles": 1, "nodes": 2, "bytes": 3, "fail": 4, "pass": 5, "skip": 6, "errors": 7,
-            "records": 8, "arena_bytes": 9, "first_error": 10}
+            "records": 8, "arena_bytes": 9, "first_error": 10, "record_bytes": 11, "record_cap": 12,
+            "max_top": 13, "slots": 14, "heap_bytes": 15}
+
+
+def synth_cfn_doc(index, n_resources=50):
+    """Native synthetic template text (byte-identical to synth.cfn_doc; no GPU needed)."""
+    n = lib().gg_synth_cfn_doc(index, n_resources, None, 0)
+    buf = ctypes.create_string_buffer(n + 1)
+    lib().gg_synth_cfn_doc(index, n_resources, buf, n + 1)
+    return buf.value.decode("utf-8")
 
 
 def device_available():

@@ -58,6 +58,31 @@ int32_t gg_session_tile_status(gg_session *s, uint8_t *out, size_t n);
 double gg_session_last_kernel_ms(gg_session *s);
 int32_t gg_device_available(void);
 
+/* Asynchronous evaluation on a caller stream (bench.py passes torch's current stream). */
+void gg_session_set_stream(gg_session *s, void *hip_stream);
+int32_t gg_session_launch(gg_session *s, extern_err_t *err);  /* enqueue; no host sync */
+double gg_session_wait(gg_session *s, extern_err_t *err);     /* kernel ms of the last launch */
+int32_t gg_session_fetch(gg_session *s, extern_err_t *err);   /* statuses + records to host */
+/* Per (rules file, top rule) x {PASS, FAIL, SKIP, error} u64 tallies of the last launch; index
+ * ((file * (max_top + 1) + rule) * 4 + status), rule == max_top is the file-level line.  The
+ * device buffer is what the multi-GPU path all-reduces over RCCL. */
+size_t gg_session_ncounts(gg_session *s);
+void *gg_session_counts_device(gg_session *s);
+/* write tallies into a caller-owned device buffer of >= ncounts u64 (NULL: internal buffer) */
+void gg_session_bind_counts(gg_session *s, void *dev, size_t n);
+/* evaluation-kernel ms of every launch since the last drain (HIP events on the launch stream) */
+size_t gg_session_drain_kernel_ms(gg_session *s, double *out, size_t cap, extern_err_t *err);
+int32_t gg_session_counts(gg_session *s, uint64_t *out, size_t n);
+
+/* Loader self-check (tests): 1 = JSON fast path builds the libyaml path's exact arena,
+ * 0 = they differ, -1 = fast path declined the document. */
+int32_t gg_loader_selfcheck(const char *text, size_t len);
+
+/* Synthetic CloudFormation corpus (BASELINE configs[1]); byte-identical to synth.py cfn_doc. */
+size_t gg_synth_cfn_doc(uint64_t index, int32_t n_resources, char *buf, size_t cap);
+int32_t gg_session_add_synthetic(gg_session *s, uint64_t first, size_t n, int32_t n_resources, int32_t nthreads,
+                                 extern_err_t *err);
+
 #ifdef __cplusplus
 }
 #endif
