@@ -28,6 +28,7 @@
 
 namespace gg {
 __global__ void guard_eval_kernel(LaunchArgs A);
+__global__ void guard_eval_lanes_kernel(LaunchArgs A);
 __global__ void rule_count_kernel(const TileOut* tiles, const uint8_t* rule_status, const DevProg* progs, uint32_t nfiles,
                                   uint32_t ntiles, uint32_t max_top, unsigned long long* counts);
 }
@@ -151,8 +152,11 @@ struct gg_session {
   DBuf<DNode> d_nodes;
   DBuf<char> d_bytes;
   DBuf<uint32_t> d_roots;
+  DBuf<uint64_t> d_base;
   DBuf<DevProg> d_progs;
-  DBuf<uint8_t> d_heaps;
+  DBuf<uint8_t> d_heaps;        // wave mode: one heap per wave slot
+  DBuf<uint8_t> d_lane_heaps;   // lane mode: one heap per lane
+  DBuf<uint32_t> d_retry;       // tiles handed from lane mode to wave mode
   DBuf<TileOut> d_tiles;
   DBuf<uint8_t> d_rule_status;
   DBuf<Rec> d_recs;
@@ -168,8 +172,11 @@ struct gg_session {
   std::vector<unsigned long long> counts;
   bool uploaded = false;
   uint32_t max_top = 1;
-  uint32_t nslots = 0;
+  uint32_t nslots = 0;            // wave-mode grid
+  uint32_t lane_slots = 0;        // lane-mode grid (waves)
   uint32_t heap_bytes = 512 * 1024;
+  uint32_t lane_heap_bytes = 64 * 1024;
+  int32_t mode = 0;               // 0: lane mode + wave-mode retry; 1: wave mode only
   size_t rec_cap = 0;
   // results
   std::vector<TileOut> tiles;
@@ -193,6 +200,7 @@ void session_upload(gg_session* s) {
   s->d_nodes.upload(s->docs.nodes.data(), s->docs.nodes.size(), st);
   s->d_bytes.upload(s->docs.bytes.data(), s->docs.bytes.size() ? s->docs.bytes.size() : 1, st);
   s->d_roots.upload(s->docs.roots.data(), s->docs.roots.size(), st);
+  s->d_base.upload(s->docs.base.data(), s->docs.base.size(), st);
   std::vector<DevProg> dps;
   s->max_top = 1;
   for (auto& p : s->progs) {
@@ -202,9 +210,15 @@ void session_upload(gg_session* s) {
   }
   s->d_progs.upload(dps.data(), dps.size(), st);
   size_t ntiles = s->docs.ndocs() * s->progs.size();
-  uint32_t slots = (uint32_t)std::min<size_t>(std::max<size_t>(ntiles, 1), (size_t)g_dev.ncu * 8);
+  size_t nbatches = (s->docs.ndocs() + 63) / 64 * s->progs.size();
+  // wave mode: all tiles (mode 1) or only the lane kernel's overflow tiles (mode 0)
+  size_t wave_slots = s->mode == 1 ? (size_t)g_dev.ncu * 8 : (size_t)g_dev.ncu * 2;
+  uint32_t slots = (uint32_t)std::min<size_t>(std::max<size_t>(ntiles, 1), wave_slots);
   s->nslots = slots;
   s->d_heaps.alloc((size_t)slots * s->heap_bytes);
+  s->lane_slots = s->mode == 1 ? 0 : (uint32_t)std::min<size_t>(std::max<size_t>(nbatches, 1), (size_t)g_dev.ncu * 8);
+  s->d_lane_heaps.alloc((size_t)s->lane_slots * 64 * s->lane_heap_bytes);
+  s->d_retry.alloc(std::max<size_t>(ntiles, 1));
   s->d_tiles.alloc(std::max<size_t>(ntiles, 1));
   s->d_rule_status.alloc(std::max<size_t>(ntiles * s->max_top, 1));
   s->rec_cap = std::min<size_t>(std::max<size_t>(ntiles * 48, 4096), (size_t)96 * 1024 * 1024);
@@ -228,13 +242,16 @@ void session_launch(gg_session* s) {
   unsigned long long* counts = s->ext_counts ? s->ext_counts : s->d_counts.p;
   HIPCHK(hipMemsetAsync(counts, 0, s->ncounts * sizeof(unsigned long long), st));
   LaunchArgs A{};
-  A.docs.nodes = s->d_nodes.p; A.docs.bytes = s->d_bytes.p; A.docs.roots = s->d_roots.p; A.docs.ndocs = (uint32_t)s->docs.ndocs();
+  A.docs.nodes = s->d_nodes.p; A.docs.bytes = s->d_bytes.p; A.docs.roots = s->d_roots.p; A.docs.base = s->d_base.p; A.docs.ndocs = (uint32_t)s->docs.ndocs();
   A.progs = s->d_progs.p; A.nfiles = (uint32_t)s->progs.size();
   A.ntiles = ntiles; A.tile_base = 0;
   A.heaps = s->d_heaps.p; A.heap_bytes = s->heap_bytes; A.nslots = s->nslots;
   A.tiles = s->d_tiles.p; A.rule_status = s->d_rule_status.p; A.max_top = s->max_top;
   A.recs = s->d_recs.p; A.rec_cap = (uint32_t)s->rec_cap;
-  A.rec_cursor = s->d_counters.p; A.tile_cursor = s->d_counters.p + 1;
+  A.rec_cursor = s->d_counters.p; A.tile_cursor = s->d_counters.p + 1;   // [1] lane batches, [2] wave tiles
+  A.retry_count = s->d_counters.p + 3;
+  A.lane_heaps = s->d_lane_heaps.p; A.lane_heap_bytes = s->lane_heap_bytes;
+  A.retry_list = s->mode == 1 ? nullptr : s->d_retry.p;
   if (!ntiles) return;
   if (s->nq == s->evq.size()) {
     std::pair<hipEvent_t, hipEvent_t> pr;
@@ -244,6 +261,10 @@ void session_launch(gg_session* s) {
   }
   s->ev0 = s->evq[s->nq].first; s->ev1 = s->evq[s->nq].second; s->nq++;
   HIPCHK(hipEventRecord(s->ev0, st));
+  if (s->mode != 1) {
+    hipLaunchKernelGGL(guard_eval_lanes_kernel, dim3(s->lane_slots), dim3(64), 0, st, A);
+    HIPCHK(hipGetLastError());
+  }
   hipLaunchKernelGGL(guard_eval_kernel, dim3(s->nslots), dim3(64), 0, st, A);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(s->ev1, st));
@@ -327,7 +348,7 @@ bool session_report(gg_session* s, std::string& out, int32_t& exit_code, ReportE
   // the first tile in (doc, rules-file) order that raised an error aborts the run (structured.rs:110)
   for (size_t t = 0; t < s->tiles.size(); t++) {
     if (s->tiles[t].err) {
-      tile_error(s->docs, *progs[t % nf], s->tiles[t], err);
+      tile_error(s->docs, (uint32_t)(t / nf), *progs[t % nf], s->tiles[t], err);
       exit_code = -1;
       return false;
     }
@@ -377,23 +398,24 @@ void merge_batches(DocBatch& dst, std::vector<DocBatch>& parts) {
     bbase[t + 1] = bbase[t] + parts[t].bytes.size();
     rbase[t + 1] = rbase[t] + parts[t].roots.size();
   }
-  if (bbase[np] > kMaxPoolBytes || nbase[np] > kMaxPoolBytes)
-    throw std::runtime_error("document batch is full (u32 arena offsets); evaluate it and start a new batch");
+  if (bbase[np] > kMaxPoolBytes)
+    throw std::runtime_error("document batch is full (u32 string-pool offsets); evaluate it and start a new batch");
   dst.nodes.resize(nbase[np]); dst.line.resize(nbase[np]); dst.col.resize(nbase[np]);
   dst.kline.resize(nbase[np]); dst.kcol.resize(nbase[np]);
   dst.bytes.resize(bbase[np]);
   dst.roots.resize(rbase[np]);
+  dst.base.resize(rbase[np]);
   for (auto& p : parts) if (p.serde) dst.serde = true;
+  // node indices are document-relative, so only string-pool offsets and document bases move
   auto work = [&](size_t t) {
     const DocBatch& src = parts[t];
-    uint32_t nb = (uint32_t)nbase[t], bb = (uint32_t)bbase[t];
+    uint32_t bb = (uint32_t)bbase[t];
+    size_t nb = nbase[t];
     DNode* out = dst.nodes.data() + nb;
     for (size_t i = 0; i < src.nodes.size(); i++) {
       DNode n = src.nodes[i];
-      if (n.kind == K_LIST || n.kind == K_MAP) n.a += nb;
-      else if (n.kind == K_STRING) n.a += bb;
+      if (n.kind == K_STRING) n.a += bb;
       if (n.key_off != NONE) n.key_off += bb;
-      if (n.parent != NONE) n.parent += nb;
       out[i] = n;
     }
     size_t nn = src.nodes.size() * sizeof(uint32_t);
@@ -404,7 +426,10 @@ void merge_batches(DocBatch& dst, std::vector<DocBatch>& parts) {
       memcpy(dst.kcol.data() + nb, src.kcol.data(), nn);
     }
     if (!src.bytes.empty()) memcpy(&dst.bytes[bb], src.bytes.data(), src.bytes.size());
-    for (size_t r = 0; r < src.roots.size(); r++) dst.roots[rbase[t] + r] = src.roots[r] + nb;
+    for (size_t r = 0; r < src.roots.size(); r++) {
+      dst.roots[rbase[t] + r] = src.roots[r];
+      dst.base[rbase[t] + r] = src.base[r] + nb;
+    }
   };
   std::vector<std::thread> th;
   for (size_t t = 1; t < np; t++) th.emplace_back(work, t);
@@ -473,7 +498,7 @@ char* cfn_guard_run_checks(validate_input_t data, validate_input_t rules, bool v
     session_run(&s, true);
     if (s.tiles[0].err) {
       ReportError re;
-      tile_error(s.docs, s.progs[0]->prog, s.tiles[0], re);
+      tile_error(s.docs, 0, s.progs[0]->prog, s.tiles[0], re);
       set_err(err, ffi_code(re.kind), error_display(re.kind, re.msg));
       return nullptr;
     }
@@ -547,6 +572,15 @@ void gg_session_free(gg_session* s) {
 }
 
 void gg_session_set_stream(gg_session* s, void* stream) { s->stream = (hipStream_t)stream; }
+
+int32_t gg_session_configure(gg_session* s, int32_t mode, uint32_t lane_heap_bytes) {
+  if (mode != 0 && mode != 1) return -1;
+  if (lane_heap_bytes && lane_heap_bytes < 32 * 1024) return -1;   // frames + record staging + tables
+  s->mode = mode;
+  if (lane_heap_bytes) s->lane_heap_bytes = lane_heap_bytes;
+  s->uploaded = false;
+  return 0;
+}
 
 int32_t gg_session_launch(gg_session* s, extern_err_t* err) {
   set_err(err, 0, "");
@@ -724,13 +758,19 @@ int64_t gg_session_stat(gg_session* s, int32_t what) {
     }
     case 7: { int64_t c = 0; for (auto& t : s->tiles) if (t.err) c++; return c; }
     case 8: return (int64_t)s->recs.size();
-    case 9: return (int64_t)(s->docs.nodes.size() * sizeof(DNode) + s->docs.bytes.size() + s->docs.roots.size() * 4);
+    case 9: return (int64_t)(s->docs.nodes.size() * sizeof(DNode) + s->docs.bytes.size() + s->docs.roots.size() * 12);
     case 10: for (auto& t : s->tiles) if (t.err) return t.err; return 0;
     case 11: return (int64_t)s->recs.size() * (int64_t)sizeof(Rec);
     case 12: return (int64_t)s->rec_cap;
     case 13: return (int64_t)s->max_top;
     case 14: return (int64_t)s->nslots;
     case 15: return (int64_t)s->heap_bytes;
+    case 16: {   // tiles the lane kernel handed to wave mode in the last launch
+      uint32_t v = 0;
+      if (s->d_counters.p) HIPCHK(hipMemcpy(&v, s->d_counters.p + 3, 4, hipMemcpyDeviceToHost));
+      return v;
+    }
+    case 17: return (int64_t)s->lane_slots;
     default: return -1;
   }
 }

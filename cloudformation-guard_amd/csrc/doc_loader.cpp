@@ -207,14 +207,17 @@ uint32_t serde_yaml_scalar(Tree& t, const std::string& val, bool plain) {
   n.kind = K_STRING; n.s = val; return t.add(std::move(n));
 }
 
+constexpr size_t kNoParent = ~(size_t)0;
+
 struct Emitter {
   DocBatch& b;
   Tree& t;
   bool serde;
-  void fill(uint32_t ti, uint32_t slot, uint32_t parent, uint32_t line, uint32_t col) {
+  uint64_t base;   // global index of the document's first node; stored indices are relative
+  void fill(uint32_t ti, size_t slot, size_t parent, uint32_t line, uint32_t col) {
     TN& n = t.n[ti];
     DNode& d = b.nodes[slot];
-    d.kind = n.kind; d.count = 0; d.a = 0; d.b = 0; d.parent = parent;
+    d.kind = n.kind; d.count = 0; d.a = 0; d.b = 0; d.parent = parent == kNoParent ? NONE : (uint32_t)(parent - base);
     b.line[slot] = line; b.col[slot] = col;
     switch (n.kind) {
       case K_STRING: {
@@ -228,10 +231,10 @@ struct Emitter {
       case K_FLOAT: { uint64_t u; memcpy(&u, &n.f, 8); d.a = (uint32_t)u; d.b = (uint32_t)(u >> 32); break; }
       case K_LIST: {
         uint32_t cnt = (uint32_t)n.kids.size();
-        uint32_t first = (uint32_t)b.nodes.size();
+        size_t first = b.nodes.size();
         grow(cnt);
         DNode& dd = b.nodes[slot];
-        dd.a = first; dd.count = cnt;
+        dd.a = (uint32_t)(first - base); dd.count = cnt;
         for (uint32_t j = 0; j < cnt; j++) {
           uint32_t k = t.n[ti].kids[j];
           const TN& kn = t.n[k];
@@ -256,10 +259,10 @@ struct Emitter {
           }
         }
         uint32_t cnt = (uint32_t)keys.size();
-        uint32_t first = (uint32_t)b.nodes.size();
+        size_t first = b.nodes.size();
         grow(cnt);
         DNode& dd = b.nodes[slot];
-        dd.a = first; dd.count = cnt;
+        dd.a = (uint32_t)(first - base); dd.count = cnt;
         for (uint32_t j = 0; j < cnt; j++) {
           DNode& c = b.nodes[first + j];
           c.key_len = (uint32_t)keys[j].size();
@@ -295,16 +298,18 @@ bool check_bad(const Tree& t, uint32_t ti, LoadError& err) {
 
 bool emit_root(DocBatch& b, Tree& t, uint32_t root, const std::string& name, bool serde, LoadError& err) {
   if (!check_bad(t, root, err)) return false;
-  Emitter e{b, t, serde};
-  uint32_t slot = (uint32_t)b.nodes.size();
+  if (t.n.size() > kMaxDocNodes) { err.kind = "IncompatibleError"; err.msg = "document too large for the MI355X arena"; return false; }
+  size_t slot = b.nodes.size();
+  Emitter e{b, t, serde, (uint64_t)slot};
   e.grow(1);
   b.nodes[slot].key_off = NONE; b.nodes[slot].key_len = 0; b.nodes[slot].key_hash = 0;
   const TN& r = t.n[root];
   uint32_t line = 0, col = 0;
   // root: Path::root() (L0,C0) keeps its location for lists; maps/scalars take their own mark
   if (!serde && r.kind != K_LIST) { line = r.line; col = r.col; }
-  e.fill(root, slot, NONE, line, col);
-  b.roots.push_back(slot);
+  e.fill(root, slot, kNoParent, line, col);
+  b.roots.push_back(0);
+  b.base.push_back(slot);
   b.names.push_back(name);
   return true;
 }
@@ -625,7 +630,7 @@ struct JsonP {
 }  // namespace
 
 void DocBatch::clear() {
-  islots.clear(); ilen.clear(); iused = 0;
+  islots.clear(); ilen.clear(); iused = 0; base.clear();
   nodes.clear(); bytes.clear(); line.clear(); col.clear(); kline.clear(); kcol.clear(); roots.clear(); names.clear();
   serde = false;
 }
@@ -655,13 +660,14 @@ uint32_t DocBatch::intern(const char* p, uint32_t n, uint32_t hash) {
   return off;
 }
 
-std::string DocBatch::path(uint32_t node) const {
+std::string DocBatch::path(uint64_t base, uint32_t node) const {
   std::vector<std::string> parts;
+  const DNode* N = nodes.data() + base;
   uint32_t cur = node;
-  while (nodes[cur].parent != NONE) {
-    uint32_t p = nodes[cur].parent;
-    if (nodes[p].kind == K_MAP) parts.push_back(bytes.substr(nodes[cur].key_off, nodes[cur].key_len));
-    else parts.push_back(std::to_string(cur - nodes[p].a));
+  while (N[cur].parent != NONE) {
+    uint32_t p = N[cur].parent;
+    if (N[p].kind == K_MAP) parts.push_back(bytes.substr(N[cur].key_off, N[cur].key_len));
+    else parts.push_back(std::to_string(cur - N[p].a));
     cur = p;
   }
   std::string out;
@@ -669,8 +675,8 @@ std::string DocBatch::path(uint32_t node) const {
   return out;
 }
 
-std::string DocBatch::path_display(uint32_t node) const {
-  return path(node) + "[L:" + std::to_string(line[node]) + ",C:" + std::to_string(col[node]) + "]";
+std::string DocBatch::path_display(uint64_t base, uint32_t node) const {
+  return path(base, node) + "[L:" + std::to_string(line[base + node]) + ",C:" + std::to_string(col[base + node]) + "]";
 }
 
 
@@ -849,8 +855,10 @@ struct JsonFast {
     return true;
   }
 
-  // pass 2: emit into the arena; `slot` already allocated by the parent
-  void v2(DocBatch& b, uint32_t slot, uint32_t parent) {
+  // pass 2: emit into the arena; `slot` already allocated by the parent (global index);
+  // stored child/parent indices are relative to the document's first node `dbase`
+  uint64_t dbase = 0;
+  void v2(DocBatch& b, size_t slot, uint32_t parent) {
     DNode& d = b.nodes[slot];
     d.parent = parent;
     d.count = 0; d.a = 0; d.b = 0;
@@ -866,16 +874,16 @@ struct JsonFast {
     if (c == '{' || c == '[') {
       bool map = c == '{';
       uint32_t cnt = counts[ci++];
-      uint32_t first = (uint32_t)b.nodes.size();
+      size_t first = b.nodes.size();
       size_t sz = first + (size_t)cnt;
       b.nodes.resize(sz); b.line.resize(sz); b.col.resize(sz); b.kline.resize(sz); b.kcol.resize(sz);
       DNode& dd = b.nodes[slot];
       dd.kind = map ? K_MAP : K_LIST;
-      dd.a = first; dd.count = cnt;
+      dd.a = (uint32_t)(first - dbase); dd.count = cnt;
       i++;
       ws();
       for (uint32_t j = 0; j < cnt; j++) {
-        uint32_t cs = first + j;
+        size_t cs = first + j;
         if (map) {
           uint32_t kl = line, kc = col();
           str(true);
@@ -893,7 +901,7 @@ struct JsonFast {
           b.kline[cs] = 0; b.kcol[cs] = 0;
         }
         b.line[cs] = line; b.col[cs] = col();
-        v2(b, cs, slot);
+        v2(b, cs, (uint32_t)(slot - dbase));
         ws();
         i++;  // ',' or the closing bracket
         ws();
@@ -926,9 +934,11 @@ static bool load_json_fast(DocBatch& b, const char* text, size_t len, const std:
   if (!p.v1(0)) return false;
   p.ws();
   if (p.i != len) return false;
+  if (len + 1 > kMaxDocNodes) return false;
   // pass 2
   p.i = start; p.line = sline; p.line_start = sls; p.ci = 0;
-  uint32_t slot = (uint32_t)b.nodes.size();
+  size_t slot = b.nodes.size();
+  p.dbase = slot;
   size_t sz = slot + 1;
   b.nodes.resize(sz); b.line.resize(sz); b.col.resize(sz); b.kline.resize(sz); b.kcol.resize(sz);
   b.nodes[slot].key_off = NONE; b.nodes[slot].key_len = 0; b.nodes[slot].key_hash = 0;
@@ -936,7 +946,8 @@ static bool load_json_fast(DocBatch& b, const char* text, size_t len, const std:
   b.line[slot] = list ? 0 : sline; b.col[slot] = list ? 0 : scol;   // emit_root: lists keep Path::root()'s (0,0)
   b.kline[slot] = 0; b.kcol[slot] = 0;
   p.v2(b, slot, NONE);
-  b.roots.push_back(slot);
+  b.roots.push_back(0);
+  b.base.push_back(slot);
   b.names.push_back(name);
   return true;
 }
@@ -945,7 +956,7 @@ bool load_document(DocBatch& b, const char* text, size_t len, const std::string&
   Tree t;
   uint32_t root = 0;
   // u32 arena offsets: refuse a document that could push the pool or node count past the cap
-  if (b.bytes.size() + len > kMaxPoolBytes || b.nodes.size() + len + 1 > kMaxPoolBytes) {
+  if (b.bytes.size() + len > kMaxPoolBytes) {
     err.kind = "IncompatibleError";
     err.msg = "document batch is full (u32 arena offsets); evaluate it and start a new batch";
     return false;
@@ -995,7 +1006,7 @@ int loader_selfcheck(const char* text, size_t len) {
   bool ok = load_document(b, text, len, "x", LOAD_LIBYAML, e);
   g_json_fast = saved;
   if (!ok) return -1;
-  if (a.nodes.size() != b.nodes.size() || a.bytes != b.bytes || a.roots != b.roots || a.line != b.line ||
+  if (a.nodes.size() != b.nodes.size() || a.bytes != b.bytes || a.roots != b.roots || a.base != b.base || a.line != b.line ||
       a.col != b.col || a.kline != b.kline || a.kcol != b.kcol)
     return 0;
   return memcmp(a.nodes.data(), b.nodes.data(), a.nodes.size() * sizeof(DNode)) == 0 ? 1 : 0;

@@ -20,7 +20,11 @@ struct DocBatch {
   std::string bytes;
   std::vector<uint32_t> line, col;       // per node mark (PathAwareValue location)
   std::vector<uint32_t> kline, kcol;     // per map-entry node: its key's mark
-  std::vector<uint32_t> roots;           // per document: root node
+  // Node indices inside a document are DOCUMENT-RELATIVE (child/parent fields, roots, records):
+  // doc k's nodes are nodes[base[k] .. base[k+1]) and its root is nodes[base[k] + roots[k]].
+  // The literal arena of a compiled rules file has no `base` (one implicit document at 0).
+  std::vector<uint32_t> roots;           // per document: root node (relative; 0 for loaded docs)
+  std::vector<uint64_t> base;            // per document: global index of its first node
   std::vector<std::string> names;        // per document: data file name
   bool serde = false;                    // loaded by the serde (FFI) loader: key paths differ
   // string pool interning: map keys and string scalars repeat heavily across templates
@@ -32,12 +36,13 @@ struct DocBatch {
   uint32_t intern(const char* p, uint32_t n, uint32_t hash);
 
   size_t ndocs() const { return roots.size(); }
-  std::string path(uint32_t node) const;  // JSON pointer ("" for a root)
-  std::string path_display(uint32_t node) const;  // "{pointer}[L:{line},C:{col}]"
+  std::string path(uint64_t base, uint32_t node) const;  // JSON pointer ("" for a root)
+  std::string path_display(uint64_t base, uint32_t node) const;  // "{pointer}[L:{line},C:{col}]"
   void clear();
 };
 
 constexpr size_t kMaxPoolBytes = 0xF0000000u;
+constexpr size_t kMaxDocNodes = 0x1FFFFFFFu;   // relative refs share a u32 with the LIT/SYN/KEY flag bits
 
 enum LoadMode { LOAD_LIBYAML = 0, LOAD_SERDE = 1 };
 

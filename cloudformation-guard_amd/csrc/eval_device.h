@@ -39,7 +39,8 @@ struct DevProg {
 struct DevBatch {
   const DNode* nodes;
   const char* bytes;
-  const uint32_t* roots;   // per doc
+  const uint32_t* roots;   // per doc: root node (document-relative)
+  const uint64_t* base;    // per doc: global index of the document's first node
   uint32_t ndocs;
 };
 
@@ -58,7 +59,11 @@ struct LaunchArgs {
   Rec* recs;               // global record arena
   uint32_t rec_cap;
   uint32_t* rec_cursor;    // atomic bump
-  uint32_t* tile_cursor;   // atomic work queue
+  uint32_t* tile_cursor;   // atomic work queues: [0] lane-mode batches, [1] wave-mode tiles
+  uint8_t* lane_heaps;     // lane mode: per lane scratch
+  uint32_t lane_heap_bytes;
+  uint32_t* retry_list;    // tiles the lane kernel hands to the wave kernel (null: wave kernel runs all)
+  uint32_t* retry_count;
 };
 
 }  // namespace gg

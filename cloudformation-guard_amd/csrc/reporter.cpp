@@ -87,39 +87,42 @@ struct R {
   const DocBatch& docs;
   const Program& prog;
   bool serde;
+  uint64_t dbase;   // global index of the reported document's first node (refs are relative)
 
   static const uint32_t KEY_BIT = 0x20000000u;   // "the key of map entry X" (MapValue.keys)
   const DocBatch& B(uint32_t ref) const { return (ref & LIT_BIT) ? prog.lit : docs; }
   uint32_t I(uint32_t ref) const { return ref & ~(LIT_BIT | KEY_BIT); }
+  uint64_t base_of(uint32_t ref) const { return (ref & LIT_BIT) ? 0 : dbase; }
+  uint64_t G(uint32_t ref) const { return base_of(ref) + I(ref); }
   bool is_key(uint32_t ref) const { return (ref & KEY_BIT) != 0; }
   // key refs read as a String node whose bytes are the entry's key
   DNode key_node(uint32_t ref) const {
-    const DNode& e = B(ref).nodes[I(ref)];
+    const DNode& e = B(ref).nodes[G(ref)];
     DNode d; d.kind = K_STRING; d.count = e.key_len; d.a = e.key_off; d.b = e.key_hash;
     d.key_off = NONE; d.key_len = 0; d.key_hash = 0; d.parent = NONE;
     return d;
   }
-  DNode N(uint32_t ref) const { return is_key(ref) ? key_node(ref) : B(ref).nodes[I(ref)]; }
+  DNode N(uint32_t ref) const { return is_key(ref) ? key_node(ref) : B(ref).nodes[G(ref)]; }
   std::string str(uint32_t ref) const { DNode n = N(ref); return B(ref).bytes.substr(n.a, n.count); }
   std::string key(uint32_t ref) const { DNode n = N(ref); return B(ref).bytes.substr(n.key_off, n.key_len); }
   uint32_t child(uint32_t ref, uint32_t j) const { return (ref & LIT_BIT) | (N(ref).a + j); }
   // key PV paths: libyaml loader -> the map's path at the key mark (path_value.rs:467-470);
   // serde loader / rule literals -> map path + "/key" at the map's (0,0) location (:391-395)
   bool key_serde(uint32_t ref) const { return (ref & LIT_BIT) || docs.serde; }
-  uint32_t parent_of(uint32_t ref) const { return B(ref).nodes[I(ref)].parent; }
+  uint32_t parent_of(uint32_t ref) const { return B(ref).nodes[G(ref)].parent; }
   std::string path(uint32_t ref) const {
-    if (!is_key(ref)) return B(ref).path(I(ref));
-    std::string mp = B(ref).path(parent_of(ref));
-    if (key_serde(ref)) { const DNode& e = B(ref).nodes[I(ref)]; return mp + "/" + B(ref).bytes.substr(e.key_off, e.key_len); }
+    if (!is_key(ref)) return B(ref).path(base_of(ref), I(ref));
+    std::string mp = B(ref).path(base_of(ref), parent_of(ref));
+    if (key_serde(ref)) { const DNode& e = B(ref).nodes[G(ref)]; return mp + "/" + B(ref).bytes.substr(e.key_off, e.key_len); }
     return mp;
   }
   uint32_t line(uint32_t ref) const {
-    if (!is_key(ref)) return B(ref).line[I(ref)];
-    return key_serde(ref) ? 0 : B(ref).kline[I(ref)];
+    if (!is_key(ref)) return B(ref).line[G(ref)];
+    return key_serde(ref) ? 0 : B(ref).kline[G(ref)];
   }
   uint32_t col(uint32_t ref) const {
-    if (!is_key(ref)) return B(ref).col[I(ref)];
-    return key_serde(ref) ? 0 : B(ref).kcol[I(ref)];
+    if (!is_key(ref)) return B(ref).col[G(ref)];
+    return key_serde(ref) ? 0 : B(ref).kcol[G(ref)];
   }
   std::string loc(uint32_t l, uint32_t c) const { return "[L:" + std::to_string(l) + ",C:" + std::to_string(c) + "]"; }
   std::string path_display(uint32_t ref) const { return path(ref) + loc(line(ref), col(ref)); }
@@ -210,7 +213,7 @@ struct R {
           // MapValue.keys: libyaml mode -> parent path at the key mark; serde mode -> path/key at L0,C0
           bool lit = (ref & LIT_BIT) != 0;
           if (serde || lit) keys += "String((" + dbg_path(mp + "/" + k, 0, 0) + ", " + rust_debug_str(k) + "))";
-          else keys += "String((" + dbg_path(mp, B(c).kline[I(c)], B(c).kcol[I(c)]) + ", " + rust_debug_str(k) + "))";
+          else keys += "String((" + dbg_path(mp, B(c).kline[G(c)], B(c).kcol[G(c)]) + ", " + rust_debug_str(k) + "))";
           vals += rust_debug_str(k) + ": " + debug(c);
         }
         return "Map((" + p + ", MapValue { keys: [" + keys + "], values: {" + vals + "} }))";
@@ -551,9 +554,9 @@ std::string error_display(const std::string& kind, const std::string& msg) {
   return msg;
 }
 
-void tile_error(const DocBatch& docs, const Program& prog, const TileOut& t, ReportError& err) {
+void tile_error(const DocBatch& docs, uint32_t doc, const Program& prog, const TileOut& t, ReportError& err) {
   err.set = true;
-  R r{docs, prog, docs.serde};
+  R r{docs, prog, docs.serde, docs.base.empty() ? 0 : docs.base[doc]};
   switch (t.err) {
     case E_EMPTY_INCOMPATIBLE:
       err.kind = "IncompatibleError";
@@ -621,8 +624,8 @@ bool report_document(const DocBatch& docs, uint32_t doc, const std::vector<const
     for (size_t f = 0; f < progs.size(); f++) {
       const Program& P = *progs[f];
       const TileResult& T = *tiles[f];
-      if (T.out.err) { tile_error(docs, P, T.out, err); return false; }
-      R r{docs, P, docs.serde};
+      if (T.out.err) { tile_error(docs, doc, P, T.out, err); return false; }
+      R r{docs, P, docs.serde, docs.base[doc]};
       Walker w{r, T.recs};
       J items = w.items(0xFFFFFFFFu);
       for (auto& it : items.a) not_compliant.push(std::move(it));

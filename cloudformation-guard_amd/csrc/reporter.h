@@ -26,7 +26,7 @@ bool report_document(const DocBatch& docs, uint32_t doc, const std::vector<const
                      const std::vector<const TileResult*>& tiles, int indent, std::string& out, ReportError& err);
 
 // error text for a tile error (Error Display, guard/src/rules/errors.rs:11-54)
-void tile_error(const DocBatch& docs, const Program& prog, const TileOut& t, ReportError& err);
+void tile_error(const DocBatch& docs, uint32_t doc, const Program& prog, const TileOut& t, ReportError& err);
 
 std::string error_display(const std::string& kind, const std::string& msg);
 

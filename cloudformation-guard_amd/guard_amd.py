@@ -77,6 +77,7 @@ def lib():
     L.gg_session_counts_device.argtypes = [ctypes.c_void_p]
     L.gg_session_counts_device.restype = ctypes.c_void_p
     L.gg_session_counts.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+    L.gg_session_configure.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint32]
     L.gg_session_bind_counts.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
     L.gg_session_bind_counts.restype = None
     L.gg_session_drain_kernel_ms.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ExternError)]
@@ -200,6 +201,11 @@ class Session:
         if err.code != 0:
             _raise(err)
 
+    def configure(self, mode=0, lane_heap_bytes=0):
+        """mode 0: one tile per lane (+ wave-mode retry of overflowing tiles); 1: one tile per wave."""
+        if lib().gg_session_configure(self.s, mode, lane_heap_bytes) != 0:
+            raise ValueError("bad session configuration")
+
     def set_stream(self, stream_handle):
         lib().gg_session_set_stream(self.s, ctypes.c_void_p(stream_handle))
 
@@ -244,7 +250,7 @@ class Session:
 
     STAT = {"ndocs": 0, "nfiles": 1, "nodes": 2, "bytes": 3, "fail": 4, "pass": 5, "skip": 6, "errors": 7,
             "records": 8, "arena_bytes": 9, "first_error": 10, "record_bytes": 11, "record_cap": 12,
-            "max_top": 13, "slots": 14, "heap_bytes": 15}
+            "max_top": 13, "slots": 14, "heap_bytes": 15, "retried": 16, "lane_slots": 17}
 
 
 def synth_cfn_doc(index, n_resources=50):

@@ -60,6 +60,9 @@ int32_t gg_device_available(void);
 
 /* Asynchronous evaluation on a caller stream (bench.py passes torch's current stream). */
 void gg_session_set_stream(gg_session *s, void *hip_stream);
+/* mode 0 (default): one tile per lane, tiles that outgrow the lane heap re-run one tile per
+ * wavefront; mode 1: one tile per wavefront for every tile.  lane_heap_bytes 0 keeps 64 KB. */
+int32_t gg_session_configure(gg_session *s, int32_t mode, uint32_t lane_heap_bytes);
 int32_t gg_session_launch(gg_session *s, extern_err_t *err);  /* enqueue; no host sync */
 double gg_session_wait(gg_session *s, extern_err_t *err);     /* kernel ms of the last launch */
 int32_t gg_session_fetch(gg_session *s, extern_err_t *err);   /* statuses + records to host */

@@ -113,3 +113,38 @@ def test_session_large_batch_statuses_vs_oracle():
             root = E.RootScope(rf, doc)
             status = E.eval_rules_file(rf, root, "d%d" % i)
             assert st[i * len(rules) + f] == want[status], (i, f)
+
+
+def _session_report(docs, rules, mode, lane_heap=0):
+    s = guard_amd.Session()
+    s.configure(mode, lane_heap)
+    for name, text in rules:
+        s.add_rules(text, name)
+    s.add_docs(docs, ["synthetic-%d.json" % i for i in range(len(docs))])
+    s.eval(1)
+    out, code = s.report()
+    retried = s.stat(s.STAT["retried"])
+    s.close()
+    return out, code, retried
+
+
+@pytest.mark.gpu
+def test_lane_mode_matches_wave_mode():
+    """One-tile-per-lane and one-tile-per-wavefront kernels produce byte-identical reports."""
+    docs = synth.cfn_corpus(130, start=777, n_resources=50)   # 3 lane batches, last one ragged
+    rules = rule_pack()
+    lane, lcode, _ = _session_report(docs, rules, 0)
+    wave, wcode, _ = _session_report(docs, rules, 1)
+    assert lcode == wcode
+    assert lane == wave
+
+
+@pytest.mark.gpu
+def test_lane_overflow_retried_in_wave_mode():
+    """Tiles that outgrow the lane heap are re-run in wave mode; results unchanged."""
+    docs = synth.cfn_corpus(8, start=31, n_resources=200)
+    rules = rule_pack()
+    lane, lcode, retried = _session_report(docs, rules, 0, 32 * 1024)
+    wave, wcode, _ = _session_report(docs, rules, 1)
+    assert retried > 0
+    assert (lane, lcode) == (wave, wcode)
