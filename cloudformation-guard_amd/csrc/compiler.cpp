@@ -74,8 +74,7 @@ struct Compiler {
     auto it = str_ids.find(s);
     if (it != str_ids.end()) return it->second;
     PStr ps;
-    ps.off = (uint32_t)P.lit.bytes.size(); ps.len = (uint32_t)s.size(); ps.hash = fnv1a(s.data(), s.size()); ps.pad = 0;
-    P.lit.bytes += s;
+    ps.off = lit_str(s); ps.len = (uint32_t)s.size(); ps.hash = fnv1a(s.data(), s.size()); ps.pad = 0;
     P.strs.push_back(ps);
     uint32_t id = (uint32_t)P.strs.size() - 1;
     str_ids[s] = id;
@@ -105,6 +104,15 @@ struct Compiler {
   }
 
   // ---- literal arena ---------------------------------------------------------
+  // literal pool strings: 16-byte aligned, zero-padded to 16 bytes (the device compares in chunks)
+  uint32_t lit_str(const std::string& v) {
+    std::string& B = P.lit.bytes;
+    B.append((16 - (B.size() & 15)) & 15, '\0');
+    uint32_t off = (uint32_t)B.size();
+    B += v;
+    B.append((16 - (v.size() & 15)) & 15, '\0');
+    return off;
+  }
   void lit_fill(const LitValue& v, uint32_t slot, uint32_t parent) {
     DocBatch& L = P.lit;
     DNode& d = L.nodes[slot];
@@ -113,14 +121,16 @@ struct Compiler {
     switch (v.k) {
       case LitValue::Null: d.kind = K_NULL; break;
       case LitValue::String: {
-        d.kind = K_STRING; d.a = (uint32_t)L.bytes.size(); d.count = (uint32_t)v.s.size(); d.b = fnv1a(v.s.data(), v.s.size());
-        L.bytes += v.s; break;
+        d.kind = K_STRING; d.count = (uint32_t)v.s.size(); d.b = fnv1a(v.s.data(), v.s.size());
+        d.a = lit_str(v.s); break;
       }
       case LitValue::Regex: {
         uint32_t rid = regex(v.s);
         DNode& dd = L.nodes[slot];
-        dd.kind = K_REGEX; dd.a = (uint32_t)L.bytes.size(); dd.count = (uint32_t)v.s.size(); dd.b = rid;
-        L.bytes += v.s; break;
+        uint32_t off = lit_str(v.s);
+        DNode& dr = L.nodes[slot];
+        dr.kind = K_REGEX; dr.a = off; dr.count = (uint32_t)v.s.size(); dr.b = rid;
+        break;
       }
       case LitValue::Bool: d.kind = K_BOOL; d.a = v.b ? 1 : 0; break;
       case LitValue::Int: { d.kind = K_INT; uint64_t u = (uint64_t)v.i; d.a = (uint32_t)u; d.b = (uint32_t)(u >> 32); break; }
@@ -154,9 +164,9 @@ struct Compiler {
         L.nodes[slot].a = first; L.nodes[slot].count = n;
         for (uint32_t j = 0; j < n; j++) {
           const std::string& k = v.kv[j].first;
+          uint32_t koff = lit_str(k);
           DNode& c = L.nodes[first + j];
-          c.key_off = (uint32_t)L.bytes.size(); c.key_len = (uint32_t)k.size(); c.key_hash = fnv1a(k.data(), k.size());
-          L.bytes += k;
+          c.key_off = koff; c.key_len = (uint32_t)k.size(); c.key_hash = fnv1a(k.data(), k.size());
           lit_fill(v.kv[j].second, first + j, slot);
         }
         break;
@@ -418,6 +428,7 @@ struct Compiler {
 
   template <class T>
   void put(std::vector<uint32_t>& blob, uint32_t& off, uint32_t& n, const std::vector<T>& v) {
+    while (blob.size() & 3) blob.push_back(0);   // 16-byte aligned sections
     off = (uint32_t)blob.size();
     n = (uint32_t)v.size();
     size_t words = (v.size() * sizeof(T) + 3) / 4;

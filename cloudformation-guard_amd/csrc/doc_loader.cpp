@@ -654,8 +654,10 @@ uint32_t DocBatch::intern(const char* p, uint32_t n, uint32_t hash) {
     if (ilen[h] == n && memcmp(bytes.data() + islots[h] - 1, p, n) == 0) return islots[h] - 1;
     h = (h + 1) & mask;
   }
+  // 16-byte aligned start, zero padding to a 16-byte multiple (device compares in 16-byte chunks)
   uint32_t off = (uint32_t)bytes.size();
   bytes.append(p, n);
+  bytes.append((16 - (n & 15)) & 15, '\0');
   islots[h] = off + 1; ilen[h] = n; iused++;
   return off;
 }
