@@ -106,6 +106,7 @@ def main():
     import torch
     import guard_amd
     import rulepack
+    import sharding
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -129,8 +130,8 @@ def main():
     for name, text in rules:
         sess.add_rules(text, name)
     t0 = time.time()
-    first = rank * args.docs
-    sess.add_synthetic(first, args.docs, n_resources=args.resources, threads=threads)
+    first, count = sharding.shard_range(rank, world, args.docs)
+    sess.add_synthetic(first, count, n_resources=args.resources, threads=threads)
     t_load = time.time() - t0
     t0 = time.time()
     sess.upload()
@@ -156,8 +157,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         sess.launch()
-        if dist is not None:
-            dist.all_reduce(counts)
+        sharding.all_reduce_tallies(counts, dist)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()

@@ -34,3 +34,20 @@ def test_no_cpu_fallback():
         guard_amd.run_checks("{}", "d", "Resources exists", "r")
     assert ei.value.code == -1
     assert "no HIP device" in ei.value.message
+
+
+def test_c_consumer_builds_and_fails_loudly_without_gpu(tmp_path):
+    """A guard-ffi style C program compiles against include/ and links the library unchanged;
+    with no GPU in this container it gets code -1 (no CPU fallback)."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    pkg = os.path.join(root, "cloudformation-guard_amd")
+    exe = str(tmp_path / "ffi_run_checks")
+    subprocess.check_call(["gcc", os.path.join(root, "examples", "ffi_run_checks.c"), "-I", os.path.join(root, "include"),
+                           "-L", pkg, "-lcfnguard_mi355x", "-Wl,-rpath," + pkg, "-o", exe])
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    if guard_amd.device_available():   # on a GPU box the same binary evaluates on the device
+        assert r.returncode == 0 and '"status": "FAIL"' in r.stdout
+    else:
+        assert r.returncode == 2
+        assert r.stdout.startswith("error: -1 (no HIP device")
