@@ -20,7 +20,10 @@ YAML_LIB = "/opt/conda/lib"
 HOST_SRCS = ["doc_loader.cpp", "rules_parser.cpp", "regex_dfa.cpp", "cruet.cpp", "compiler.cpp", "reporter.cpp",
              "synth_corpus.cpp"]
 HIP_SRCS = ["eval_kernel.hip", "capi.cpp"]
-FLAGS = ["-O3", "-std=c++17", "-fPIC", "-I" + YAML_INC, "-Wno-unused-result"]
+# occupancy target of the lane-mode kernel (waves per SIMD); it caps VGPRs at 512 / N
+LANE_WAVES_PER_EU = os.environ.get("GG_LANE_WAVES_PER_EU", "2")
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-I" + YAML_INC, "-Wno-unused-result",
+         "-DGG_LANE_WAVES_PER_EU=" + LANE_WAVES_PER_EU]
 
 
 def _needs(src, obj, deps):
@@ -32,7 +35,7 @@ def _needs(src, obj, deps):
 
 def build(verbose=False):
     os.makedirs(OBJ, exist_ok=True)
-    headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".h", ".inc"))]
     headers.append(os.path.join(HERE, "..", "include", "cfn_guard_mi355x.h"))
     jobs = []
     for s in HOST_SRCS + HIP_SRCS:

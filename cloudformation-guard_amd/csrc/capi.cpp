@@ -216,7 +216,10 @@ void session_upload(gg_session* s) {
   uint32_t slots = (uint32_t)std::min<size_t>(std::max<size_t>(ntiles, 1), wave_slots);
   s->nslots = slots;
   s->d_heaps.alloc((size_t)slots * s->heap_bytes);
-  s->lane_slots = s->mode == 1 ? 0 : (uint32_t)std::min<size_t>(std::max<size_t>(nbatches, 1), (size_t)g_dev.ncu * 8);
+  // lane-mode grid: waves per CU (default 8 = the kernel's occupancy at 2 waves/SIMD)
+  size_t lane_waves_per_cu = 8;
+  if (const char* e = getenv("GG_LANE_WAVES_PER_CU")) lane_waves_per_cu = std::max(1, atoi(e));
+  s->lane_slots = s->mode == 1 ? 0 : (uint32_t)std::min<size_t>(std::max<size_t>(nbatches, 1), (size_t)g_dev.ncu * lane_waves_per_cu);
   s->d_lane_heaps.alloc((size_t)s->lane_slots * 64 * s->lane_heap_bytes);
   s->d_retry.alloc(std::max<size_t>(ntiles, 1));
   s->d_tiles.alloc(std::max<size_t>(ntiles, 1));

@@ -190,6 +190,27 @@ struct Compiler {
   }
 
   // ---- queries -----------------------------------------------------------------
+  // A filter whose conjunctions are the single clause `<key> == '<string literal>'` (the
+  // desugared type block `Resources.*[ Type == 'AWS::S3::Bucket' ]` and most `let x =
+  // Resources.*[ Type == ... ]`) is marked so the device can test a value with one map lookup
+  // and one string compare (PPart.c = clause id + 1); values the shortcut cannot decide exactly
+  // (lists, missing keys that need case conversion, non-map values) take the generic path.
+  uint32_t fast_filter_clause(uint32_t cj) {
+    const PRange2 C = conjs[cj];
+    if (C.n != 1) return 0;
+    const PRange2 D = disjs[disj_refs[C.first]];
+    if (D.n != 1) return 0;
+    uint32_t cid = clause_refs[D.first];
+    const PClause& pc = clauses[cid];
+    if (pc.kind != C_ACCESS) return 0;
+    uint32_t op = pc.flags & 15u, nt = (pc.flags >> 4) & 1u, neg = (pc.flags >> 5) & 1u, rk = (pc.flags >> 8) & 15u;
+    if (op != OP_EQ || nt || neg || rk != RHS_LITERAL) return 0;
+    const PQuery& q = queries[pc.a];
+    if (q.n != 1 || parts[q.first].kind != P_KEY) return 0;
+    if (!(pc.b & LIT_BIT) || P.lit.nodes[pc.b & ~LIT_BIT].kind != K_STRING) return 0;
+    return cid + 1;
+  }
+
   uint32_t query(const AccessQuery& q) {
     uint32_t qid = (uint32_t)queries.size();
     queries.push_back(PQuery{0, 0, q.match_all ? 1u : 0u, 0});
@@ -219,7 +240,10 @@ struct Compiler {
         case QueryPart::Index: pp.kind = P_INDEX; pp.a = (uint32_t)qp.index; break;
         case QueryPart::AllValues: pp.kind = P_ALL_VALUES; pp.a = qp.has_name ? var(qp.key) : NONE; break;
         case QueryPart::AllIndices: pp.kind = P_ALL_INDICES; pp.a = qp.has_name ? var(qp.key) : NONE; break;
-        case QueryPart::Filter: pp.kind = P_FILTER; pp.a = conj(*qp.filter); pp.b = qp.has_name ? var(qp.key) : NONE; break;
+        case QueryPart::Filter:
+          pp.kind = P_FILTER; pp.a = conj(*qp.filter); pp.b = qp.has_name ? var(qp.key) : NONE;
+          pp.c = fast_filter_clause(pp.a);
+          break;
         case QueryPart::MapKeyFilter: {
           // MapKeyFilterClause (exprs.rs:183-187): rhs literal | query (rooted at the map) | function
           pp.kind = P_MAP_KEY_FILTER;

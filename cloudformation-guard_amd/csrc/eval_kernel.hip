@@ -51,10 +51,11 @@ __device__ __attribute__((always_inline)) inline void tile_begin(CtxT& c, const 
 // program over different documents.  Records are published with one atomic per wave (wave
 // prefix sum).  Tiles that outgrow the 64 KB lane heap (heap, record staging or frame limits)
 // are queued for the wave-mode kernel below instead of failing.
-__global__ void __launch_bounds__(64) guard_eval_lanes_kernel(LaunchArgs A) {
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE_WAVES_PER_EU))) guard_eval_lanes_kernel(LaunchArgs A) {
   using namespace ln;
   const uint32_t lane = __lane_id();
-  uint8_t* heap = A.lane_heaps + ((size_t)blockIdx.x * 64 + lane) * A.lane_heap_bytes;
+  // 64 lanes share one interleaved region (see haddr in eval_core.inc)
+  uint8_t* heap = A.lane_heaps + (size_t)blockIdx.x * 64 * A.lane_heap_bytes;
   const uint32_t nchunks = (A.docs.ndocs + 63u) / 64u;
   const uint32_t nbatches = nchunks * A.nfiles;
   for (;;) {
@@ -71,6 +72,7 @@ __global__ void __launch_bounds__(64) guard_eval_lanes_kernel(LaunchArgs A) {
     uint32_t status = ST_SKIP, n = 0;
     if (active) {
       tile_begin(c, A, P, doc, heap, A.lane_heap_bytes, FRAMES_BYTES, RECS_BYTES);
+      c.lane16 = lane * 16u;
       c.syn_off = alloc_pers(c, 256 * 16);
       c.memo = alloc_pers(c, (P->n_slots ? P->n_slots : 1) * 4);
       if (!c.err) for (uint32_t i = 0; i < P->n_slots; i++) u32a(c, c.memo)[i] = 3u;
@@ -101,8 +103,7 @@ __global__ void __launch_bounds__(64) guard_eval_lanes_kernel(LaunchArgs A) {
       bool retry = c.err == E_HEAP || c.err == E_RECORDS || c.err == E_DEPTH;
       if (retry) A.retry_list[atomicAdd(A.retry_count, 1u)] = tile;
       if (n && off + n > A.rec_cap) { c.err = E_RECORDS; n = 0; }
-      const Rec* src = (const Rec*)(heap + FRAMES_BYTES);
-      for (uint32_t i = 0; i < n; i++) A.recs[off + i] = src[i];
+      for (uint32_t i = 0; i < n; i++) A.recs[off + i] = hload<Rec>(c, FRAMES_BYTES + i * (uint32_t)sizeof(Rec));
       TileOut o;
       o.status = status; o.err = c.err; o.err_a = c.err_a; o.err_b = c.err_b;
       o.rec_off = off; o.rec_n = n; o.pad0 = 0; o.pad1 = 0;
@@ -129,6 +130,7 @@ __global__ void __launch_bounds__(64) guard_eval_kernel(LaunchArgs A) {
     const DevProg* P = &A.progs[file];
     Ctx c;
     tile_begin(c, A, P, doc, heap, A.heap_bytes, FRAMES_BYTES, RECS_BYTES);
+    c.lane16 = 0;
     c.syn_off = alloc_pers(c, 256 * 16);
     c.memo = alloc_pers(c, (P->n_slots ? P->n_slots : 1) * 4);
     if (!c.err) for (uint32_t i = 0; i < P->n_slots; i++) u32a(c, c.memo)[i] = 3u;
