@@ -138,6 +138,8 @@ struct GpuProgram {
     dp.n_top = prog.blob[sizeof(ProgHeader) / 4 + 1];
     dp.n_slots = h.n_name_slots;
     dp.n_rules_total = h.n_rules;
+    dp.blob = b;
+    dp.lds_words = h.off_dfa;
   }
 };
 
@@ -774,6 +776,12 @@ int64_t gg_session_stat(gg_session* s, int32_t what) {
       return v;
     }
     case 17: return (int64_t)s->lane_slots;
+    case 18: { size_t m = 0; for (auto& p : s->progs) m = std::max(m, p->prog.blob.size() * 4); return (int64_t)m; }
+    case 19: {   // largest program blob without its regex DFA tables (the part staged in LDS)
+      size_t m = 0;
+      for (auto& p : s->progs) m = std::max(m, p->prog.blob.size() * 4 - (size_t)p->prog.hdr.n_dfa * 2);
+      return (int64_t)m;
+    }
     default: return -1;
   }
 }

@@ -482,11 +482,12 @@ struct Compiler {
     put(blob, h.off_param_vars, h.n_param_vars, param_vars);
     put(blob, h.off_alts, h.n_alts, alts);
     put(blob, h.off_regex, h.n_regex, regexes);
-    put(blob, h.off_dfa, h.n_dfa, dfa);
     put(blob, h.off_lit_nodes, h.n_lit_nodes, P.lit.nodes);
     put(blob, h.off_lit_ranges, h.n_lit_ranges, P.ranges);
     std::vector<char> bytes(P.lit.bytes.begin(), P.lit.bytes.end());
     put(blob, h.off_bytes, h.n_bytes, bytes);
+    // regex DFA tables last: the kernels stage everything before them in LDS (eval_kernel.hip)
+    put(blob, h.off_dfa, h.n_dfa, dfa);
     h.nwords = (uint32_t)blob.size();
     memcpy(blob.data(), &h, sizeof(ProgHeader));
     blob[sizeof(ProgHeader) / 4] = top_first;

@@ -34,6 +34,8 @@ struct DevProg {
   uint32_t n_top;         // number of top-level rules
   uint32_t n_slots;
   uint32_t n_rules_total;
+  const uint32_t* blob;   // device blob the pointers above index into
+  uint32_t lds_words;     // words before the DFA tables (the part the kernels stage in LDS)
 };
 
 struct DevBatch {

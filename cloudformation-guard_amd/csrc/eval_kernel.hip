@@ -36,6 +36,36 @@ namespace ln {
 }  // namespace ln
 
 // ------------------------------------------------------------------ kernels ---
+// Rules program staging: every section of the file's program blob before the regex DFA tables
+// (KBs: clauses, query parts, strings, literals) is copied into the workgroup's LDS and the
+// DevProg pointers are rebased onto the copy, so the interpreter's program reads are LDS reads
+// instead of dependent global loads.  Programs larger than the LDS window stay in HBM.
+static const uint32_t LDS_PROG_WORDS = 2048;   // 8 KB per workgroup (one wave)
+
+__device__ __attribute__((always_inline)) inline const DevProg* stage_program(const DevProg* G, DevProg* sp, uint4* sblob) {
+  const uint32_t lane = __lane_id();
+  __syncthreads();   // the previous batch's reads of the window are complete
+  const uint32_t n = G->lds_words;
+  if (n > LDS_PROG_WORDS) return G;
+  const uint4* src = (const uint4*)G->blob;
+  for (uint32_t i = lane; i < (n + 3u) / 4u; i += 64u) sblob[i] = src[i];
+  if (lane == 0) {
+    DevProg d = *G;
+    const char* gb = (const char*)G->blob;
+    const size_t lim = (size_t)n * 4u;
+    char* lb = (char*)sblob;
+#define GG_REBASE(f) do { size_t o = (size_t)((const char*)d.f - gb); if (o < lim) d.f = (decltype(d.f))(lb + o); } while (0)
+    GG_REBASE(strs); GG_REBASE(parts); GG_REBASE(queries); GG_REBASE(clauses); GG_REBASE(conjs); GG_REBASE(disjs);
+    GG_REBASE(clause_refs); GG_REBASE(disj_refs); GG_REBASE(blocks); GG_REBASE(lets); GG_REBASE(rules);
+    GG_REBASE(name_rules); GG_REBASE(name_rule_ids); GG_REBASE(funcs); GG_REBASE(params); GG_REBASE(param_vars);
+    GG_REBASE(alts); GG_REBASE(regex); GG_REBASE(lit_nodes); GG_REBASE(lit_ranges); GG_REBASE(bytes);
+#undef GG_REBASE
+    *sp = d;
+  }
+  __syncthreads();
+  return sp;
+}
+
 // Shared per-tile prologue: scratch heap layout, root frame, memo table.
 template <typename CtxT>
 __device__ __attribute__((always_inline)) inline void tile_begin(CtxT& c, const LaunchArgs& A, const DevProg* P,
@@ -58,6 +88,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
   uint8_t* heap = A.lane_heaps + (size_t)blockIdx.x * 64 * A.lane_heap_bytes;
   const uint32_t nchunks = (A.docs.ndocs + 63u) / 64u;
   const uint32_t nbatches = nchunks * A.nfiles;
+  // interpreter state lives in LDS (one Ctx per lane), not in the per-lane stack
+  __shared__ Ctx s_ctx[64];
+  __shared__ DevProg s_prog;
+  __shared__ uint4 s_blob[LDS_PROG_WORDS / 4];
+  Ctx& c = s_ctx[lane];
+  uint32_t staged = NONE;
+  const DevProg* P = nullptr;
   for (;;) {
     uint32_t b = 0;
     if (lane == 0) b = atomicAdd(A.tile_cursor, 1u);
@@ -66,9 +103,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
     const uint32_t file = b % A.nfiles, chunk = b / A.nfiles;
     const uint32_t doc = chunk * 64u + lane;
     const bool active = doc < A.docs.ndocs;
-    const DevProg* P = &A.progs[file];
+    if (file != staged) { P = stage_program(&A.progs[file], &s_prog, s_blob); staged = file; }
     const uint32_t tile = doc * A.nfiles + file;
-    Ctx c;
     uint32_t status = ST_SKIP, n = 0;
     if (active) {
       tile_begin(c, A, P, doc, heap, A.lane_heap_bytes, FRAMES_BYTES, RECS_BYTES);
@@ -120,6 +156,12 @@ __global__ void __launch_bounds__(64) guard_eval_kernel(LaunchArgs A) {
   const uint32_t lane = __lane_id();
   uint8_t* heap = A.heaps + (size_t)blockIdx.x * A.heap_bytes;
   const uint32_t ntiles = A.retry_list ? *A.retry_count : A.ntiles;
+  __shared__ Ctx s_ctx[64];
+  __shared__ DevProg s_prog;
+  __shared__ uint4 s_blob[LDS_PROG_WORDS / 4];
+  Ctx& c = s_ctx[lane];
+  uint32_t staged = NONE;
+  const DevProg* P = nullptr;
   for (;;) {
     uint32_t t = 0;
     if (lane == 0) t = atomicAdd(A.tile_cursor + 1, 1u);
@@ -127,8 +169,7 @@ __global__ void __launch_bounds__(64) guard_eval_kernel(LaunchArgs A) {
     if (t >= ntiles) break;
     uint32_t tile = A.retry_list ? A.retry_list[t] : A.tile_base + t;
     uint32_t doc = tile / A.nfiles, file = tile % A.nfiles;
-    const DevProg* P = &A.progs[file];
-    Ctx c;
+    if (file != staged) { P = stage_program(&A.progs[file], &s_prog, s_blob); staged = file; }
     tile_begin(c, A, P, doc, heap, A.heap_bytes, FRAMES_BYTES, RECS_BYTES);
     c.lane16 = 0;
     c.syn_off = alloc_pers(c, 256 * 16);
