@@ -33,16 +33,21 @@ def _needs(src, obj, deps):
     return any(os.path.getmtime(d) > t for d in [src] + deps)
 
 
-def build(verbose=False):
-    os.makedirs(OBJ, exist_ok=True)
+def build(verbose=False, variant=""):
+    """variant "" = the product library; "stats" = diagnostic build with evaluator counters
+    (libcfnguard_mi355x_stats.so, loaded only when GG_LIB points at it)."""
+    out = OUT if not variant else OUT.replace(".so", "_" + variant + ".so")
+    obj_dir = OBJ if not variant else OBJ + "_" + variant
+    flags = FLAGS + (["-DGG_STATS"] if variant == "stats" else [])
+    os.makedirs(obj_dir, exist_ok=True)
     headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".h", ".inc"))]
     headers.append(os.path.join(HERE, "..", "include", "cfn_guard_mi355x.h"))
     jobs = []
     for s in HOST_SRCS + HIP_SRCS:
         src = os.path.join(CSRC, s)
-        obj = os.path.join(OBJ, s.replace(".cpp", ".o").replace(".hip", ".o"))
+        obj = os.path.join(obj_dir, s.replace(".cpp", ".o").replace(".hip", ".o"))
         if _needs(src, obj, headers):
-            cmd = [HIPCC, "--offload-arch=gfx950"] + FLAGS + ["-c", src, "-o", obj]
+            cmd = [HIPCC, "--offload-arch=gfx950"] + flags + ["-c", src, "-o", obj]
             jobs.append((s, cmd))
 
     def run(job):
@@ -56,20 +61,20 @@ def build(verbose=False):
         for name in ex.map(run, jobs):
             if verbose:
                 print("compiled", name)
-    objs = [os.path.join(OBJ, s.replace(".cpp", ".o").replace(".hip", ".o")) for s in HOST_SRCS + HIP_SRCS]
-    if jobs or not os.path.exists(OUT):
+    objs = [os.path.join(obj_dir, s.replace(".cpp", ".o").replace(".hip", ".o")) for s in HOST_SRCS + HIP_SRCS]
+    if jobs or not os.path.exists(out):
         # libyaml is loaded from the package directory ($ORIGIN): an rpath to /opt/conda/lib would
         # also pull conda's older libstdc++ in front of the one libamdhip64 needs
         local_yaml = os.path.join(HERE, "libyaml-0.so.2")
         shutil.copyfile(os.path.join(YAML_LIB, "libyaml-0.so.2"), local_yaml)
         cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC"] + objs + [
-            "-o", OUT, local_yaml, "-Wl,-rpath,$ORIGIN", "-lpthread"]
+            "-o", out, local_yaml, "-Wl,-rpath,$ORIGIN", "-lpthread"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError("link failed:\n" + r.stderr[-4000:])
-    return OUT
+    return out
 
 
 if __name__ == "__main__":
-    print(build(verbose=True))
+    print(build(verbose=True, variant=sys.argv[1] if len(sys.argv) > 1 else ""))
     sys.exit(0)

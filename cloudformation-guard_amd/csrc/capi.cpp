@@ -164,6 +164,7 @@ struct gg_session {
   DBuf<Rec> d_recs;
   DBuf<uint32_t> d_counters;
   DBuf<unsigned long long> d_counts;   // per (file, top rule) x {PASS, FAIL, SKIP, error}
+  DBuf<unsigned long long> d_stats;    // diagnostic counters (stats build variant)
   size_t ncounts = 0;
   hipStream_t stream = nullptr;        // caller stream (e.g. torch's current stream); null = library stream
   hipEvent_t ev0 = nullptr, ev1 = nullptr;   // brackets of the most recent launch (= evq[nq - 1])
@@ -229,6 +230,8 @@ void session_upload(gg_session* s) {
   s->rec_cap = std::min<size_t>(std::max<size_t>(ntiles * 48, 4096), (size_t)96 * 1024 * 1024);
   s->d_recs.alloc(s->rec_cap);
   s->d_counters.alloc(16);
+  s->d_stats.alloc(16);
+  HIPCHK(hipMemsetAsync(s->d_stats.p, 0, 16 * sizeof(unsigned long long), st));
   s->ncounts = s->progs.size() * (s->max_top + 1) * 4;
   if (s->ncounts * sizeof(uint32_t) > 60 * 1024)
     throw std::runtime_error("too many (rules file x rule) tallies for one LDS block; split the rules files across sessions");
@@ -257,6 +260,7 @@ void session_launch(gg_session* s) {
   A.retry_count = s->d_counters.p + 3;
   A.lane_heaps = s->d_lane_heaps.p; A.lane_heap_bytes = s->lane_heap_bytes;
   A.retry_list = s->mode == 1 ? nullptr : s->d_retry.p;
+  A.stats = s->d_stats.p;
   if (!ntiles) return;
   if (s->nq == s->evq.size()) {
     std::pair<hipEvent_t, hipEvent_t> pr;
@@ -793,6 +797,17 @@ int32_t gg_session_tile_status(gg_session* s, uint8_t* out, size_t n) {
 }
 
 double gg_session_last_kernel_ms(gg_session* s) { return s->last_kernel_ms; }
+
+// diagnostic lane-kernel counters accumulated since upload (all zero unless built with GG_STATS):
+// node reads, heap accesses, query_retrieval calls, clause evaluations, frames pushed, records,
+// map entries scanned by key lookups, fast-filter tests, tiles
+int32_t gg_session_kernel_stats(gg_session* s, uint64_t* out, size_t n) {
+  if (!s->d_stats.p) return -1;
+  std::vector<unsigned long long> v(16);
+  HIPCHK(hipMemcpy(v.data(), s->d_stats.p, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  for (size_t i = 0; i < n && i < 16; i++) out[i] = v[i];
+  return 0;
+}
 
 int32_t gg_device_available(void) {
   int n = 0;

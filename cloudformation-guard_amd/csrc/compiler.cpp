@@ -195,9 +195,39 @@ struct Compiler {
   // Resources.*[ Type == ... ]`) is marked so the device can test a value with one map lookup
   // and one string compare (PPart.c = clause id + 1); values the shortcut cannot decide exactly
   // (lists, missing keys that need case conversion, non-map values) take the generic path.
+  //
+  // A filter whose FIRST conjunction is that clause and whose other conjunctions can never raise
+  // an error (error_free_clause) is marked as well, with bit 31 set: when the shortcut says the
+  // first clause FAILs, the conjunction is FAIL whatever the rest yields -- the reference still
+  // evaluates the rest (conjunctions do not short-circuit, eval.rs:1970-2065), but inside a filter
+  // its records are discarded and it cannot raise, so skipping it changes nothing observable.
+  bool lit_has_regex(uint32_t ref) const {
+    const DNode& n = P.lit.nodes[ref & ~LIT_BIT];
+    if (n.kind == K_REGEX) return true;
+    if (n.kind == K_LIST || n.kind == K_MAP)
+      for (uint32_t j = 0; j < n.count; j++) if (lit_has_regex(n.a + j)) return true;
+    return false;
+  }
+  // access clause over plain navigation steps with no EMPTY (raises on scalars) and no regex or
+  // query/function operand: its evaluation can only produce statuses and records
+  bool error_free_clause(uint32_t cid) const {
+    const PClause& pc = clauses[cid];
+    if (pc.kind != C_ACCESS) return false;
+    uint32_t op = pc.flags & 15u, rk = (pc.flags >> 8) & 15u;
+    if (op == OP_EMPTY) return false;
+    if (op < OP_EXISTS && (rk != RHS_LITERAL || !(pc.b & LIT_BIT) || lit_has_regex(pc.b))) return false;
+    const PQuery& q = queries[pc.a];
+    for (uint32_t i = 0; i < q.n; i++) {
+      const PPart& pp = parts[q.first + i];
+      bool plain = pp.kind == P_THIS || pp.kind == P_KEY || pp.kind == P_KEY_INDEX || pp.kind == P_INDEX ||
+                   ((pp.kind == P_ALL_VALUES || pp.kind == P_ALL_INDICES) && pp.a == NONE);
+      if (!plain) return false;
+    }
+    return true;
+  }
   uint32_t fast_filter_clause(uint32_t cj) {
     const PRange2 C = conjs[cj];
-    if (C.n != 1) return 0;
+    if (C.n < 1) return 0;
     const PRange2 D = disjs[disj_refs[C.first]];
     if (D.n != 1) return 0;
     uint32_t cid = clause_refs[D.first];
@@ -208,7 +238,12 @@ struct Compiler {
     const PQuery& q = queries[pc.a];
     if (q.n != 1 || parts[q.first].kind != P_KEY) return 0;
     if (!(pc.b & LIT_BIT) || P.lit.nodes[pc.b & ~LIT_BIT].kind != K_STRING) return 0;
-    return cid + 1;
+    if (C.n == 1) return cid + 1;
+    for (uint32_t i = 1; i < C.n; i++) {
+      const PRange2 Di = disjs[disj_refs[C.first + i]];
+      for (uint32_t j = 0; j < Di.n; j++) if (!error_free_clause(clause_refs[Di.first + j])) return 0;
+    }
+    return (cid + 1) | 0x80000000u;
   }
 
   uint32_t query(const AccessQuery& q) {

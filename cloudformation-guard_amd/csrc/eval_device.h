@@ -66,6 +66,7 @@ struct LaunchArgs {
   uint32_t lane_heap_bytes;
   uint32_t* retry_list;    // tiles the lane kernel hands to the wave kernel (null: wave kernel runs all)
   uint32_t* retry_count;
+  unsigned long long* stats;   // diagnostic counters [8] (stats build variant), else unused
 };
 
 }  // namespace gg

@@ -74,6 +74,16 @@ __device__ __attribute__((always_inline)) inline void tile_begin(CtxT& c, const 
   c.P = P; c.dn = A.docs.nodes + A.docs.base[doc]; c.db = A.docs.bytes; c.heap = heap; c.cap = heap_bytes;
   c.tmp = frames_bytes + recs_bytes; c.pers = heap_bytes; c.nframes = 0; c.nrec = 0;
   c.err = 0; c.err_a = 0; c.err_b = 0; c.suppress = 0; c.rec_created = 0; c.depth = 0; c.nsyn = 0;
+#ifdef GG_STATS
+  for (int i = 0; i < 8; i++) c.st[i] = 0;
+#endif
+}
+template <typename CtxT>
+__device__ __attribute__((always_inline)) inline void tile_stats(CtxT& c, const LaunchArgs& A) {
+#ifdef GG_STATS
+  for (int i = 0; i < 8; i++) atomicAdd(&A.stats[i], (unsigned long long)c.st[i]);
+  atomicAdd(&A.stats[8], 1ull);
+#endif
 }
 
 // Lane mode (the throughput path): each lane evaluates one (document, rules file) tile.  A wave
@@ -123,6 +133,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
       }
       status = fails ? ST_FAIL : (passes ? ST_PASS : ST_SKIP);
       n = c.err ? 0 : c.nrec;
+      tile_stats(c, A);
     }
     // wave-aggregated record allocation
     uint32_t incl = n;

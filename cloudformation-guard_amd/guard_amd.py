@@ -14,7 +14,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libcfnguard_mi355x.so")
+# GG_LIB selects a diagnostic build variant (e.g. libcfnguard_mi355x_stats.so); default: the product library
+LIB_PATH = os.environ.get("GG_LIB") or os.path.join(HERE, "libcfnguard_mi355x.so")
 
 
 class ExternError(ctypes.Structure):
@@ -82,6 +83,7 @@ def lib():
     L.gg_session_bind_counts.restype = None
     L.gg_session_drain_kernel_ms.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ExternError)]
     L.gg_session_drain_kernel_ms.restype = ctypes.c_size_t
+    L.gg_session_kernel_stats.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
     L.gg_synth_cfn_doc.argtypes = [ctypes.c_uint64, ctypes.c_int32, ctypes.c_char_p, ctypes.c_size_t]
     L.gg_synth_cfn_doc.restype = ctypes.c_size_t
     L.gg_session_add_synthetic.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_int32,
@@ -241,6 +243,11 @@ class Session:
         if err.code != 0:
             _raise(err)
         return list(buf)[:min(n, cap)]
+
+    def kernel_stats(self):
+        out = (ctypes.c_uint64 * 16)()
+        lib().gg_session_kernel_stats(self.s, out, 16)
+        return list(out)
 
     def counts(self):
         n = self.ncounts()

@@ -76,6 +76,8 @@ void gg_session_bind_counts(gg_session *s, void *dev, size_t n);
 /* evaluation-kernel ms of every launch since the last drain (HIP events on the launch stream) */
 size_t gg_session_drain_kernel_ms(gg_session *s, double *out, size_t cap, extern_err_t *err);
 int32_t gg_session_counts(gg_session *s, uint64_t *out, size_t n);
+/* diagnostic evaluator counters (nonzero only in the GG_STATS build variant) */
+int32_t gg_session_kernel_stats(gg_session *s, uint64_t *out, size_t n);
 
 /* Loader self-check (tests): 1 = JSON fast path builds the libyaml path's exact arena,
  * 0 = they differ, -1 = fast path declined the document. */
