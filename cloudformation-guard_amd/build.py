@@ -39,6 +39,8 @@ def build(verbose=False, variant=""):
     out = OUT if not variant else OUT.replace(".so", "_" + variant + ".so")
     obj_dir = OBJ if not variant else OBJ + "_" + variant
     flags = FLAGS + (["-DGG_STATS"] if variant == "stats" else [])
+    if variant.startswith("eu"):   # occupancy experiments: eu<N> = amdgpu_waves_per_eu(N)
+        flags = [f for f in flags if not f.startswith("-DGG_LANE_WAVES_PER_EU=")] + ["-DGG_LANE_WAVES_PER_EU=" + variant[2:]]
     os.makedirs(obj_dir, exist_ok=True)
     headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".h", ".inc"))]
     headers.append(os.path.join(HERE, "..", "include", "cfn_guard_mi355x.h"))
