@@ -18,10 +18,12 @@
 #include <string>
 #include <thread>
 #include <vector>
+#include <unordered_map>
 
 #include "../../include/cfn_guard_mi355x.h"
 #include "doc_loader.h"
 #include "eval_device.h"
+#include "host_format.h"
 #include "program.h"
 #include "reporter.h"
 #include "synth_corpus.h"
@@ -103,12 +105,45 @@ struct DBuf {
   ~DBuf() { release(); }
 };
 
+// String ids of a rules program against a document batch: a program string (query key, case
+// converted key, string literal, literal map key) gets the batch's id for the same text, or an id
+// above every pool offset (shared by equal texts) when no document has it, so the device compares
+// program and document strings by id.  Patches a copy of the blob.
+struct StringIds {
+  std::unordered_map<std::string, uint32_t> absent;
+  uint32_t id(const DocBatch& docs, const char* p, uint32_t n) {
+    uint32_t off = docs.find(p, n);
+    if (off != NONE) return off;
+    auto it = absent.find(std::string(p, n));
+    if (it != absent.end()) return it->second;
+    uint32_t v = 0xF0000000u + (uint32_t)absent.size();
+    absent.emplace(std::string(p, n), v);
+    return v;
+  }
+};
+
+std::vector<uint32_t> canonical_blob(const Program& prog, const DocBatch& docs, StringIds& ids) {
+  std::vector<uint32_t> b = prog.blob;
+  const ProgHeader& h = prog.hdr;
+  const char* pb = (const char*)(prog.blob.data() + h.off_bytes);
+  PStr* strs = (PStr*)(b.data() + h.off_strs);
+  for (uint32_t i = 0; i < h.n_strs; i++) strs[i].hash = ids.id(docs, pb + strs[i].off, strs[i].len);
+  DNode* lit = (DNode*)(b.data() + h.off_lit_nodes);
+  for (uint32_t i = 0; i < h.n_lit_nodes; i++) {
+    if (lit[i].kind == K_STRING) lit[i].b = ids.id(docs, pb + lit[i].a, lit[i].count);
+    if (lit[i].key_off != NONE) lit[i].key_hash = ids.id(docs, pb + lit[i].key_off, lit[i].key_len);
+  }
+  return b;
+}
+
 struct GpuProgram {
   Program prog;
   DBuf<uint32_t> blob;
   DevProg dp{};
-  void upload(hipStream_t s) {
-    blob.upload(prog.blob.data(), prog.blob.size(), s);
+  std::vector<uint32_t> staged;   // canonical copy of prog.blob (kept alive for the async upload)
+  void upload(hipStream_t s, const DocBatch& docs, StringIds& ids) {
+    staged = canonical_blob(prog, docs, ids);
+    blob.upload(staged.data(), staged.size(), s);
     const uint32_t* b = blob.p;
     const ProgHeader& h = prog.hdr;
     dp.strs = (const PStr*)(b + h.off_strs);
@@ -206,8 +241,9 @@ void session_upload(gg_session* s) {
   s->d_base.upload(s->docs.base.data(), s->docs.base.size(), st);
   std::vector<DevProg> dps;
   s->max_top = 1;
+  StringIds ids;
   for (auto& p : s->progs) {
-    p->upload(st);
+    p->upload(st, s->docs, ids);
     dps.push_back(p->dp);
     s->max_top = std::max<uint32_t>(s->max_top, p->dp.n_top);
   }
@@ -396,35 +432,46 @@ bool session_report(gg_session* s, std::string& out, int32_t& exit_code, ReportE
   return true;
 }
 
-// Appends per-thread batches to dst: sizes first, one resize, then each part is copied and
-// rebased by its own thread (the arena of a 1M-template corpus is tens of GB).
+// Appends per-thread batches to dst.  Every distinct string of every part is interned into dst's
+// pool first (parts in order), so the merged pool again holds each string once and pool offsets
+// stay string ids; then each part's nodes are copied, remapped and rebased by its own thread (the
+// arena of a 1M-template corpus is tens of GB).
 void merge_batches(DocBatch& dst, std::vector<DocBatch>& parts) {
   size_t np = parts.size();
-  std::vector<size_t> nbase(np + 1), bbase(np + 1), rbase(np + 1);
-  nbase[0] = dst.nodes.size(); bbase[0] = dst.bytes.size(); rbase[0] = dst.roots.size();
+  std::vector<size_t> nbase(np + 1), rbase(np + 1);
+  nbase[0] = dst.nodes.size(); rbase[0] = dst.roots.size();
   for (size_t t = 0; t < np; t++) {
     nbase[t + 1] = nbase[t] + parts[t].nodes.size();
-    bbase[t + 1] = bbase[t] + parts[t].bytes.size();
     rbase[t + 1] = rbase[t] + parts[t].roots.size();
   }
-  if (bbase[np] > kMaxPoolBytes)
-    throw std::runtime_error("document batch is full (u32 string-pool offsets); evaluate it and start a new batch");
+  // part pool offset (16-byte granule) -> dst pool offset
+  std::vector<std::vector<uint32_t>> remap(np);
+  for (size_t t = 0; t < np; t++) {
+    const DocBatch& src = parts[t];
+    remap[t].assign(src.bytes.size() / 16 + 1, NONE);
+    for (size_t i = 0; i < src.islots.size(); i++) {
+      if (!src.islots[i]) continue;
+      uint32_t off = src.islots[i] - 1, len = src.ilen[i];
+      if (dst.bytes.size() + len + 16 > kMaxPoolBytes)
+        throw std::runtime_error("document batch is full (u32 string-pool offsets); evaluate it and start a new batch");
+      remap[t][off / 16] = dst.intern(src.bytes.data() + off, len, fnv1a(src.bytes.data() + off, len));
+    }
+  }
   dst.nodes.resize(nbase[np]); dst.line.resize(nbase[np]); dst.col.resize(nbase[np]);
   dst.kline.resize(nbase[np]); dst.kcol.resize(nbase[np]);
-  dst.bytes.resize(bbase[np]);
   dst.roots.resize(rbase[np]);
   dst.base.resize(rbase[np]);
   for (auto& p : parts) if (p.serde) dst.serde = true;
-  // node indices are document-relative, so only string-pool offsets and document bases move
+  // node indices are document-relative, so only string ids and document bases move
   auto work = [&](size_t t) {
     const DocBatch& src = parts[t];
-    uint32_t bb = (uint32_t)bbase[t];
+    const uint32_t* rm = remap[t].data();
     size_t nb = nbase[t];
     DNode* out = dst.nodes.data() + nb;
     for (size_t i = 0; i < src.nodes.size(); i++) {
       DNode n = src.nodes[i];
-      if (n.kind == K_STRING) n.a += bb;
-      if (n.key_off != NONE) n.key_off += bb;
+      if (n.kind == K_STRING) { n.a = rm[n.a / 16]; n.b = n.a; }
+      if (n.key_off != NONE) { n.key_off = rm[n.key_off / 16]; n.key_hash = n.key_off; }
       out[i] = n;
     }
     size_t nn = src.nodes.size() * sizeof(uint32_t);
@@ -434,7 +481,6 @@ void merge_batches(DocBatch& dst, std::vector<DocBatch>& parts) {
       memcpy(dst.kline.data() + nb, src.kline.data(), nn);
       memcpy(dst.kcol.data() + nb, src.kcol.data(), nn);
     }
-    if (!src.bytes.empty()) memcpy(&dst.bytes[bb], src.bytes.data(), src.bytes.size());
     for (size_t r = 0; r < src.roots.size(); r++) {
       dst.roots[rbase[t] + r] = src.roots[r];
       dst.base[rbase[t] + r] = src.base[r] + nb;

@@ -222,8 +222,8 @@ struct Emitter {
     switch (n.kind) {
       case K_STRING: {
         d.count = (uint32_t)n.s.size();
-        d.b = fnv1a(n.s.data(), n.s.size());
-        d.a = b.intern(n.s.data(), d.count, d.b);
+        d.a = b.intern(n.s.data(), d.count, fnv1a(n.s.data(), n.s.size()));
+        d.b = d.a;   // string id = canonical pool offset (equal ids <=> equal strings)
         break;
       }
       case K_BOOL: d.a = (uint32_t)n.i; break;
@@ -266,8 +266,8 @@ struct Emitter {
         for (uint32_t j = 0; j < cnt; j++) {
           DNode& c = b.nodes[first + j];
           c.key_len = (uint32_t)keys[j].size();
-          c.key_hash = fnv1a(keys[j].data(), keys[j].size());
-          c.key_off = b.intern(keys[j].data(), c.key_len, c.key_hash);
+          c.key_off = b.intern(keys[j].data(), c.key_len, fnv1a(keys[j].data(), keys[j].size()));
+          c.key_hash = c.key_off;   // key id
           b.kline[first + j] = serde ? 0 : kmarks[j].first;
           b.kcol[first + j] = serde ? 0 : kmarks[j].second;
           const TN& kn = t.n[vals[j]];
@@ -635,6 +635,17 @@ void DocBatch::clear() {
   serde = false;
 }
 
+uint32_t DocBatch::find(const char* p, uint32_t n) const {
+  if (islots.empty()) return NONE;
+  size_t mask = islots.size() - 1;
+  size_t h = fnv1a(p, n) & mask;
+  while (islots[h]) {
+    if (ilen[h] == n && memcmp(bytes.data() + islots[h] - 1, p, n) == 0) return islots[h] - 1;
+    h = (h + 1) & mask;
+  }
+  return NONE;
+}
+
 uint32_t DocBatch::intern(const char* p, uint32_t n, uint32_t hash) {
   if ((iused + 1) * 2 > islots.size()) {
     size_t cap = islots.empty() ? 4096 : islots.size() * 2;
@@ -869,8 +880,8 @@ struct JsonFast {
       str(true);
       d.kind = K_STRING;
       d.count = (uint32_t)sbuf.size();
-      d.b = fnv1a(sbuf.data(), sbuf.size());
-      d.a = b.intern(sbuf.data(), d.count, d.b);
+      d.a = b.intern(sbuf.data(), d.count, fnv1a(sbuf.data(), sbuf.size()));
+      d.b = d.a;
       return;
     }
     if (c == '{' || c == '[') {
@@ -891,8 +902,8 @@ struct JsonFast {
           str(true);
           DNode& e = b.nodes[cs];
           e.key_len = (uint32_t)sbuf.size();
-          e.key_hash = fnv1a(sbuf.data(), sbuf.size());
-          e.key_off = b.intern(sbuf.data(), e.key_len, e.key_hash);
+          e.key_off = b.intern(sbuf.data(), e.key_len, fnv1a(sbuf.data(), sbuf.size()));
+          e.key_hash = e.key_off;
           b.kline[cs] = kl; b.kcol[cs] = kc;
           while (s[i] == ' ') i++;
           i++;  // ':'

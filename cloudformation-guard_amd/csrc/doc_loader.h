@@ -33,7 +33,11 @@ struct DocBatch {
   std::vector<uint32_t> islots;          // open addressing: pool offset + 1 (0 = empty)
   std::vector<uint32_t> ilen;            // parallel to islots: string length
   size_t iused = 0;
+  // The pool holds each distinct string once per batch (merge_batches re-interns per-thread
+  // parts), so a string's pool offset is its id: DNode.b of a string and DNode.key_hash of a map
+  // entry carry that id, and the device tests string equality by comparing ids.
   uint32_t intern(const char* p, uint32_t n, uint32_t hash);
+  uint32_t find(const char* p, uint32_t n) const;   // pool offset of an interned string, or NONE
 
   size_t ndocs() const { return roots.size(); }
   std::string path(uint64_t base, uint32_t node) const;  // JSON pointer ("" for a root)
