@@ -31,6 +31,7 @@
 namespace gg {
 __global__ void guard_eval_kernel(LaunchArgs A);
 __global__ void guard_eval_lanes_kernel(LaunchArgs A);
+__global__ void resource_type_kernel(DevBatch D);
 __global__ void rule_count_kernel(const TileOut* tiles, const uint8_t* rule_status, const DevProg* progs, uint32_t nfiles,
                                   uint32_t ntiles, uint32_t max_top, unsigned long long* counts);
 }
@@ -190,6 +191,10 @@ struct gg_session {
   DBuf<char> d_bytes;
   DBuf<uint32_t> d_roots;
   DBuf<uint64_t> d_base;
+  DBuf<uint32_t> d_res_map;     // per doc: root.Resources node (resource-type column, DevBatch)
+  DBuf<uint32_t> d_tix_off;
+  DBuf<uint32_t> d_tix;
+  uint32_t type_key = NONE;
   DBuf<DevProg> d_progs;
   DBuf<uint8_t> d_heaps;        // wave mode: one heap per wave slot
   DBuf<uint8_t> d_lane_heaps;   // lane mode: one heap per lane
@@ -239,6 +244,34 @@ void session_upload(gg_session* s) {
   s->d_bytes.upload(s->docs.bytes.data(), s->docs.bytes.size() ? s->docs.bytes.size() : 1, st);
   s->d_roots.upload(s->docs.roots.data(), s->docs.roots.size(), st);
   s->d_base.upload(s->docs.base.data(), s->docs.base.size(), st);
+  {
+    // resource-type column layout: root.Resources of every document and its entry count
+    const DocBatch& D = s->docs;
+    const uint32_t rkey = D.find("Resources", 9);
+    s->type_key = D.find("Type", 4);
+    size_t nd = D.ndocs();
+    std::vector<uint32_t> rmap(nd, NONE), toff(nd, 0);
+    size_t total = 0;
+    if (rkey != NONE && s->type_key != NONE) {
+      for (size_t d = 0; d < nd; d++) {
+        const DNode* N = D.nodes.data() + D.base[d];
+        const DNode& root = N[D.roots[d]];
+        toff[d] = (uint32_t)total;
+        if (root.kind != K_MAP) continue;
+        for (uint32_t k = 0; k < root.count; k++) {
+          const DNode& e = N[root.a + k];
+          if (e.key_hash != rkey) continue;
+          if (e.kind == K_MAP) { rmap[d] = root.a + k; total += e.count; }
+          break;
+        }
+      }
+    }
+    if (total > 0xFFFFFFF0u) { std::fill(rmap.begin(), rmap.end(), NONE); total = 0; }
+    s->d_res_map.upload(rmap.data(), std::max<size_t>(nd, 1), st);
+    s->d_tix_off.upload(toff.data(), std::max<size_t>(nd, 1), st);
+    s->d_tix.alloc(std::max<size_t>(total, 1));
+    HIPCHK(hipStreamSynchronize(st));   // the host vectors above die at the end of this scope
+  }
   std::vector<DevProg> dps;
   s->max_top = 1;
   StringIds ids;
@@ -287,6 +320,7 @@ void session_launch(gg_session* s) {
   HIPCHK(hipMemsetAsync(counts, 0, s->ncounts * sizeof(unsigned long long), st));
   LaunchArgs A{};
   A.docs.nodes = s->d_nodes.p; A.docs.bytes = s->d_bytes.p; A.docs.roots = s->d_roots.p; A.docs.base = s->d_base.p; A.docs.ndocs = (uint32_t)s->docs.ndocs();
+  A.docs.res_map = s->d_res_map.p; A.docs.tix_off = s->d_tix_off.p; A.docs.tix = s->d_tix.p; A.docs.type_key = s->type_key;
   A.progs = s->d_progs.p; A.nfiles = (uint32_t)s->progs.size();
   A.ntiles = ntiles; A.tile_base = 0;
   A.heaps = s->d_heaps.p; A.heap_bytes = s->heap_bytes; A.nslots = s->nslots;
@@ -306,6 +340,11 @@ void session_launch(gg_session* s) {
   }
   s->ev0 = s->evq[s->nq].first; s->ev1 = s->evq[s->nq].second; s->nq++;
   HIPCHK(hipEventRecord(s->ev0, st));
+  if (s->type_key != NONE && A.docs.ndocs) {
+    uint32_t blocks = std::min<uint32_t>((A.docs.ndocs + 3) / 4, g_dev.ncu * 16);
+    hipLaunchKernelGGL(resource_type_kernel, dim3(blocks), dim3(256), 0, st, A.docs);
+    HIPCHK(hipGetLastError());
+  }
   if (s->mode != 1) {
     hipLaunchKernelGGL(guard_eval_lanes_kernel, dim3(s->lane_slots), dim3(64), 0, st, A);
     HIPCHK(hipGetLastError());

@@ -44,6 +44,14 @@ struct DevBatch {
   const uint32_t* roots;   // per doc: root node (document-relative)
   const uint64_t* base;    // per doc: global index of the document's first node
   uint32_t ndocs;
+  // CloudFormation resource-type column: for each document whose root has a `Resources` map,
+  // tix[tix_off[d] + j] describes entry j of that map (TIX_* or the string id of its `Type`).
+  // Built per launch by resource_type_kernel; `Resources.*[ Type == '...' ]` filters read it
+  // instead of walking every resource's entries.
+  const uint32_t* res_map;   // per doc: document-relative node of root.Resources (map), or NONE
+  const uint32_t* tix_off;   // per doc: first column entry
+  uint32_t* tix;
+  uint32_t type_key;         // string id of "Type" (NONE if no document has the key)
 };
 
 struct LaunchArgs {

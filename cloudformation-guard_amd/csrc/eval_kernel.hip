@@ -74,6 +74,9 @@ __device__ __attribute__((always_inline)) inline void tile_begin(CtxT& c, const 
   c.P = P; c.dn = A.docs.nodes + A.docs.base[doc]; c.db = A.docs.bytes; c.heap = heap; c.cap = heap_bytes;
   c.tmp = frames_bytes + recs_bytes; c.pers = heap_bytes; c.nframes = 0; c.nrec = 0;
   c.err = 0; c.err_a = 0; c.err_b = 0; c.suppress = 0; c.rec_created = 0; c.depth = 0; c.nsyn = 0;
+  c.resmap = A.docs.res_map ? A.docs.res_map[doc] : NONE;
+  c.tix = c.resmap != NONE ? A.docs.tix + A.docs.tix_off[doc] : nullptr;
+  c.type_key = A.docs.type_key; c.ffok = NONE;
 #ifdef GG_STATS
   for (int i = 0; i < 8; i++) c.st[i] = 0;
 #endif
@@ -216,6 +219,35 @@ __global__ void __launch_bounds__(64) guard_eval_kernel(LaunchArgs A) {
 }  // namespace gg
 
 namespace gg {
+
+// Resource-type column (DevBatch::tix): one wavefront per document, lanes over the entries of the
+// root's `Resources` map (coalesced reads of the contiguous entry block), each lane looking up its
+// resource's exact `Type` key.  Runs at the start of every evaluation launch.
+__global__ void __launch_bounds__(256) resource_type_kernel(DevBatch D) {
+  const uint32_t lane = __lane_id();
+  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) / 64u;
+  const uint32_t nwaves = gridDim.x * blockDim.x / 64u;
+  for (uint32_t d = wave; d < D.ndocs; d += nwaves) {
+    const uint32_t rm = D.res_map[d];
+    if (rm == NONE) continue;
+    const DNode* dn = D.nodes + D.base[d];
+    const DNode m = dn[rm];
+    uint32_t* out = D.tix + D.tix_off[d];
+    for (uint32_t j = lane; j < m.count; j += 64u) {
+      const DNode r = dn[m.a + j];
+      uint32_t v = TIX_UNDECIDED;
+      if (r.kind == K_MAP) {
+        for (uint32_t k = 0; k < r.count; k++) {
+          const DNode e = dn[r.a + k];
+          if (e.key_hash != D.type_key) continue;
+          v = e.kind == K_STRING ? e.b : (e.kind == K_LIST ? TIX_UNDECIDED : TIX_NOT_STRING);
+          break;
+        }
+      }
+      out[j] = v;
+    }
+  }
+}
 
 // Per-(rules file, top rule) PASS/FAIL/SKIP tallies over every tile of one evaluation, plus a
 // per-file line (index max_top) holding file statuses and errored tiles (status slot 3).

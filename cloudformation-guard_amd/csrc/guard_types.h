@@ -24,6 +24,9 @@ enum Kind : uint32_t {
 };
 
 static const uint32_t NONE = 0xFFFFFFFFu;
+// resource-type column entries (eval_kernel.hip resource_type_kernel): a string id, or
+static const uint32_t TIX_UNDECIDED = 0xFFFFFFFFu;   // not a map / no exact `Type` key / Type is a list
+static const uint32_t TIX_NOT_STRING = 0xFFFFFFFEu;  // `Type` present but neither string nor list
 static const uint32_t LIT_BIT = 0x80000000u;
 
 struct DNode {
