@@ -123,6 +123,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
       tile_begin(c, A, P, doc, heap, A.lane_heap_bytes, FRAMES_BYTES, RECS_BYTES);
       c.lane16 = lane * 16u;
       c.syn_off = alloc_pers(c, 256 * 16);
+      c.wbase = alloc_pers(c, WLEVELS * (uint32_t)sizeof(WLevel)); c.wdepth = 0;
       c.memo = alloc_pers(c, (P->n_slots ? P->n_slots : 1) * 4);
       if (!c.err) for (uint32_t i = 0; i < P->n_slots; i++) u32a(c, c.memo)[i] = 3u;
       push_frame(c, F_ROOT, NONE, A.docs.roots[doc], P->root_block);
@@ -187,6 +188,7 @@ __global__ void __launch_bounds__(64) guard_eval_kernel(LaunchArgs A) {
     tile_begin(c, A, P, doc, heap, A.heap_bytes, FRAMES_BYTES, RECS_BYTES);
     c.lane16 = 0;
     c.syn_off = alloc_pers(c, 256 * 16);
+      c.wbase = alloc_pers(c, WLEVELS * (uint32_t)sizeof(WLevel)); c.wdepth = 0;
     c.memo = alloc_pers(c, (P->n_slots ? P->n_slots : 1) * 4);
     if (!c.err) for (uint32_t i = 0; i < P->n_slots; i++) u32a(c, c.memo)[i] = 3u;
     push_frame(c, F_ROOT, NONE, A.docs.roots[doc], P->root_block);
