@@ -61,7 +61,7 @@ def _oracle_worker(args):
     return time.time() - t, n * len(rules)
 
 
-def cpu_baseline(n_resources, per_core=150):
+def cpu_baseline(n_resources, per_core=600):
     import multiprocessing as mp
     cores = _cpu_share()
     ctx = mp.get_context("spawn")
@@ -100,7 +100,7 @@ def main():
     ap.add_argument("--resources", type=int, default=50)
     ap.add_argument("--threads", type=int, default=0, help="host loader threads (default: CPU share)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-per-core", type=int, default=150)
+    ap.add_argument("--cpu-per-core", type=int, default=600)
     args = ap.parse_args()
 
     import torch

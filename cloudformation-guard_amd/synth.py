@@ -118,3 +118,131 @@ rule EBS_VOLUMES_ENCRYPTED {
     }
 }
 """
+
+
+# ---------------------------------------------------------------------------------------------
+# cfg 4 (BASELINE.json configs[3]; SURVEY.md 8d): Terraform plan JSON -- planned_values with a
+# root module and nested child modules (nesting depth 6-10 under the plan root) and a
+# resource_changes array, 200-2000 entries per plan at full size.  Doc i: xorshift32 seed 4242 ^ i.
+
+TF_TYPES = ["aws_s3_bucket", "aws_instance", "aws_iam_role", "aws_security_group", "aws_db_instance"]
+
+
+def _tf_values(r, t, k):
+    if t == "aws_s3_bucket":
+        v = {"bucket": "tf-bucket-%d" % k, "acl": r.pick(["private", "public-read", "log-delivery-write"]),
+             "force_destroy": r.chance(0.3)}
+        if r.chance(0.7):
+            v["tags"] = {"Name": "b%d" % k, "Environment": r.pick(["Dev", "Prod", "null"])}
+        elif r.chance(0.5):
+            v["tags"] = None
+        if r.chance(0.6):
+            v["versioning"] = [{"enabled": r.chance(0.7), "mfa_delete": False}]
+        if r.chance(0.5):
+            v["server_side_encryption_configuration"] = [{"rule": [{"apply_server_side_encryption_by_default": [
+                {"sse_algorithm": r.pick(["aws:kms", "AES256"]), "kms_master_key_id": None}]}]}]
+        return v
+    if t == "aws_instance":
+        v = {"ami": "ami-%08x" % r.next(), "instance_type": r.pick(["t3.micro", "m5.large", "c5.xlarge", "t2.nano"]),
+             "monitoring": r.chance(0.5), "ebs_optimized": r.chance(0.6)}
+        if r.chance(0.8):
+            v["root_block_device"] = [{"encrypted": r.chance(0.7), "volume_size": 8 + r.next() % 200,
+                                       "volume_type": r.pick(["gp2", "gp3"])}]
+        if r.chance(0.6):
+            v["tags"] = {"Name": "i%d" % k}
+        return v
+    if t == "aws_iam_role":
+        return {"name": "role-%d" % k, "max_session_duration": 3600 * (1 + r.next() % 12),
+                "assume_role_policy": json.dumps({"Version": "2012-10-17", "Statement": [
+                    {"Effect": "Allow", "Principal": {"Service": r.pick(["ec2.amazonaws.com", "lambda.amazonaws.com"])},
+                     "Action": "sts:AssumeRole"}]}, separators=(",", ":"))}
+    if t == "aws_security_group":
+        ing = []
+        for _ in range(1 + r.next() % 3):
+            port = r.pick([22, 80, 443, 3389])
+            ing.append({"from_port": port, "to_port": port, "protocol": "tcp",
+                        "cidr_blocks": [r.pick(["0.0.0.0/0", "10.0.0.0/8", "172.16.0.0/12"])],
+                        "description": r.pick(["ssh", "web", "rdp", ""])})
+        return {"name": "sg-%d" % k, "ingress": ing, "egress": [{"from_port": 0, "to_port": 0, "protocol": "-1",
+                                                                  "cidr_blocks": ["0.0.0.0/0"]}]}
+    return {"engine": r.pick(["mysql", "postgres"]), "storage_encrypted": r.chance(0.6),
+            "publicly_accessible": r.chance(0.2), "backup_retention_period": r.next() % 14,
+            "allocated_storage": 20 + r.next() % 1000}
+
+
+def _tf_module(r, prefix, n, depth, k0):
+    res = []
+    for k in range(n):
+        t = TF_TYPES[r.next() % len(TF_TYPES)]
+        name = "r%d" % (k0 + k)
+        res.append({"address": "%s%s.%s" % (prefix, t, name), "mode": "managed", "type": t, "name": name,
+                    "provider_name": "registry.terraform.io/hashicorp/aws", "schema_version": 0,
+                    "values": _tf_values(r, t, k0 + k)})
+    mod = {"resources": res}
+    if depth > 0:
+        child = _tf_module(r, "%smodule.m%d." % (prefix, depth), max(1, n // 4), depth - 1, k0 + n)
+        child["address"] = "%smodule.m%d" % (prefix, depth)
+        mod["child_modules"] = [child]
+    return mod
+
+
+def tf_plan_doc(i, n_resources=200):
+    r = XorShift32(4242 ^ i)
+    depth = 2 + r.next() % 3   # module nesting: the deepest leaf values sit 6-10 levels below the root
+    root = _tf_module(r, "", n_resources, depth, 0)
+    changes = []
+    for res in root["resources"]:
+        act = r.pick([["create"], ["update"], ["no-op"], ["delete", "create"]])
+        changes.append({"address": res["address"], "mode": "managed", "type": res["type"], "name": res["name"],
+                        "change": {"actions": act, "before": None if act == ["create"] else res["values"],
+                                   "after": res["values"], "after_unknown": {}}})
+    return {"format_version": "1.1", "terraform_version": "1.5.7",
+            "planned_values": {"root_module": root}, "resource_changes": changes}
+
+
+def tf_corpus(n, start=0, n_resources=200):
+    return [json.dumps(tf_plan_doc(start + i, n_resources), separators=(",", ":")) for i in range(n)]
+
+
+# ---------------------------------------------------------------------------------------------
+# cfg 5 (BASELINE.json configs[4]; SURVEY.md 8d): AWS Config configuration items of one account
+# snapshot, wrapped into a CloudFormation-shaped `Resources` map keyed by resource id (the
+# network-reachability rules query `Resources.*`).  Each snapshot holds Redshift subnet groups,
+# subnets, route-table associations, route tables, routes and gateways with `Ref` joins between
+# them, plus configuration-item metadata.  Doc i: xorshift32 seed 5151 ^ i.
+
+def config_snapshot_doc(i, n_groups=4):
+    r = XorShift32(5151 ^ i)
+    res = {}
+
+    def ci(rid, t, props):
+        res[rid] = {"Type": t, "Properties": props,
+                    "configurationItemStatus": r.pick(["OK", "ResourceDiscovered", "ResourceDeleted"]),
+                    "resourceId": rid, "awsRegion": r.pick(["us-east-1", "eu-west-1"]),
+                    "tags": {"owner": r.pick(["net", "data", "sec"])}}
+
+    for g in range(n_groups):
+        subnets = ["subnet%da%d" % (g, j) for j in range(1 + r.next() % 3)]
+        refs = [{"Ref": s} for s in subnets]
+        if r.chance(0.3):
+            refs.append("subnet-%08x" % r.next())
+        ci("rcsg%d" % g, r.pick(["AWS::Redshift::ClusterSubnetGroup", "AWS::Redshift::ClusterSubnetGroup",
+                                 "AWS::RDS::DBSubnetGroup"]), {"SubnetIds": refs, "Description": "group %d" % g})
+        rt = "rt%d" % g
+        ci(rt, "AWS::EC2::RouteTable" if r.chance(0.9) else "AWS::EC2::Subnet", {"VpcId": {"Ref": "vpc"}})
+        gw = "gw%d" % g
+        ci(gw, r.pick(["AWS::EC2::InternetGateway", "AWS::EC2::TransitGateway", "AWS::EC2::NatGateway"]), {})
+        ci("route%d" % g, "AWS::EC2::Route", {"RouteTableId": {"Ref": rt}, "GatewayId": {"Ref": gw},
+                                              "DestinationCidrBlock": r.pick(["0.0.0.0/0", "10.0.0.0/8"])})
+        for s in subnets:
+            ci(s, "AWS::EC2::Subnet" if r.chance(0.95) else "AWS::EC2::Instance",
+               {"CidrBlock": "10.%d.%d.0/24" % (g, r.next() % 256), "MapPublicIpOnLaunch": r.chance(0.3),
+                "VpcId": {"Ref": "vpc"}})
+            ci("assoc-%s" % s, "AWS::EC2::SubnetRouteTableAssociation", {"SubnetId": {"Ref": s},
+                                                                          "RouteTableId": {"Ref": rt}})
+    ci("vpc", "AWS::EC2::VPC", {"CidrBlock": "10.0.0.0/16", "EnableDnsSupport": True})
+    return {"Resources": res}
+
+
+def config_corpus(n, start=0, n_groups=4):
+    return [json.dumps(config_snapshot_doc(start + i, n_groups), separators=(",", ":")) for i in range(n)]

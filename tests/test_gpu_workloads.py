@@ -1,0 +1,80 @@
+"""GPU parity on the other BASELINE.json workloads (configs[3], configs[4]) and on structural
+equality, through the C ABI, against the CPU oracle.
+
+* cfg 4: Terraform plan JSON (synth.tf_corpus) x tests/golden/tf_rulepack (the reference's
+  terraform-infra-related/check-s3-tags-present.guard plus pack-local filter-heavy rules);
+* cfg 5: AWS Config snapshots wrapped as Resources maps (synth.config_corpus) x
+  tests/golden/net_rulepack (the reference's network-reachability-analysis rule plus pack-local
+  regex / join rules);
+* container equality (tests/golden/edge_rulepack): map / list ==, !=, IN over the iterative
+  compare_eq / PartialEq.
+
+Small batches are compared byte-for-byte with the oracle's structured JSON; full-size plans
+(2000 resources, cfg 4's upper bound) are compared with the oracle on two documents and, on a
+larger batch, through a size-independent property: the lane-per-tile and wave-per-tile kernels
+produce identical reports.
+"""
+import os
+
+import pytest
+
+import guard_amd
+import synth
+from guard_oracle import validate_structured as oracle_validate
+
+pytestmark = pytest.mark.gpu
+G = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _pack(d):
+    p = os.path.join(G, d)
+    return [(f, open(os.path.join(p, f)).read()) for f in sorted(os.listdir(p)) if f.endswith(".guard")]
+
+
+def _vs_oracle(docs, rules, prefix):
+    data = [("%s-%d.json" % (prefix, i), d) for i, d in enumerate(docs)]
+    exp, ecode, _ = oracle_validate(rules, data)
+    out, code = guard_amd.validate_structured(rules, data)
+    assert code == ecode
+    assert out == exp
+
+
+def _session_report(docs, rules, mode, prefix):
+    s = guard_amd.Session()
+    s.configure(mode, 0)
+    for name, text in rules:
+        s.add_rules(text, name)
+    s.add_docs(docs, ["%s-%d.json" % (prefix, i) for i in range(len(docs))])
+    s.eval(1)
+    assert s.stat(s.STAT["errors"]) == 0
+    out, code = s.report()
+    s.close()
+    return out, code
+
+
+def test_terraform_plans_vs_oracle():
+    _vs_oracle(synth.tf_corpus(12, start=0, n_resources=40), _pack("tf_rulepack"), "plan")
+
+
+def test_terraform_full_size_plans_vs_oracle():
+    _vs_oracle(synth.tf_corpus(2, start=100, n_resources=2000), _pack("tf_rulepack"), "bigplan")
+
+
+def test_terraform_full_size_lane_matches_wave():
+    docs = synth.tf_corpus(70, start=200, n_resources=600)   # two lane batches, the second ragged
+    rules = _pack("tf_rulepack")
+    assert _session_report(docs, rules, 0, "p") == _session_report(docs, rules, 1, "p")
+
+
+def test_config_snapshots_vs_oracle():
+    _vs_oracle(synth.config_corpus(24, start=0, n_groups=4), _pack("net_rulepack"), "snapshot")
+
+
+def test_config_snapshots_lane_matches_wave():
+    docs = synth.config_corpus(130, start=1000, n_groups=8)
+    rules = _pack("net_rulepack")
+    assert _session_report(docs, rules, 0, "s") == _session_report(docs, rules, 1, "s")
+
+
+def test_container_equality_vs_oracle():
+    _vs_oracle(synth.cfn_corpus(16, start=300, n_resources=20), _pack("edge_rulepack"), "doc")
