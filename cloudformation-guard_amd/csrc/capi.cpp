@@ -199,6 +199,8 @@ struct gg_session {
   DBuf<uint8_t> d_heaps;        // wave mode: one heap per wave slot
   DBuf<uint8_t> d_lane_heaps;   // lane mode: one heap per lane
   DBuf<uint32_t> d_retry;       // tiles handed from lane mode to wave mode
+  DBuf<uint8_t> d_big_heaps;    // large-heap wave pass: tiles that outgrow the wave heap
+  DBuf<uint32_t> d_retry2;      // tiles handed from the wave pass to the large-heap pass
   DBuf<TileOut> d_tiles;
   DBuf<uint8_t> d_rule_status;
   DBuf<Rec> d_recs;
@@ -218,6 +220,9 @@ struct gg_session {
   uint32_t nslots = 0;            // wave-mode grid
   uint32_t lane_slots = 0;        // lane-mode grid (waves)
   uint32_t heap_bytes = 512 * 1024;
+  static constexpr uint32_t kWaveFrames = 16 * 1024, kWaveRecs = 64 * 1024;
+  // large-heap pass (rare: documents with thousands of failing clause values or deep nesting)
+  static constexpr uint32_t kBigHeap = 32u << 20, kBigFrames = 1u << 20, kBigRecs = 16u << 20, kBigSlots = 8;
   uint32_t lane_heap_bytes = 64 * 1024;
   int32_t mode = 0;               // 0: lane mode + wave-mode retry; 1: wave mode only
   size_t rec_cap = 0;
@@ -294,6 +299,8 @@ void session_upload(gg_session* s) {
   s->lane_slots = s->mode == 1 ? 0 : (uint32_t)std::min<size_t>(std::max<size_t>(nbatches, 1), (size_t)g_dev.ncu * lane_waves_per_cu);
   s->d_lane_heaps.alloc((size_t)s->lane_slots * 64 * s->lane_heap_bytes);
   s->d_retry.alloc(std::max<size_t>(ntiles, 1));
+  s->d_retry2.alloc(std::max<size_t>(ntiles, 1));
+  s->d_big_heaps.alloc((size_t)gg_session::kBigSlots * gg_session::kBigHeap);
   s->d_tiles.alloc(std::max<size_t>(ntiles, 1));
   s->d_rule_status.alloc(std::max<size_t>(ntiles * s->max_top, 1));
   s->rec_cap = std::min<size_t>(std::max<size_t>(ntiles * 48, 4096), (size_t)96 * 1024 * 1024);
@@ -330,6 +337,8 @@ void session_launch(gg_session* s) {
   A.retry_count = s->d_counters.p + 3;
   A.lane_heaps = s->d_lane_heaps.p; A.lane_heap_bytes = s->lane_heap_bytes;
   A.retry_list = s->mode == 1 ? nullptr : s->d_retry.p;
+  A.wave_frames_bytes = gg_session::kWaveFrames; A.wave_recs_bytes = gg_session::kWaveRecs;
+  A.retry2_list = s->d_retry2.p; A.retry2_count = s->d_counters.p + 4;
   A.stats = s->d_stats.p;
   if (!ntiles) return;
   if (s->nq == s->evq.size()) {
@@ -351,6 +360,17 @@ void session_launch(gg_session* s) {
   }
   hipLaunchKernelGGL(guard_eval_kernel, dim3(s->nslots), dim3(64), 0, st, A);
   HIPCHK(hipGetLastError());
+  {
+    // large-heap pass over the wave pass's overflow list (counters[4]; its cursor is counters[6]);
+    // normally empty, so its waves exit at once
+    LaunchArgs B = A;
+    B.retry_list = s->d_retry2.p; B.retry_count = s->d_counters.p + 4; B.tile_cursor = s->d_counters.p + 5;
+    B.heaps = s->d_big_heaps.p; B.heap_bytes = gg_session::kBigHeap; B.nslots = gg_session::kBigSlots;
+    B.wave_frames_bytes = gg_session::kBigFrames; B.wave_recs_bytes = gg_session::kBigRecs;
+    B.retry2_list = nullptr; B.retry2_count = nullptr;
+    hipLaunchKernelGGL(guard_eval_kernel, dim3(gg_session::kBigSlots), dim3(64), 0, st, B);
+    HIPCHK(hipGetLastError());
+  }
   HIPCHK(hipEventRecord(s->ev1, st));
   uint32_t cblocks = std::min<uint32_t>((ntiles + 255) / 256, g_dev.ncu * 4);
   hipLaunchKernelGGL(rule_count_kernel, dim3(cblocks), dim3(256), s->ncounts * sizeof(uint32_t), st, s->d_tiles.p,

@@ -74,6 +74,10 @@ struct LaunchArgs {
   uint32_t lane_heap_bytes;
   uint32_t* retry_list;    // tiles the lane kernel hands to the wave kernel (null: wave kernel runs all)
   uint32_t* retry_count;
+  uint32_t wave_frames_bytes;  // wave mode: frame region at the start of each wave heap
+  uint32_t wave_recs_bytes;    // wave mode: record staging region after it
+  uint32_t* retry2_list;       // tiles the wave pass hands to the large-heap pass (null: none)
+  uint32_t* retry2_count;
   unsigned long long* stats;   // diagnostic counters [8] (stats build variant), else unused
 };
 

@@ -72,7 +72,7 @@ __device__ __attribute__((always_inline)) inline void tile_begin(CtxT& c, const 
                                                                  uint32_t doc, uint8_t* heap, uint32_t heap_bytes,
                                                                  uint32_t frames_bytes, uint32_t recs_bytes) {
   c.P = P; c.dn = A.docs.nodes + A.docs.base[doc]; c.db = A.docs.bytes; c.heap = heap; c.cap = heap_bytes;
-  c.tmp = frames_bytes + recs_bytes; c.pers = heap_bytes; c.nframes = 0; c.nrec = 0;
+  c.tmp = frames_bytes + recs_bytes; c.pers = heap_bytes; c.fcap = frames_bytes; c.rcap = recs_bytes; c.nframes = 0; c.nrec = 0;
   c.err = 0; c.err_a = 0; c.err_b = 0; c.suppress = 0; c.rec_created = 0; c.depth = 0; c.nsyn = 0;
   c.resmap = A.docs.res_map ? A.docs.res_map[doc] : NONE;
   c.tix = c.resmap != NONE ? A.docs.tix + A.docs.tix_off[doc] : nullptr;
@@ -185,7 +185,7 @@ __global__ void __launch_bounds__(64) guard_eval_kernel(LaunchArgs A) {
     uint32_t tile = A.retry_list ? A.retry_list[t] : A.tile_base + t;
     uint32_t doc = tile / A.nfiles, file = tile % A.nfiles;
     if (file != staged) { P = stage_program(&A.progs[file], &s_prog, s_blob); staged = file; }
-    tile_begin(c, A, P, doc, heap, A.heap_bytes, FRAMES_BYTES, RECS_BYTES);
+    tile_begin(c, A, P, doc, heap, A.heap_bytes, A.wave_frames_bytes, A.wave_recs_bytes);
     c.lane16 = 0;
     c.syn_off = alloc_pers(c, 256 * 16);
       c.wbase = alloc_pers(c, WLEVELS * (uint32_t)sizeof(WLevel)); c.wdepth = 0;
@@ -201,13 +201,17 @@ __global__ void __launch_bounds__(64) guard_eval_kernel(LaunchArgs A) {
       if (st == ST_PASS) passes++; else if (st == ST_FAIL) fails++;
     }
     uint32_t status = fails ? ST_FAIL : (passes ? ST_PASS : ST_SKIP);
+    // a tile that outgrows this pass's heap, record staging or frame limits goes to the next pass
+    // (a larger heap per wave), when there is one
+    if (A.retry2_list && lane == 0 && (c.err == E_HEAP || c.err == E_RECORDS || c.err == E_DEPTH))
+      A.retry2_list[atomicAdd(A.retry2_count, 1u)] = tile;
     // publish records
     uint32_t off = 0;
     uint32_t n = c.err ? 0 : c.nrec;
     if (lane == 0 && n) off = atomicAdd(A.rec_cursor, n);
     off = __shfl(off, 0);
     if (n && off + n > A.rec_cap) { c.err = E_RECORDS; n = 0; }
-    const Rec* src = (const Rec*)(heap + FRAMES_BYTES);
+    const Rec* src = (const Rec*)(heap + c.fcap);
     for (uint32_t i = lane; i < n; i += 64) A.recs[off + i] = src[i];
     if (lane == 0) {
       TileOut o;
