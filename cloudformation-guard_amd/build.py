@@ -39,8 +39,11 @@ def build(verbose=False, variant=""):
     out = OUT if not variant else OUT.replace(".so", "_" + variant + ".so")
     obj_dir = OBJ if not variant else OBJ + "_" + variant
     flags = FLAGS + (["-DGG_STATS"] if variant == "stats" else [])
-    if variant.startswith("eu"):   # occupancy experiments: eu<N> = amdgpu_waves_per_eu(N)
-        flags = [f for f in flags if not f.startswith("-DGG_LANE_WAVES_PER_EU=")] + ["-DGG_LANE_WAVES_PER_EU=" + variant[2:]]
+    if variant.startswith("eu"):   # occupancy experiments: eu<N>[p<W>] = amdgpu_waves_per_eu(N), W-word LDS program window
+        eu, _, pw = variant[2:].partition("p")
+        flags = [f for f in flags if not f.startswith("-DGG_LANE_WAVES_PER_EU=")] + ["-DGG_LANE_WAVES_PER_EU=" + eu]
+        if pw:
+            flags.append("-DGG_LDS_PROG_WORDS=" + pw)
     os.makedirs(obj_dir, exist_ok=True)
     headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".h", ".inc"))]
     headers.append(os.path.join(HERE, "..", "include", "cfn_guard_mi355x.h"))

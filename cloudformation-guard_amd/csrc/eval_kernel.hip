@@ -40,7 +40,10 @@ namespace ln {
 // (KBs: clauses, query parts, strings, literals) is copied into the workgroup's LDS and the
 // DevProg pointers are rebased onto the copy, so the interpreter's program reads are LDS reads
 // instead of dependent global loads.  Programs larger than the LDS window stay in HBM.
-static const uint32_t LDS_PROG_WORDS = 2048;   // 8 KB per workgroup (one wave)
+#ifndef GG_LDS_PROG_WORDS
+#define GG_LDS_PROG_WORDS 2048
+#endif
+static const uint32_t LDS_PROG_WORDS = GG_LDS_PROG_WORDS;   // 8 KB per workgroup (one wave)
 
 __device__ __attribute__((always_inline)) inline const DevProg* stage_program(const DevProg* G, DevProg* sp, uint4* sblob) {
   const uint32_t lane = __lane_id();
@@ -105,7 +108,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
   __shared__ Ctx s_ctx[64];
   __shared__ DevProg s_prog;
   __shared__ uint4 s_blob[LDS_PROG_WORDS / 4];
-  Ctx& c = s_ctx[lane];
+  LCtx& c = *(LCtx*)&s_ctx[lane];
   uint32_t staged = NONE;
   const DevProg* P = nullptr;
   for (;;) {
@@ -174,7 +177,7 @@ __global__ void __launch_bounds__(64) guard_eval_kernel(LaunchArgs A) {
   __shared__ Ctx s_ctx[64];
   __shared__ DevProg s_prog;
   __shared__ uint4 s_blob[LDS_PROG_WORDS / 4];
-  Ctx& c = s_ctx[lane];
+  LCtx& c = *(LCtx*)&s_ctx[lane];
   uint32_t staged = NONE;
   const DevProg* P = nullptr;
   for (;;) {
