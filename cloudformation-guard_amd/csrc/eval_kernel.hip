@@ -74,7 +74,7 @@ template <typename CtxT>
 __device__ __attribute__((always_inline)) inline void tile_begin(CtxT& c, const LaunchArgs& A, const DevProg* P,
                                                                  uint32_t doc, uint8_t* heap, uint32_t heap_bytes,
                                                                  uint32_t frames_bytes, uint32_t recs_bytes) {
-  c.P = P; c.dn = A.docs.nodes + A.docs.base[doc]; c.db = A.docs.bytes; c.heap = heap; c.cap = heap_bytes;
+  c.P = (decltype(c.P))P; c.dn = A.docs.nodes + A.docs.base[doc]; c.db = A.docs.bytes; c.heap = heap; c.cap = heap_bytes;
   c.tmp = frames_bytes + recs_bytes; c.pers = heap_bytes; c.fcap = frames_bytes; c.rcap = recs_bytes; c.nframes = 0; c.nrec = 0;
   c.err = 0; c.err_a = 0; c.err_b = 0; c.suppress = 0; c.rec_created = 0; c.depth = 0; c.nsyn = 0;
   c.resmap = A.docs.res_map ? A.docs.res_map[doc] : NONE;
@@ -122,6 +122,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
     if (file != staged) { P = stage_program(&A.progs[file], &s_prog, s_blob); staged = file; }
     const uint32_t tile = doc * A.nfiles + file;
     uint32_t status = ST_SKIP, n = 0;
+    if (P != &s_prog) {
+      // the program did not fit the LDS window: lane mode reads it through LDS-typed pointers only,
+      // so the whole batch goes to the wave kernel
+      if (active) A.retry_list[atomicAdd(A.retry_count, 1u)] = tile;
+      continue;
+    }
     if (active) {
       tile_begin(c, A, P, doc, heap, A.lane_heap_bytes, FRAMES_BYTES, RECS_BYTES);
       c.lane16 = lane * 16u;
