@@ -35,8 +35,22 @@ def _pav_json(v):
     return OMap([("path", s["path"]), ("value", s["value"])])
 
 
-def _messages(custom, error):
-    return OMap([("custom_message", custom), ("error_message", error)])
+class Msgs(OMap):
+    """Messages (eval_context.rs:1608-1614): custom_message, error_message; ``location`` is
+    skip_serializing but read by the SARIF writer (sarif.rs:139-142)"""
+    __slots__ = ("location",)
+
+    def __init__(self, items, location=None):
+        OMap.__init__(self, items)
+        self.location = location
+
+
+def _loc(v):
+    return (v.line, v.col)
+
+
+def _messages(custom, error, location=None):
+    return Msgs([("custom_message", custom), ("error_message", error)], location)
 
 
 def _unary_cmp_msg(cmp, neg):
@@ -128,13 +142,15 @@ def report_all_failed(checks):
                     res = frm[1]
                     msg = "Check was not compliant as property [%s] %s.%s" % (res.path_display(), cmp_msg, errm)
                     check = OMap([("Resolved", OMap([("value", _pav_json(res)), ("comparison", [cmp, neg])]))])
+                    loc = (0, 0)   # Location::default() (eval_context.rs:2231-2234)
                 else:
                     ur = frm[1]
                     msg = "Check was not compliant as property [%s] is missing. Value traversed to [%s].%s" % (
                         ur.remaining_query, P.display(ur.traversed_to), errm)
                     check = OMap([("UnResolved", OMap([("value", _ur_json(ur)), ("comparison", [cmp, neg])]))])
+                    loc = _loc(ur.traversed_to)
                 clauses.append(("Clause", ("Unary", OMap([
-                    ("check", check), ("context", cur.context), ("messages", _messages(custom, msg))]))))
+                    ("check", check), ("context", cur.context), ("messages", _messages(custom, msg, loc))]))))
             elif ck == "Comparison":
                 m = cc[1]
                 cmp, neg = m["comparison"]
@@ -146,7 +162,7 @@ def report_all_failed(checks):
                     msg = ("Check was not compliant as property [%s] to compare from is missing. "
                            "Value traversed to [%s].%s" % (ur.remaining_query, P.display(ur.traversed_to), errm))
                     clauses.append(("Clause", ("Binary", OMap([
-                        ("context", cur.context), ("messages", _messages(custom, msg)),
+                        ("context", cur.context), ("messages", _messages(custom, msg, _loc(ur.traversed_to))),
                         ("check", OMap([("UnResolved", OMap([("value", _ur_json(ur)), ("comparison", [cmp, neg])]))]))]))))
                 else:
                     res = frm[1]
@@ -158,7 +174,7 @@ def report_all_failed(checks):
                         msg = "Check was not compliant as property value [%s] %s value [%s].%s" % (
                             P.display(res), a if neg else b, P.display(to[1]), errm)
                         clauses.append(("Clause", ("Binary", OMap([
-                            ("context", cur.context), ("messages", _messages(custom, msg)),
+                            ("context", cur.context), ("messages", _messages(custom, msg, _loc(to[1]))),
                             ("check", OMap([("Resolved", OMap([("from", _pav_json(res)), ("to", _pav_json(to[1])),
                                                                ("comparison", [cmp, neg])]))]))]))))
                     else:
@@ -166,7 +182,7 @@ def report_all_failed(checks):
                         msg = ("Check was not compliant as property [%s] to compare to is missing. "
                                "Value traversed to [%s].%s" % (ur.remaining_query, P.display(ur.traversed_to), errm))
                         clauses.append(("Clause", ("Binary", OMap([
-                            ("context", cur.context), ("messages", _messages(custom, msg)),
+                            ("context", cur.context), ("messages", _messages(custom, msg, _loc(ur.traversed_to))),
                             ("check", OMap([("UnResolved", OMap([("value", _ur_json(ur)), ("comparison", [cmp, neg])]))]))]))))
             elif ck == "InComparison":
                 m = cc[1]
@@ -176,7 +192,7 @@ def report_all_failed(checks):
                     frm.path_display(), slice_display(to, _qr_display))
                 clauses.append(("Clause", ("Binary", OMap([
                     ("context", cur.context),
-                    ("messages", _messages(m["custom_message"], err)),
+                    ("messages", _messages(m["custom_message"], err, _loc(frm))),
                     ("check", OMap([("InResolved", OMap([
                         ("from", _pav_json(frm)),
                         ("to", [_pav_json(t[1]) for t in to if t[0] == "R"]),
@@ -193,6 +209,8 @@ def _clause_json(c):
 
 
 def _fix(o):
+    if isinstance(o, Msgs):
+        return Msgs([(k, _fix(v)) for k, v in o.items], o.location)
     if isinstance(o, OMap):
         return OMap([(k, _fix(v)) for k, v in o.items])
     if isinstance(o, list):
@@ -305,8 +323,8 @@ def eval_file_report(rules_file, doc, data_name):
     return status, simplified_json_from_root(rec)
 
 
-def validate_structured(rules, data, parsed_docs=None):
-    """``cfn-guard validate --structured -o json -S none`` over in-memory inputs.
+def validate_structured(rules, data, parsed_docs=None, output="json"):
+    """``cfn-guard validate --structured -o {json|yaml|sarif|junit} -S none`` over in-memory inputs.
 
     rules: list of (rules_file_name, text); data: list of (data_name, text).
     Returns (stdout_text, exit_code, stderr_text).  Evaluation errors abort the run with
@@ -325,10 +343,12 @@ def validate_structured(rules, data, parsed_docs=None):
             parsed_rules.append((rf, name))
     try:
         docs = parsed_docs if parsed_docs is not None else [(n, load_document(t, n)) for n, t in data]
-        records = []
+        from . import formats
+        records, suites = [], []
         for dname, doc in docs:
             fr = {"name": dname, "status": E.SKIP, "not_compliant": [], "not_applicable": set(), "compliant": set()}
-            for rf, _ in parsed_rules:
+            cases = []
+            for rf, rname in parsed_rules:
                 st, rep = eval_file_report(rf, doc, dname)
                 if st == E.FAIL:
                     exit_code = FAILURE_STATUS
@@ -336,8 +356,21 @@ def validate_structured(rules, data, parsed_docs=None):
                 fr["not_compliant"].extend(rep["not_compliant"])
                 fr["compliant"] |= rep["compliant"]
                 fr["not_applicable"] |= rep["not_applicable"]
+                if output == "junit":
+                    cases.append(formats.junit_test_case(
+                        rname, st, {"not_compliant": [_clause_json(c) for c in rep["not_compliant"]]}))
             records.append(file_report_json(fr))
-        out = to_json_pretty(records)
+            suites.append((dname, cases))
+        if output == "json":
+            out = to_json_pretty(records)
+        elif output == "yaml":
+            out = formats.to_yaml(records)
+        elif output == "sarif":
+            out = formats.to_sarif(records)
+        elif output == "junit":
+            out = formats.to_junit(suites)
+        else:
+            raise ValueError(output)
     except GuardError as e:
         return "", -1, "".join(stderr) + "Error occurred %s" % e.display()
     return out, exit_code, "".join(stderr)
