@@ -443,8 +443,8 @@ double session_run(gg_session* s, bool fetch) {
   return ms;
 }
 
-// structured JSON over (docs x programs); returns false + err for an aborting error
-bool session_report(gg_session* s, std::string& out, int32_t& exit_code, ReportError& err) {
+// structured report over (docs x programs) in format `fmt` (OutFormat); false + err for an aborting error
+bool session_report(gg_session* s, std::string& out, int32_t& exit_code, ReportError& err, int32_t fmt = OUT_JSON) {
   exit_code = s->parse_errors.empty() ? 0 : 5;
   std::vector<const Program*> progs;
   for (auto& p : s->progs) progs.push_back(&p->prog);
@@ -459,8 +459,7 @@ bool session_report(gg_session* s, std::string& out, int32_t& exit_code, ReportE
   }
   out.clear();
   size_t nd = s->docs.ndocs();
-  if (nd == 0) { out = "[]"; return true; }
-  out += "[\n";
+  ReportWriter writer(fmt);
   std::vector<TileResult> trs(nf);
   for (size_t d = 0; d < nd; d++) {
     std::vector<const TileResult*> tp;
@@ -473,12 +472,9 @@ bool session_report(gg_session* s, std::string& out, int32_t& exit_code, ReportE
       if (tr.out.status == ST_FAIL) exit_code = exit_code == 5 ? 5 : 19;
       tp.push_back(&tr);
     }
-    out.append(2, ' ');
-    if (!report_document(s->docs, (uint32_t)d, progs, tp, 1, out, err)) { exit_code = -1; return false; }
-    if (d + 1 < nd) out += ",";
-    out += "\n";
+    if (!writer.add(s->docs, (uint32_t)d, progs, tp, err)) { exit_code = -1; return false; }
   }
-  out += "]";
+  out = writer.finish();
   // validate.rs: exit code 19 when any rules file FAILed (structured.rs:110-112), 5 on parse errors
   if (exit_code != 5) {
     bool anyfail = false;
@@ -637,7 +633,17 @@ char* cfn_guard_run_checks(validate_input_t data, validate_input_t rules, bool v
 
 char* cfn_guard_validate_batch(const validate_input_t* docs, size_t n_docs, const validate_input_t* rules, size_t n_rules,
                                int32_t* exit_code, extern_err_t* err) {
+  return cfn_guard_validate_batch_format(docs, n_docs, rules, n_rules, OUT_JSON, exit_code, err);
+}
+
+char* cfn_guard_validate_batch_format(const validate_input_t* docs, size_t n_docs, const validate_input_t* rules,
+                                      size_t n_rules, int32_t output_format, int32_t* exit_code, extern_err_t* err) {
   set_err(err, 0, "");
+  if (output_format < OUT_JSON || output_format > OUT_JUNIT) {
+    set_err(err, 18, "IllegalArguments: unknown output format");
+    if (exit_code) *exit_code = -1;
+    return nullptr;
+  }
   if (exit_code) *exit_code = 0;
   try {
     std::string why;
@@ -663,7 +669,7 @@ char* cfn_guard_validate_batch(const validate_input_t* docs, size_t n_docs, cons
     std::string out;
     int32_t code = 0;
     ReportError re;
-    if (!session_report(&s, out, code, re)) {
+    if (!session_report(&s, out, code, re, output_format)) {
       set_err(err, ffi_code(re.kind), error_display(re.kind, re.msg));
       if (exit_code) *exit_code = -1;
       return nullptr;
@@ -841,12 +847,17 @@ int32_t gg_session_eval(gg_session* s, int32_t iters, double* ms_out, extern_err
 }
 
 char* gg_session_report(gg_session* s, int32_t* exit_code, extern_err_t* err) {
+  return gg_session_report_format(s, OUT_JSON, exit_code, err);
+}
+
+char* gg_session_report_format(gg_session* s, int32_t output_format, int32_t* exit_code, extern_err_t* err) {
   set_err(err, 0, "");
   if (!s->evaluated) { set_err(err, -1, "session not evaluated"); return nullptr; }
+  if (output_format < OUT_JSON || output_format > OUT_JUNIT) { set_err(err, 18, "IllegalArguments: unknown output format"); return nullptr; }
   std::string out;
   int32_t code = 0;
   ReportError re;
-  if (!session_report(s, out, code, re)) {
+  if (!session_report(s, out, code, re, output_format)) {
     if (exit_code) *exit_code = -1;
     set_err(err, ffi_code(re.kind), error_display(re.kind, re.msg));
     return nullptr;

@@ -1,7 +1,11 @@
 // Device records -> structured JSON (see reporter.h).
 #include "reporter.h"
 
+#include <yaml.h>
+
 #include <algorithm>
+#include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <set>
 
@@ -17,6 +21,7 @@ struct J {
   bool b = false;
   std::vector<J> a;
   std::vector<std::pair<std::string, J>> o;
+  int64_t loc_line = -1, loc_col = -1;   // Messages.location (skip_serializing; read by the SARIF writer)
   static J null() { return J(); }
   static J str(const std::string& v) { J j; j.t = Str; j.s = v; return j; }
   static J raw(const std::string& v) { J j; j.t = Raw; j.s = v; return j; }
@@ -302,6 +307,14 @@ struct R {
   static J messages(const J& custom, const J& error) {
     J m = J::obj(); m.add("custom_message", custom); m.add("error_message", error); return m;
   }
+  static J messages(const J& custom, const J& error, std::pair<int64_t, int64_t> loc) {
+    J m = messages(custom, error); m.loc_line = loc.first; m.loc_col = loc.second; return m;
+  }
+  // self_path().1 of the value a QR carries (resolved value, or an unresolved one's traversed_to)
+  std::pair<int64_t, int64_t> q_loc(const QR& q) const {
+    if (q.node == NONE) return {0, 0};
+    return {(int64_t)line(q.node), (int64_t)col(q.node)};
+  }
   J comparison(uint32_t op, bool neg) const {
     static const char* names[] = {"Eq", "In", "Gt", "Lt", "Le", "Ge", "Exists", "Empty", "IsString", "IsList", "IsMap",
                                   "IsBool", "IsInt", "IsFloat", "IsNull"};
@@ -409,7 +422,9 @@ struct Walker {
           J un = J::obj();
           un.add("check", std::move(check));
           un.add("context", J::str(ctx));
-          un.add("messages", R::messages(J::str(r.custom(pc)), J::str(msg)));
+          // eval_context.rs:2231-2234: the unresolved value's location, Location::default() otherwise
+          un.add("messages", R::messages(J::str(r.custom(pc)), J::str(msg),
+                                         (rc.from.meta & 3u) == QR_UNRESOLVED ? r.q_loc(rc.from) : std::make_pair<int64_t, int64_t>(0, 0)));
           list.push(clause_wrap("Clause", clause_wrap("Unary", std::move(un))));
           break;
         }
@@ -467,7 +482,7 @@ struct Walker {
           if ((rc.from.meta & 3u) == QR_UNRESOLVED) {
             std::string msg = "Check was not compliant as property [" + r.remaining(rc.from) +
                               "] to compare from is missing. Value traversed to [" + r.unresolved_display(rc.from) + "]." + errm;
-            bin.add("messages", R::messages(J::str(cust), J::str(msg)));
+            bin.add("messages", R::messages(J::str(cust), J::str(msg), r.q_loc(rc.from)));
             J u = J::obj(); u.add("value", r.unresolved_json(rc.from)); u.add("comparison", r.comparison(op, neg));
             J check = J::obj(); check.add("UnResolved", std::move(u));
             bin.add("check", std::move(check));
@@ -476,14 +491,14 @@ struct Walker {
             if ((rc.to.meta & 3u) == QR_UNRESOLVED) {
               std::string msg = "Check was not compliant as property [" + r.remaining(rc.to) +
                                 "] to compare to is missing. Value traversed to [" + r.unresolved_display(rc.to) + "]." + errm;
-              bin.add("messages", R::messages(J::str(cust), J::str(msg)));
+              bin.add("messages", R::messages(J::str(cust), J::str(msg), r.q_loc(rc.to)));
               J u = J::obj(); u.add("value", r.unresolved_json(rc.to)); u.add("comparison", r.comparison(op, neg));
               J check = J::obj(); check.add("UnResolved", std::move(u));
               bin.add("check", std::move(check));
             } else {
               std::string msg = "Check was not compliant as property value [" + r.pav_display(rc.from) + "] " + op_msg(op, neg) +
                                 " value [" + r.pav_display(rc.to) + "]." + errm;
-              bin.add("messages", R::messages(J::str(cust), J::str(msg)));
+              bin.add("messages", R::messages(J::str(cust), J::str(msg), r.q_loc(rc.to)));
               J rr = J::obj(); rr.add("from", r.pav_json(rc.from)); rr.add("to", r.pav_json(rc.to)); rr.add("comparison", r.comparison(op, neg));
               J check = J::obj(); check.add("Resolved", std::move(rr));
               bin.add("check", std::move(check));
@@ -515,7 +530,7 @@ struct Walker {
           std::string err = "Check was not compliant as property [" + r.q_path_display(rc.from) + "] was not present in [" + fixed + "]";
           J bin = J::obj();
           bin.add("context", J::str(mk ? std::string() : r.prog.ctx[pcp->d]));
-          bin.add("messages", R::messages(mk ? J::null() : r.custom_opt(*pcp), J::str(err)));
+          bin.add("messages", R::messages(mk ? J::null() : r.custom_opt(*pcp), J::str(err), r.q_loc(rc.from)));
           J inr = J::obj();
           inr.add("from", r.pav_json(rc.from));
           J arr = J::arr();
@@ -615,8 +630,12 @@ void tile_error(const DocBatch& docs, uint32_t doc, const Program& prog, const T
   }
 }
 
-bool report_document(const DocBatch& docs, uint32_t doc, const std::vector<const Program*>& progs,
-                     const std::vector<const TileResult*>& tiles, int indent, std::string& out, ReportError& err) {
+namespace {
+
+// FileReport for one data file over every program (CommonStructuredReporter::report,
+// structured.rs:99-133); per_file[f] receives program f's not_compliant items when non-null
+bool build_file_report(const DocBatch& docs, uint32_t doc, const std::vector<const Program*>& progs,
+                       const std::vector<const TileResult*>& tiles, J& fr, std::vector<J>* per_file, ReportError& err) {
   try {
     uint32_t status = ST_SKIP;
     J not_compliant = J::arr();
@@ -628,6 +647,7 @@ bool report_document(const DocBatch& docs, uint32_t doc, const std::vector<const
       R r{docs, P, docs.serde, docs.base[doc]};
       Walker w{r, T.recs};
       J items = w.items(0xFFFFFFFFu);
+      if (per_file) per_file->push_back(items);
       for (auto& it : items.a) not_compliant.push(std::move(it));
       status = status_and(status, T.out.status);
       for (uint32_t k = 0; k < P.n_rules; k++) {
@@ -636,7 +656,7 @@ bool report_document(const DocBatch& docs, uint32_t doc, const std::vector<const
         else if (T.rule_status[k] == ST_SKIP) skip.insert(nm);
       }
     }
-    J fr = J::obj();
+    fr = J::obj();
     fr.add("name", J::str(docs.names[doc]));
     fr.add("metadata", J::obj());
     fr.add("status", J::str(status_str(status)));
@@ -645,12 +665,340 @@ bool report_document(const DocBatch& docs, uint32_t doc, const std::vector<const
     J co = J::arr(); for (auto& s : pass) co.push(J::str(s));
     fr.add("not_applicable", std::move(na));
     fr.add("compliant", std::move(co));
-    pretty(fr, indent, out);
     return true;
   } catch (Fatal& f) {
     err.set = true; err.kind = f.kind; err.msg = f.msg;
     return false;
   }
+}
+
+const J* field(const J& o, const char* k) {
+  for (auto& kv : o.o) if (kv.first == k) return &kv.second;
+  return nullptr;
+}
+
+// ClauseReport::get_message (eval_context.rs:1808-1826)
+void get_messages(const J& clause, std::vector<const J*>& out) {
+  const std::string& kind = clause.o[0].first;
+  const J& body = clause.o[0].second;
+  if (kind == "Rule" || kind == "Disjunctions") {
+    for (auto& ch : field(body, "checks")->a) get_messages(ch, out);
+  } else if (kind == "Block") {
+    out.push_back(field(body, "messages"));
+  } else {
+    out.push_back(field(body.o[0].second, "messages"));
+  }
+}
+
+// ---- YAML: serde_yaml 0.9 over unsafe-libyaml (libyaml 0.2.5), width unlimited, unicode on.
+// serde_yaml picks the scalar style of a string: literal when it holds a newline, single-quoted
+// when its plain form would resolve to null / bool / int / float (de.rs visit_untagged_scalar),
+// otherwise the emitter's choice.
+bool yaml_resolves_to_non_string(const std::string& v) {
+  if (v.empty() || v == "~" || v == "null" || v == "Null" || v == "NULL") return true;
+  if (v == "true" || v == "True" || v == "TRUE" || v == "false" || v == "False" || v == "FALSE") return true;
+  if (v.size() >= 2 && v[0] == '+' && (v[1] == '+' || v[1] == '-')) return false;
+  auto all = [](const std::string& s, size_t from, const char* set) {
+    if (from >= s.size()) return false;
+    for (size_t i = from; i < s.size(); i++) if (!strchr(set, s[i])) return false;
+    return true;
+  };
+  // radix-prefixed integers (parse_unsigned_int / parse_negative_int)
+  size_t o = (v[0] == '+' || v[0] == '-') ? 1 : 0;
+  if (v.size() > o + 2 && v[o] == '0') {
+    const char c = v[o + 1];
+    if (c == 'x' && all(v, o + 2, "0123456789abcdefABCDEF")) return true;
+    if (c == 'o' && all(v, o + 2, "01234567")) return true;
+    if (c == 'b' && all(v, o + 2, "01")) return true;
+  }
+  // .inf / .nan spellings (parse_f64)
+  const std::string u = v.substr(v[0] == '+' || v[0] == '-' ? 1 : 0);
+  if (u == ".inf" || u == ".Inf" || u == ".INF") return true;
+  if (v == ".nan" || v == ".NaN" || v == ".NAN") return true;
+  // Rust f64 grammar, finite values: [+-]?(digits(.digits?)?|.digits)([eE][+-]?digits)?
+  size_t i = o, n = v.size(), d1 = 0, d2 = 0;
+  while (i < n && isdigit((unsigned char)v[i])) { i++; d1++; }
+  if (i < n && v[i] == '.') { i++; while (i < n && isdigit((unsigned char)v[i])) { i++; d2++; } }
+  if (d1 + d2 == 0) return false;
+  if (i < n && (v[i] == 'e' || v[i] == 'E')) {
+    i++;
+    if (i < n && (v[i] == '+' || v[i] == '-')) i++;
+    size_t de = 0;
+    while (i < n && isdigit((unsigned char)v[i])) { i++; de++; }
+    if (!de) return false;
+  }
+  if (i != n) return false;
+  return std::isfinite(strtod(v.c_str(), nullptr));
+}
+
+int yaml_write_handler(void* data, unsigned char* buffer, size_t size) {
+  static_cast<std::string*>(data)->append((const char*)buffer, size);
+  return 1;
+}
+
+struct YamlOut {
+  yaml_emitter_t em;
+  std::string buf;
+  bool ok = true;
+  YamlOut() {
+    yaml_emitter_initialize(&em);
+    yaml_emitter_set_output(&em, yaml_write_handler, &buf);
+    yaml_emitter_set_width(&em, -1);
+    yaml_emitter_set_unicode(&em, 1);
+  }
+  ~YamlOut() { yaml_emitter_delete(&em); }
+  void emit(yaml_event_t& ev) { if (ok && !yaml_emitter_emit(&em, &ev)) ok = false; }
+  void scalar(const std::string& v, yaml_scalar_style_t style) {
+    yaml_event_t ev;
+    yaml_scalar_event_initialize(&ev, nullptr, nullptr, (yaml_char_t*)v.data(), (int)v.size(), 1, 1, style);
+    emit(ev);
+  }
+  void str(const std::string& v) {
+    yaml_scalar_style_t st = YAML_ANY_SCALAR_STYLE;
+    if (v.find('\n') != std::string::npos) st = YAML_LITERAL_SCALAR_STYLE;
+    else if (yaml_resolves_to_non_string(v)) st = YAML_SINGLE_QUOTED_SCALAR_STYLE;
+    scalar(v, st);
+  }
+  void value(const J& j) {
+    yaml_event_t ev;
+    switch (j.t) {
+      case J::Null: scalar("null", YAML_ANY_SCALAR_STYLE); return;
+      case J::Bool: scalar(j.b ? "true" : "false", YAML_ANY_SCALAR_STYLE); return;
+      case J::Raw: scalar(j.s, YAML_ANY_SCALAR_STYLE); return;
+      case J::Str: str(j.s); return;
+      case J::Arr:
+        yaml_sequence_start_event_initialize(&ev, nullptr, nullptr, 1, YAML_BLOCK_SEQUENCE_STYLE);
+        emit(ev);
+        for (auto& x : j.a) value(x);
+        yaml_sequence_end_event_initialize(&ev);
+        emit(ev);
+        return;
+      case J::Obj:
+        yaml_mapping_start_event_initialize(&ev, nullptr, nullptr, 1, YAML_BLOCK_MAPPING_STYLE);
+        emit(ev);
+        for (auto& kv : j.o) { str(kv.first); value(kv.second); }
+        yaml_mapping_end_event_initialize(&ev);
+        emit(ev);
+        return;
+    }
+  }
+};
+
+// ---- JUnit: quick_xml writer, indent 4 (reporters/mod.rs:66-420)
+std::string xml_escape(const std::string& s) {
+  std::string o;
+  for (char ch : s) {
+    switch (ch) {
+      case '&': o += "&amp;"; break;
+      case '<': o += "&lt;"; break;
+      case '>': o += "&gt;"; break;
+      case '\'': o += "&apos;"; break;
+      case '"': o += "&quot;"; break;
+      default: o.push_back(ch);
+    }
+  }
+  return o;
+}
+
+const char* kSarifDescription =
+    "AWS CloudFormation Guard is an open-source general-purpose policy-as-code evaluation tool. It provides developers "
+    "with a simple-to-use, yet powerful and expressive domain-specific language (DSL) to define policies and enables "
+    "developers to validate JSON- or YAML- formatted structured data with those policies.";
+
+std::string sanitize_path(const std::string& p) { return !p.empty() && p[0] == '/' ? p.substr(1) : p; }
+
+}  // namespace
+
+struct ReportWriter::Impl {
+  int32_t fmt;
+  size_t ndocs = 0;
+  std::string json;                       // OUT_JSON
+  YamlOut* yaml = nullptr;                // OUT_YAML
+  J artifacts = J::arr(), results = J::arr();   // OUT_SARIF
+  std::set<std::string> seen;
+  std::string suites;                     // OUT_JUNIT
+  size_t tests = 0, failures = 0;
+};
+
+ReportWriter::ReportWriter(int32_t fmt) : p_(new Impl) {
+  p_->fmt = fmt;
+  if (fmt == OUT_YAML) {
+    p_->yaml = new YamlOut();
+    yaml_event_t ev;
+    yaml_stream_start_event_initialize(&ev, YAML_UTF8_ENCODING);
+    p_->yaml->emit(ev);
+    yaml_document_start_event_initialize(&ev, nullptr, nullptr, nullptr, 1);
+    p_->yaml->emit(ev);
+    yaml_sequence_start_event_initialize(&ev, nullptr, nullptr, 1, YAML_BLOCK_SEQUENCE_STYLE);
+    p_->yaml->emit(ev);
+  }
+}
+
+ReportWriter::~ReportWriter() {
+  delete p_->yaml;
+  delete p_;
+}
+
+bool ReportWriter::add(const DocBatch& docs, uint32_t doc, const std::vector<const Program*>& progs,
+                       const std::vector<const TileResult*>& tiles, ReportError& err) {
+  J fr;
+  std::vector<J> per_file;
+  if (!build_file_report(docs, doc, progs, tiles, fr, p_->fmt == OUT_JUNIT ? &per_file : nullptr, err)) return false;
+  Impl& I = *p_;
+  I.ndocs++;
+  switch (I.fmt) {
+    case OUT_YAML:
+      I.yaml->value(fr);
+      break;
+    case OUT_SARIF: {
+      // SarifRun::from (sarif.rs:29-51): FAILed reports only
+      if (field(fr, "status")->s != "FAIL") break;
+      const std::string& name = docs.names[doc];
+      if (!name.empty() && I.seen.insert(name).second) {
+        J loc = J::obj(); loc.add("uri", J::str(sanitize_path(name)));
+        J a = J::obj(); a.add("location", std::move(loc));
+        I.artifacts.push(std::move(a));
+      }
+      for (auto& failure : field(fr, "not_compliant")->a) {
+        std::string rule_id;
+        if (failure.o[0].first == "Rule") {
+          std::string rn = field(failure.o[0].second, "name")->s;
+          rule_id = rn.substr(0, rn.find('.'));
+          for (auto& ch : rule_id) ch = (char)toupper((unsigned char)ch);
+        }
+        std::vector<const J*> msgs;
+        get_messages(failure, msgs);
+        for (const J* m : msgs) {
+          int64_t line = m->loc_line < 0 ? 0 : m->loc_line, col = m->loc_col < 0 ? 0 : m->loc_col;
+          const J* em = field(*m, "error_message");
+          const J* cm = field(*m, "custom_message");
+          std::string text = (em->t == J::Str ? em->s : std::string()) + " " + (cm->t == J::Str ? cm->s : std::string());
+          J res = J::obj();
+          res.add("ruleId", J::str(rule_id));
+          res.add("level", J::str("error"));
+          J mt = J::obj(); mt.add("text", J::str(text));
+          res.add("message", std::move(mt));
+          J art = J::obj(); art.add("uri", J::str(sanitize_path(name)));
+          J region = J::obj();
+          region.add("startLine", J::raw(std::to_string(std::max<int64_t>(line, 1))));
+          region.add("startColumn", J::raw(std::to_string(std::max<int64_t>(col, 1))));
+          J phys = J::obj(); phys.add("artifactLocation", std::move(art)); phys.add("region", std::move(region));
+          J l = J::obj(); l.add("physicalLocation", std::move(phys));
+          J locs = J::arr(); locs.push(std::move(l));
+          res.add("locations", std::move(locs));
+          I.results.push(std::move(res));
+        }
+      }
+      break;
+    }
+    case OUT_JUNIT: {
+      // JunitReporter::report (xml.rs:14-80): one test suite per data file, one test case per rules file
+      size_t nf = 0;
+      std::string cases;
+      for (size_t f = 0; f < progs.size(); f++) {
+        const std::string rname = xml_escape(progs[f]->file_name);
+        I.tests++;
+        const uint32_t st = tiles[f]->out.status;
+        if (st != ST_FAIL) {
+          cases += "        <testcase name=\"" + rname + "\" time=\"0\" status=\"" + (st == ST_PASS ? "pass" : "skip") + "\"/>\n";
+          continue;
+        }
+        nf++;
+        // get_test_case (reporters/mod.rs:108-168): the last rule failure names the failure
+        std::string fname;
+        bool named = false;
+        std::string texts;
+        size_t ntexts = 0;
+        for (auto& failure : per_file[f].a) {
+          std::vector<const J*> msgs;
+          get_messages(failure, msgs);
+          for (const J* m : msgs) {
+            if (failure.o[0].first == "Rule") {
+              std::string rn = field(failure.o[0].second, "name")->s;
+              size_t g = rn.find(".guard/");
+              fname = g == std::string::npos ? rn : rn.substr(g + 7);
+              named = true;
+            }
+            const J* cm = field(*m, "custom_message");
+            const J* em = field(*m, "error_message");
+            if (cm->t == J::Str) { texts += xml_escape(cm->s); ntexts++; }
+            if (em->t == J::Str) { texts += xml_escape(em->s); ntexts++; }
+          }
+        }
+        cases += "        <testcase name=\"" + rname + "\" time=\"0\">\n";
+        std::string attr = named ? " message=\"" + xml_escape(fname) + "\"" : std::string();
+        if (ntexts) cases += "            <failure" + attr + ">" + texts + "</failure>\n";
+        else cases += "            <failure" + attr + "/>\n";
+        cases += "        </testcase>\n";
+      }
+      I.failures += nf;
+      I.suites += "    <testsuite name=\"" + xml_escape(docs.names[doc]) + "\" errors=\"0\" failures=\"" + std::to_string(nf) +
+                  "\" time=\"0\">\n" + cases + "    </testsuite>\n";
+      break;
+    }
+    default:
+      I.json += I.ndocs == 1 ? "[\n" : ",\n";
+      I.json.append(2, ' ');
+      pretty(fr, 1, I.json);
+      break;
+  }
+  return true;
+}
+
+std::string ReportWriter::finish() {
+  Impl& I = *p_;
+  switch (I.fmt) {
+    case OUT_YAML: {
+      yaml_event_t ev;
+      yaml_sequence_end_event_initialize(&ev);
+      I.yaml->emit(ev);
+      yaml_document_end_event_initialize(&ev, 1);
+      I.yaml->emit(ev);
+      yaml_stream_end_event_initialize(&ev);
+      I.yaml->emit(ev);
+      yaml_emitter_flush(&I.yaml->em);
+      if (!I.yaml->ok) throw std::runtime_error("YAML emitter error");
+      return I.yaml->buf;
+    }
+    case OUT_SARIF: {
+      J drv = J::obj();
+      drv.add("name", J::str("cfn-guard"));
+      drv.add("semanticVersion", J::str("3.1.2"));
+      drv.add("fullName", J::str("cfn-guard 3.1.2"));
+      drv.add("organization", J::str("Amazon Web Services"));
+      drv.add("downloadUri", J::str("https://github.com/aws-cloudformation/cloudformation-guard"));
+      drv.add("informationUri", J::str("https://github.com/aws-cloudformation/cloudformation-guard"));
+      J sd = J::obj(); sd.add("text", J::str(kSarifDescription));
+      drv.add("shortDescription", std::move(sd));
+      J tool = J::obj(); tool.add("driver", std::move(drv));
+      J run = J::obj();
+      run.add("tool", std::move(tool));
+      run.add("artifacts", std::move(I.artifacts));
+      run.add("results", std::move(I.results));
+      J runs = J::arr(); runs.push(std::move(run));
+      J rep = J::obj();
+      rep.add("$schema", J::str("https://docs.oasis-open.org/sarif/sarif/v2.1.0/errata01/os/schemas/sarif-schema-2.1.0.json"));
+      rep.add("version", J::str("2.1.0"));
+      rep.add("runs", std::move(runs));
+      std::string out;
+      pretty(rep, 0, out);
+      return out;
+    }
+    case OUT_JUNIT:
+      return "<?xml version=\"1.0\" encoding=\"UTF-8\"?>\n<testsuites name=\"cfn-guard validate report\" tests=\"" +
+             std::to_string(I.tests) + "\" failures=\"" + std::to_string(I.failures) + "\" errors=\"0\" time=\"0\">\n" + I.suites +
+             "</testsuites>\n";
+    default:
+      return I.ndocs ? I.json + "\n]" : std::string("[]");
+  }
+}
+
+bool report_document(const DocBatch& docs, uint32_t doc, const std::vector<const Program*>& progs,
+                     const std::vector<const TileResult*>& tiles, int indent, std::string& out, ReportError& err) {
+  J fr;
+  if (!build_file_report(docs, doc, progs, tiles, fr, nullptr, err)) return false;
+  pretty(fr, indent, out);
+  return true;
 }
 
 }  // namespace gg

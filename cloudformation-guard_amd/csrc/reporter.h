@@ -30,4 +30,24 @@ void tile_error(const DocBatch& docs, uint32_t doc, const Program& prog, const T
 
 std::string error_display(const std::string& kind, const std::string& msg);
 
+// `validate --structured -o {json|yaml|sarif|junit}` writers over the same FileReports
+// (reporters/validate/structured.rs:99-133, sarif.rs, xml.rs + reporters/mod.rs).
+enum OutFormat : int32_t { OUT_JSON = 0, OUT_YAML = 1, OUT_SARIF = 2, OUT_JUNIT = 3 };
+
+class ReportWriter {
+ public:
+  explicit ReportWriter(int32_t fmt);
+  ~ReportWriter();
+  ReportWriter(const ReportWriter&) = delete;
+  ReportWriter& operator=(const ReportWriter&) = delete;
+  // one data file; tiles[f] is its tile of program f.  false + err on an aborting error.
+  bool add(const DocBatch& docs, uint32_t doc, const std::vector<const Program*>& progs,
+           const std::vector<const TileResult*>& tiles, ReportError& err);
+  std::string finish();
+
+ private:
+  struct Impl;
+  Impl* p_;
+};
+
 }  // namespace gg

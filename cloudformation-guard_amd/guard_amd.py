@@ -51,6 +51,13 @@ def lib():
     L.cfn_guard_validate_batch.argtypes = [ctypes.POINTER(ValidateInput), ctypes.c_size_t, ctypes.POINTER(ValidateInput),
                                            ctypes.c_size_t, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ExternError)]
     L.cfn_guard_validate_batch.restype = ctypes.c_void_p
+    L.cfn_guard_validate_batch_format.argtypes = [ctypes.POINTER(ValidateInput), ctypes.c_size_t,
+                                                  ctypes.POINTER(ValidateInput), ctypes.c_size_t, ctypes.c_int32,
+                                                  ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ExternError)]
+    L.cfn_guard_validate_batch_format.restype = ctypes.c_void_p
+    L.gg_session_report_format.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32),
+                                           ctypes.POINTER(ExternError)]
+    L.gg_session_report_format.restype = ctypes.c_void_p
     L.gg_session_new.restype = ctypes.c_void_p
     L.gg_session_free.argtypes = [ctypes.c_void_p]
     L.gg_session_add_rules.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(ExternError)]
@@ -119,14 +126,20 @@ def run_checks(data, data_name, rules, rules_name, verbose=False):
     return _take_string(p)
 
 
-def validate_structured(rules, data):
-    """rules: [(name, text)], data: [(name, text)] -> (stdout_json, exit_code).
+# `validate --structured -o <format>` (include/cfn_guard_mi355x.h CFN_GUARD_OUTPUT_*)
+OUTPUT_FORMATS = {"json": 0, "yaml": 1, "sarif": 2, "junit": 3}
+
+
+def validate_structured(rules, data, output="json"):
+    """rules: [(name, text)], data: [(name, text)] -> (stdout text, exit_code) for
+    `cfn-guard validate --structured -o <output> -S none`.
     Raises GuardError for an evaluation error (the CLI prints it to stderr, exit -1)."""
     R = (ValidateInput * max(1, len(rules)))(*[ValidateInput(_b(t), _b(n)) for n, t in rules])
     D = (ValidateInput * max(1, len(data)))(*[ValidateInput(_b(t), _b(n)) for n, t in data])
     code = ctypes.c_int32(0)
     err = ExternError()
-    p = lib().cfn_guard_validate_batch(D, len(data), R, len(rules), ctypes.byref(code), ctypes.byref(err))
+    p = lib().cfn_guard_validate_batch_format(D, len(data), R, len(rules), OUTPUT_FORMATS[output], ctypes.byref(code),
+                                              ctypes.byref(err))
     if err.code != 0:
         _raise(err)
     return _take_string(p), code.value
@@ -180,10 +193,10 @@ class Session:
             _raise(err)
         return list(ms)
 
-    def report(self):
+    def report(self, output="json"):
         code = ctypes.c_int32(0)
         err = ExternError()
-        p = lib().gg_session_report(self.s, ctypes.byref(code), ctypes.byref(err))
+        p = lib().gg_session_report_format(self.s, OUTPUT_FORMATS[output], ctypes.byref(code), ctypes.byref(err))
         if err.code != 0:
             _raise(err)
         return _take_string(p), code.value

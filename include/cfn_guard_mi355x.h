@@ -42,6 +42,16 @@ void cfn_guard_free_string(char *s);
 char *cfn_guard_validate_batch(const validate_input_t *docs, size_t n_docs, const validate_input_t *rules,
                                size_t n_rules, int32_t *exit_code, extern_err_t *err);
 
+/* Output formats of `validate --structured -o <format>` (commands/validate.rs:143-200,
+ * reporters/validate/structured.rs:124-133, sarif.rs, xml.rs). */
+#define CFN_GUARD_OUTPUT_JSON 0
+#define CFN_GUARD_OUTPUT_YAML 1
+#define CFN_GUARD_OUTPUT_SARIF 2
+#define CFN_GUARD_OUTPUT_JUNIT 3
+/* cfn_guard_validate_batch with `-o json|yaml|sarif|junit` (byte-identical to the CLI's output). */
+char *cfn_guard_validate_batch_format(const validate_input_t *docs, size_t n_docs, const validate_input_t *rules,
+                                      size_t n_rules, int32_t output_format, int32_t *exit_code, extern_err_t *err);
+
 /* ---- session API (documents resident in HBM across evaluations; used by bench.py/tests) ---- */
 typedef struct gg_session gg_session;
 gg_session *gg_session_new(void);
@@ -53,6 +63,7 @@ int32_t gg_session_add_docs(gg_session *s, const char *const *texts, const size_
 int32_t gg_session_upload(gg_session *s, extern_err_t *err);
 int32_t gg_session_eval(gg_session *s, int32_t iters, double *ms_out, extern_err_t *err);
 char *gg_session_report(gg_session *s, int32_t *exit_code, extern_err_t *err);
+char *gg_session_report_format(gg_session *s, int32_t output_format, int32_t *exit_code, extern_err_t *err);
 int64_t gg_session_stat(gg_session *s, int32_t what);
 int32_t gg_session_tile_status(gg_session *s, uint8_t *out, size_t n);
 double gg_session_last_kernel_ms(gg_session *s);

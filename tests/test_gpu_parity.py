@@ -148,3 +148,36 @@ def test_lane_overflow_retried_in_wave_mode():
     wave, wcode, _ = _session_report(docs, rules, 1)
     assert retried > 0
     assert (lane, lcode) == (wave, wcode)
+
+
+@pytest.mark.gpu
+def test_structured_yaml_sarif_junit_goldens():
+    """-o yaml / sarif / junit (guard/tests/validate.rs:597-631) through the C ABI"""
+    import re
+    dn = "s3-public-read-prohibited-template-non-compliant.yaml"
+    data = [(dn, open(os.path.join(G, "validate", "data-dir", dn)).read())]
+    for fmt in ("json", "yaml", "sarif", "junit"):
+        out, code = guard_amd.validate_structured(_rules_dir(), data, output=fmt)
+        assert code == 19
+        if fmt == "sarif":
+            out = re.sub(r'("uri": ".*")', '"uri": "some/path"', out)   # tests/utils.rs:82-90
+        assert out == open(os.path.join(G, "validate", "structured." + fmt)).read(), fmt
+
+
+@pytest.mark.gpu
+def test_output_formats_vs_oracle():
+    """every output format over the synthetic corpus and the cfg-4 / cfg-5 packs, against the oracle"""
+    def pack(d):
+        p = os.path.join(G, d)
+        return [(f, open(os.path.join(p, f)).read()) for f in sorted(os.listdir(p)) if f.endswith(".guard")]
+    cases = [
+        ([("doc%d.json" % i, d) for i, d in enumerate(synth.cfn_corpus(8, start=40, n_resources=15))], rule_pack()),
+        ([("/plans/p%d.json" % i, d) for i, d in enumerate(synth.tf_corpus(4, start=7, n_resources=20))], pack("tf_rulepack")),
+        ([("snap%d.json" % i, d) for i, d in enumerate(synth.config_corpus(4, start=9))], pack("net_rulepack")),
+        ([("doc%d.json" % i, d) for i, d in enumerate(synth.cfn_corpus(4, start=300, n_resources=20))], pack("edge_rulepack")),
+    ]
+    for data, rules in cases:
+        for fmt in ("yaml", "sarif", "junit"):
+            exp, ecode, _ = oracle_validate(rules, data, output=fmt)
+            out, code = guard_amd.validate_structured(rules, data, output=fmt)
+            assert (out, code) == (exp, ecode), (fmt, rules[0][0])
