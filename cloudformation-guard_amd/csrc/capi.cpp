@@ -297,6 +297,8 @@ void session_upload(gg_session* s) {
   size_t lane_waves_per_cu = 8;
   if (const char* e = getenv("GG_LANE_WAVES_PER_CU")) lane_waves_per_cu = std::max(1, atoi(e));
   s->lane_slots = s->mode == 1 ? 0 : (uint32_t)std::min<size_t>(std::max<size_t>(nbatches, 1), (size_t)g_dev.ncu * lane_waves_per_cu);
+  // every one of the 8 per-XCD queues needs waves (block b serves queue b % 8)
+  if (s->lane_slots) s->lane_slots = (std::max<uint32_t>(s->lane_slots, 8u) + 7u) & ~7u;
   s->d_lane_heaps.alloc((size_t)s->lane_slots * 64 * s->lane_heap_bytes);
   s->d_retry.alloc(std::max<size_t>(ntiles, 1));
   s->d_retry2.alloc(std::max<size_t>(ntiles, 1));
@@ -305,7 +307,7 @@ void session_upload(gg_session* s) {
   s->d_rule_status.alloc(std::max<size_t>(ntiles * s->max_top, 1));
   s->rec_cap = std::min<size_t>(std::max<size_t>(ntiles * 48, 4096), (size_t)96 * 1024 * 1024);
   s->d_recs.alloc(s->rec_cap);
-  s->d_counters.alloc(16);
+  s->d_counters.alloc(32);   // [0..6] cursors / counts, [16..23] per-XCD lane-mode queues
   s->d_stats.alloc(16);
   HIPCHK(hipMemsetAsync(s->d_stats.p, 0, 16 * sizeof(unsigned long long), st));
   s->ncounts = s->progs.size() * (s->max_top + 1) * 4;
@@ -322,7 +324,7 @@ hipStream_t session_stream(gg_session* s) { return s->stream ? s->stream : g_dev
 void session_launch(gg_session* s) {
   hipStream_t st = session_stream(s);
   uint32_t ntiles = (uint32_t)(s->docs.ndocs() * s->progs.size());
-  HIPCHK(hipMemsetAsync(s->d_counters.p, 0, 16 * sizeof(uint32_t), st));
+  HIPCHK(hipMemsetAsync(s->d_counters.p, 0, 32 * sizeof(uint32_t), st));
   unsigned long long* counts = s->ext_counts ? s->ext_counts : s->d_counts.p;
   HIPCHK(hipMemsetAsync(counts, 0, s->ncounts * sizeof(unsigned long long), st));
   LaunchArgs A{};
@@ -335,6 +337,7 @@ void session_launch(gg_session* s) {
   A.recs = s->d_recs.p; A.rec_cap = (uint32_t)s->rec_cap;
   A.rec_cursor = s->d_counters.p; A.tile_cursor = s->d_counters.p + 1;   // [1] lane batches, [2] wave tiles
   A.retry_count = s->d_counters.p + 3;
+  A.xcd_cursor = s->d_counters.p + 16;
   A.lane_heaps = s->d_lane_heaps.p; A.lane_heap_bytes = s->lane_heap_bytes;
   A.retry_list = s->mode == 1 ? nullptr : s->d_retry.p;
   A.wave_frames_bytes = gg_session::kWaveFrames; A.wave_recs_bytes = gg_session::kWaveRecs;

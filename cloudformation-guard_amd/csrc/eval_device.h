@@ -78,6 +78,7 @@ struct LaunchArgs {
   uint32_t wave_recs_bytes;    // wave mode: record staging region after it
   uint32_t* retry2_list;       // tiles the wave pass hands to the large-heap pass (null: none)
   uint32_t* retry2_count;
+  uint32_t* xcd_cursor;       // lane mode: one batch queue per XCD ([8])
   unsigned long long* stats;   // diagnostic counters [8] (stats build variant), else unused
 };
 

@@ -102,8 +102,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
   const uint32_t lane = __lane_id();
   // 64 lanes share one interleaved region (see haddr in eval_core.inc)
   uint8_t* heap = A.lane_heaps + (size_t)blockIdx.x * 64 * A.lane_heap_bytes;
+  // XCD-aware work queues: workgroups are dispatched round-robin over the 8 XCDs, so block b runs
+  // on XCD b % 8.  Each XCD owns a contiguous eighth of the 64-document chunks and hands out its
+  // batches chunk-major, file-minor: the rules files of one chunk run back to back on the same
+  // XCD, so the chunk's arena lines fetched by the first file are L2 hits for the others.
   const uint32_t nchunks = (A.docs.ndocs + 63u) / 64u;
-  const uint32_t nbatches = nchunks * A.nfiles;
+  const uint32_t xcd = blockIdx.x & 7u;
+  const uint32_t c0 = (uint32_t)(((uint64_t)nchunks * xcd) / 8u), c1 = (uint32_t)(((uint64_t)nchunks * (xcd + 1u)) / 8u);
+  const uint32_t nbatches = (c1 - c0) * A.nfiles;
   // interpreter state lives in LDS (one Ctx per lane), not in the per-lane stack
   __shared__ Ctx s_ctx[64];
   __shared__ DevProg s_prog;
@@ -113,10 +119,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
   const DevProg* P = nullptr;
   for (;;) {
     uint32_t b = 0;
-    if (lane == 0) b = atomicAdd(A.tile_cursor, 1u);
+    if (lane == 0) b = atomicAdd(A.xcd_cursor + xcd, 1u);
     b = __shfl(b, 0);
     if (b >= nbatches) break;
-    const uint32_t file = b % A.nfiles, chunk = b / A.nfiles;
+    const uint32_t file = b % A.nfiles, chunk = c0 + b / A.nfiles;
     const uint32_t doc = chunk * 64u + lane;
     const bool active = doc < A.docs.ndocs;
     if (file != staged) { P = stage_program(&A.progs[file], &s_prog, s_blob); staged = file; }
