@@ -23,18 +23,25 @@ from .report import OMap, Msgs, to_json_pretty
 # --------------------------------------------------------------------------------------- YAML
 _NULL = {"~", "null", "Null", "NULL"}
 _BOOL = {"true", "True", "TRUE", "false", "False", "FALSE"}
-_INT = re.compile(r"^[-+]?(0|[1-9][0-9]*)$|^0o[0-7]+$|^0x[0-9a-fA-F]+$")
-_FLOAT = re.compile(r"^[-+]?(\.[0-9]+|[0-9]+(\.[0-9]*)?)([eE][-+]?[0-9]+)?$|^[-+]?\.(inf|Inf|INF)$|^\.(nan|NaN|NAN)$")
+# serde_yaml de.rs parse_unsigned_int / parse_negative_int (radix prefixes; decimal runs of digits
+# are covered by the float grammar, which Rust's f64 parser accepts for any digit string)
+_INT = re.compile(r"^\+?0x[0-9a-fA-F]+$|^\+?0o[0-7]+$|^\+?0b[01]+$|^-0x[0-9a-fA-F]+$|^-0o[0-7]+$|^-0b[01]+$")
+# parse_f64: optional sign, Rust f64 grammar, finite values only; .inf / .nan spellings
+_FLOAT = re.compile(r"^[-+]?(\.[0-9]+|[0-9]+(\.[0-9]*)?)([eE][-+]?[0-9]+)?$")
+_SPECIAL = re.compile(r"^[-+]?\.(inf|Inf|INF)$|^\.(nan|NaN|NAN)$")
 
 
 def _resolves_to_non_string(v):
-    # serde_yaml de::visit_untagged_scalar over a plain scalar: empty / null, bool, int, float
+    """serde_yaml de::visit_untagged_scalar over the plain form: empty / null, bool, int, float"""
     if v == "" or v in _NULL or v in _BOOL:
         return True
-    if _INT.match(v) or _FLOAT.match(v):
+    if v.startswith("+") and v[1:2] in ("+", "-"):
+        return False
+    if _INT.match(v) or _SPECIAL.match(v):
         return True
-    # digits_but_not_number: a run of digits with a leading zero is still quoted
-    return len(v) > 1 and v.isdigit()
+    if _FLOAT.match(v):
+        return float(v) not in (float("inf"), float("-inf"))
+    return False
 
 
 def _str_style(v):
