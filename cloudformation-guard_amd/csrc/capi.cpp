@@ -686,6 +686,173 @@ char* cfn_guard_validate_batch_format(const validate_input_t* docs, size_t n_doc
   }
 }
 
+// ---------------------------------------------------------------- cfn-guard test ---
+namespace {
+
+const DNode* map_entry(const DocBatch& D, uint64_t base, const DNode& m, const char* key) {
+  if (m.kind != K_MAP) return nullptr;
+  const size_t kl = strlen(key);
+  for (uint32_t j = 0; j < m.count; j++) {
+    const DNode& e = D.nodes[base + m.a + j];
+    if (e.key_len == kl && memcmp(D.bytes.data() + e.key_off, key, kl) == 0) return &e;
+  }
+  return nullptr;
+}
+
+std::string node_str(const DocBatch& D, const DNode& n) { return std::string(D.bytes.data() + n.a, n.count); }
+
+struct SpecCase { bool has_name; std::string name; uint32_t input; std::vector<std::pair<std::string, std::string>> expected; };
+
+// Vec<TestSpec> (commands/test.rs:480-484) out of a loaded spec document; false + message on a shape error
+bool read_spec(const DocBatch& D, size_t doc, std::vector<SpecCase>& out, std::string& why) {
+  const uint64_t base = D.base[doc];
+  const DNode& root = D.nodes[base + D.roots[doc]];
+  if (root.kind != K_LIST) { why = "invalid type: expected a sequence"; return false; }
+  for (uint32_t i = 0; i < root.count; i++) {
+    const uint32_t ci = root.a + i;
+    const DNode& c = D.nodes[base + ci];
+    if (c.kind != K_MAP) { why = "invalid type: expected struct TestSpec"; return false; }
+    const DNode* name = map_entry(D, base, c, "name");
+    const DNode* input = map_entry(D, base, c, "input");
+    const DNode* exp = map_entry(D, base, c, "expectations");
+    if (!input) { why = "missing field `input`"; return false; }
+    if (!exp) { why = "missing field `expectations`"; return false; }
+    const DNode* rules = map_entry(D, base, *exp, "rules");
+    if (!rules) { why = "missing field `rules`"; return false; }
+    SpecCase sc;
+    sc.has_name = name && name->kind == K_STRING;
+    if (sc.has_name) sc.name = node_str(D, *name);
+    sc.input = (uint32_t)(input - &D.nodes[base]);
+    if (rules->kind == K_MAP) {
+      for (uint32_t j = 0; j < rules->count; j++) {
+        const DNode& e = D.nodes[base + rules->a + j];
+        if (e.kind != K_STRING) { why = "invalid type: expected a string"; return false; }
+        sc.expected.push_back({std::string(D.bytes.data() + e.key_off, e.key_len), node_str(D, e)});
+      }
+    }
+    out.push_back(std::move(sc));
+  }
+  return true;
+}
+
+int32_t status_of(const std::string& s) { return s == "PASS" ? (int32_t)ST_PASS : s == "FAIL" ? (int32_t)ST_FAIL : s == "SKIP" ? (int32_t)ST_SKIP : -1; }
+
+}  // namespace
+
+/* `cfn-guard test -r <rules> -t <spec files>`: every spec's inputs evaluated on the MI355X in one
+ * batch, each test case a document whose root is its `input` subtree. */
+char* cfn_guard_test(validate_input_t rules, const validate_input_t* specs, size_t n_specs, int32_t output_format,
+                     int32_t* exit_code, extern_err_t* err) {
+  set_err(err, 0, "");
+  if (exit_code) *exit_code = 0;
+  if (output_format != OUT_TEXT && output_format != OUT_JSON && output_format != OUT_YAML && output_format != OUT_JUNIT) {
+    set_err(err, 18, "IllegalArguments: test reports are text, json, yaml or junit");
+    if (exit_code) *exit_code = -1;
+    return nullptr;
+  }
+  try {
+    std::string why;
+    if (!ensure_device(why)) { set_err(err, -1, why); if (exit_code) *exit_code = -1; return nullptr; }
+    gg_session s;
+    const std::string rname = rules.file_name ? rules.file_name : "";
+    std::string perr;
+    if (!add_rules(&s, rules.content ? rules.content : "", rname, perr)) {
+      set_err(err, 5, error_display("ParseError", perr));
+      if (exit_code) *exit_code = -1;
+      return nullptr;
+    }
+    std::vector<TestSpecFile> files(n_specs);
+    std::vector<std::vector<SpecCase>> cases(n_specs);
+    std::vector<std::pair<size_t, size_t>> tile_of;   // (spec, case) of each evaluated document
+    DocBatch& D = s.docs;
+    for (size_t k = 0; k < n_specs; k++) {
+      const char* t = specs[k].content ? specs[k].content : "";
+      const std::string path = specs[k].file_name ? specs[k].file_name : "";
+      LoadError le;
+      std::string shape;
+      const size_t at = D.ndocs();
+      bool ok = load_document(D, t, strlen(t), path, LOAD_SERDE, le);
+      if (ok && !read_spec(D, at, cases[k], shape)) { ok = false; le.msg = shape; }
+      if (!ok) {
+        files[k].error = error_display("ParseError", "Unable to process data in file " + path + ", Error " + le.msg + ",");
+        if (D.ndocs() > at) { D.roots.pop_back(); D.base.pop_back(); D.names.pop_back(); }
+        continue;
+      }
+      // the spec document itself is not evaluated: one document per test case, rooted at its input
+      const uint64_t base = D.base[at];
+      D.roots.pop_back(); D.base.pop_back(); D.names.pop_back();
+      for (size_t c = 0; c < cases[k].size(); c++) {
+        D.roots.push_back(cases[k][c].input);
+        D.base.push_back(base);
+        D.names.push_back(path);
+        tile_of.push_back({k, c});
+      }
+    }
+    if (!s.progs.empty() && D.ndocs()) {
+      session_upload(&s);
+      session_run(&s, true);
+    }
+    const Program* P = s.progs.empty() ? nullptr : &s.progs[0]->prog;
+    for (size_t d = 0; d < tile_of.size(); d++) {
+      const size_t k = tile_of[d].first, c = tile_of[d].second;
+      const SpecCase& sc = cases[k][c];
+      TestCaseResult tc;
+      tc.has_name = sc.has_name;
+      tc.name = sc.name;
+      if (P) {
+        const TileOut& to = s.tiles[d];
+        if (to.err) {   // an evaluation error aborts the command (eval_rules_file(..)?)
+          ReportError re;
+          tile_error(D, (uint32_t)d, *P, to, re);
+          set_err(err, ffi_code(re.kind), error_display(re.kind, re.msg));
+          if (exit_code) *exit_code = -1;
+          return nullptr;
+        }
+        // get_by_rules (reporters/test/mod.rs:7-18): top-level rule records grouped by name
+        std::vector<std::string> order;
+        std::vector<std::vector<uint32_t>> got;
+        for (uint32_t r = 0; r < P->n_rules; r++) {
+          const std::string& nm = P->rule_names[P->rule_names.size() - P->n_rules + r];
+          size_t g = std::find(order.begin(), order.end(), nm) - order.begin();
+          if (g == order.size()) { order.push_back(nm); got.emplace_back(); }
+          got[g].push_back(s.rule_status[d * s.max_top + r]);
+        }
+        for (size_t g = 0; g < order.size(); g++) {
+          TestRuleResult rr;
+          rr.rule = order[g];
+          auto it = std::find_if(sc.expected.begin(), sc.expected.end(), [&](const std::pair<std::string, std::string>& e) { return e.first == order[g]; });
+          if (it != sc.expected.end()) {
+            rr.expected = status_of(it->second);
+            if (rr.expected < 0) {
+              set_err(err, 5, error_display("ParseError", "Unable to parse status " + it->second));
+              if (exit_code) *exit_code = -1;
+              return nullptr;
+            }
+            // get_status_result (reporters/test/mod.rs:20-54)
+            uint32_t all_skipped = 0;
+            for (uint32_t st : got[g]) {
+              if (rr.expected == (int32_t)ST_SKIP) { if (st == ST_SKIP) all_skipped++; }
+              else if ((int32_t)st == rr.expected) { rr.matched = rr.expected; break; }
+              rr.evaluated.push_back(st);
+            }
+            if (rr.matched < 0 && rr.expected == (int32_t)ST_SKIP && all_skipped == got[g].size()) rr.matched = ST_SKIP;
+          }
+          tc.rules.push_back(std::move(rr));
+        }
+      }
+      files[k].cases.push_back(std::move(tc));
+    }
+    int32_t code = 0;
+    std::string out = test_report(output_format, rname, files, code);
+    if (exit_code) *exit_code = code;
+    return dup_str(out);
+  } catch (std::exception& e) {
+    set_err(err, -1, e.what());
+    if (exit_code) *exit_code = -1;
+    return nullptr;
+  }
+}
+
 // ------------------------------------------------------------- session API ---
 gg_session* gg_session_new(void) { return new gg_session(); }
 void gg_session_free(gg_session* s) {

@@ -747,6 +747,16 @@ struct YamlOut {
     yaml_emitter_set_unicode(&em, 1);
   }
   ~YamlOut() { yaml_emitter_delete(&em); }
+  // one whole YAML stream holding `j` (serde_yaml::to_writer of one value)
+  void document(const J& j) {
+    yaml_event_t ev;
+    yaml_stream_start_event_initialize(&ev, YAML_UTF8_ENCODING); emit(ev);
+    yaml_document_start_event_initialize(&ev, nullptr, nullptr, nullptr, 1); emit(ev);
+    value(j);
+    yaml_document_end_event_initialize(&ev, 1); emit(ev);
+    yaml_stream_end_event_initialize(&ev); emit(ev);
+    yaml_emitter_flush(&em);
+  }
   void emit(yaml_event_t& ev) { if (ok && !yaml_emitter_emit(&em, &ev)) ok = false; }
   void scalar(const std::string& v, yaml_scalar_style_t style) {
     yaml_event_t ev;
@@ -991,6 +1001,103 @@ std::string ReportWriter::finish() {
     default:
       return I.ndocs ? I.json + "\n]" : std::string("[]");
   }
+}
+
+std::string test_report(int32_t fmt, const std::string& rules_name, const std::vector<TestSpecFile>& files,
+                        int32_t& exit_code) {
+  static const char* kStatus[] = {"PASS", "FAIL", "SKIP"};
+  exit_code = 0;   // SUCCESS_STATUS_CODE; 7 TEST_FAILURE_STATUS_CODE; 1 TEST_ERROR_STATUS_CODE
+  auto statuses = [&](const std::vector<uint32_t>& v) {
+    std::string o;
+    for (size_t i = 0; i < v.size(); i++) o += (i ? ", " : "") + std::string(kStatus[v[i]]);
+    return o;
+  };
+  if (fmt == OUT_TEXT) {
+    // GenericReporter::report (reporters/test/generic.rs:23-63, 105-125)
+    std::string out;
+    size_t counter = 1;
+    for (auto& f : files) {
+      if (!f.error.empty()) { out += "Error processing " + f.error + "\n"; exit_code = 1; continue; }
+      for (auto& tc : f.cases) {
+        out += "Test Case #" + std::to_string(counter++) + "\n";
+        if (tc.has_name) out += "Name: " + tc.name + "\n";
+        std::vector<std::string> pass, failv;
+        for (auto& r : tc.rules) {
+          if (r.expected < 0) { out += "  No Test expectation was set for Rule " + r.rule + "\n"; continue; }
+          std::string line = r.matched >= 0 ? r.rule + ": Expected = " + kStatus[r.matched]
+                                            : r.rule + ": Expected = " + kStatus[r.expected] + ", Evaluated = [" + statuses(r.evaluated) + "]";
+          auto& dst = r.matched >= 0 ? pass : failv;
+          if (std::find(dst.begin(), dst.end(), line) == dst.end()) dst.push_back(line);   // IndexSet
+        }
+        if (!failv.empty()) { exit_code = 7; out += "  FAIL Rules:\n"; for (auto& l : failv) out += "    " + l + "\n"; }
+        if (!pass.empty()) { out += "  PASS Rules:\n"; for (auto& l : pass) out += "    " + l + "\n"; }
+        out += "\n";
+      }
+    }
+    return out;
+  }
+  // StructuredTestReporter (reporters/test/structured.rs) + handle_structured_single_report (test.rs:326-380)
+  for (auto& f : files) {
+    if (f.error.empty()) continue;
+    exit_code = 1;
+    if (fmt == OUT_JUNIT) {
+      const std::string rn = xml_escape(rules_name);
+      return "<?xml version=\"1.0\" encoding=\"UTF-8\"?>\n<testsuites name=\"cfn-guard test report\" tests=\"1\" failures=\"0\" "
+             "errors=\"1\" time=\"0\">\n    <testsuite name=\"" + rn + "\" errors=\"1\" failures=\"0\" time=\"0\">\n"
+             "        <testcase name=\"" + rn + "\" time=\"0\" status=\"error\">\n            <error>" + xml_escape(f.error) +
+             "</error>\n        </testcase>\n    </testsuite>\n</testsuites>\n";
+    }
+    J e = J::obj(); e.add("rule_file", J::str(rules_name)); e.add("error", J::str(f.error));
+    if (fmt == OUT_YAML) { YamlOut y; y.document(e); return y.buf; }
+    std::string out; pretty(e, 0, out); return out;
+  }
+  J cases = J::arr();
+  std::string junit;
+  size_t njunit = 0, failures = 0;
+  for (auto& f : files) {
+    for (auto& tc : f.cases) {
+      J passed = J::arr(), failed = J::arr(), skipped = J::arr();
+      std::string jp, jf;
+      const std::string tid = xml_escape(tc.has_name ? tc.name : std::string());
+      for (auto& r : tc.rules) {
+        if (r.expected < 0) { J s = J::obj(); s.add("name", J::str(r.rule)); skipped.push(std::move(s)); continue; }
+        if (r.matched >= 0) {
+          J p = J::obj(); p.add("name", J::str(r.rule)); p.add("evaluated", J::str(kStatus[r.matched]));
+          passed.push(std::move(p));
+          jp += "        <testcase id=\"" + tid + "\" name=\"" + xml_escape(r.rule) + "\" time=\"0\" status=\"pass\"/>\n";
+        } else {
+          J ev = J::arr();
+          for (uint32_t st : r.evaluated) ev.push(J::str(kStatus[st]));
+          J p = J::obj(); p.add("name", J::str(r.rule)); p.add("expected", J::str(kStatus[r.expected])); p.add("evaluated", std::move(ev));
+          failed.push(std::move(p));
+          jf += "        <testcase id=\"" + tid + "\" name=\"" + xml_escape(r.rule) + "\" time=\"0\">\n            <failure>" +
+                xml_escape(std::string("Expected = ") + kStatus[r.expected] + ", Evaluated = [" + statuses(r.evaluated) + "]") +
+                "</failure>\n        </testcase>\n";
+          failures++;
+        }
+        njunit++;
+      }
+      if (!failed.a.empty()) exit_code = 7;
+      junit += jp + jf;   // build_junit_test_cases: passed rules, then failed rules
+      J c = J::obj();
+      c.add("name", J::str(tc.has_name ? tc.name : std::string()));
+      c.add("passed_rules", std::move(passed));
+      c.add("failed_rules", std::move(failed));
+      c.add("skipped_rules", std::move(skipped));
+      cases.push(std::move(c));
+    }
+  }
+  if (fmt == OUT_JUNIT)
+    return "<?xml version=\"1.0\" encoding=\"UTF-8\"?>\n<testsuites name=\"cfn-guard test report\" tests=\"" + std::to_string(njunit) +
+           "\" failures=\"" + std::to_string(failures) + "\" errors=\"0\" time=\"0\">\n    <testsuite name=\"" + xml_escape(rules_name) +
+           "\" errors=\"0\" failures=\"" + std::to_string(failures) + "\" time=\"0\">\n" + junit + "    </testsuite>\n</testsuites>\n";
+  J res = J::obj();
+  res.add("rule_file", J::str(rules_name));
+  res.add("test_cases", std::move(cases));
+  if (fmt == OUT_YAML) { YamlOut y; y.document(res); return y.buf; }
+  std::string out;
+  pretty(res, 0, out);
+  return out;
 }
 
 bool report_document(const DocBatch& docs, uint32_t doc, const std::vector<const Program*>& progs,

@@ -34,6 +34,27 @@ std::string error_display(const std::string& kind, const std::string& msg);
 // (reporters/validate/structured.rs:99-133, sarif.rs, xml.rs + reporters/mod.rs).
 enum OutFormat : int32_t { OUT_JSON = 0, OUT_YAML = 1, OUT_SARIF = 2, OUT_JUNIT = 3 };
 
+// `cfn-guard test` (commands/test.rs, reporters/test/{generic,structured}.rs): per test case, the
+// rules grouped by name in first-appearance order with their expected / evaluated statuses.
+enum : int32_t { OUT_TEXT = 4 };   // the test command's default single-line-summary text report
+struct TestRuleResult {
+  std::string rule;
+  int32_t expected = -1;              // ST_*; -1: no expectation set for the rule
+  int32_t matched = -1;               // get_status_result: the matched status, -1 = FAIL
+  std::vector<uint32_t> evaluated;    // statuses seen before the match (FAIL: all of them)
+};
+struct TestCaseResult {
+  bool has_name = false;
+  std::string name;
+  std::vector<TestRuleResult> rules;
+};
+struct TestSpecFile {
+  std::string error;                  // non-empty: the spec file did not parse (Error Display)
+  std::vector<TestCaseResult> cases;
+};
+std::string test_report(int32_t fmt, const std::string& rules_name, const std::vector<TestSpecFile>& files,
+                        int32_t& exit_code);
+
 class ReportWriter {
  public:
   explicit ReportWriter(int32_t fmt);

@@ -58,6 +58,9 @@ def lib():
     L.gg_session_report_format.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32),
                                            ctypes.POINTER(ExternError)]
     L.gg_session_report_format.restype = ctypes.c_void_p
+    L.cfn_guard_test.argtypes = [ValidateInput, ctypes.POINTER(ValidateInput), ctypes.c_size_t, ctypes.c_int32,
+                                 ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ExternError)]
+    L.cfn_guard_test.restype = ctypes.c_void_p
     L.gg_session_new.restype = ctypes.c_void_p
     L.gg_session_free.argtypes = [ctypes.c_void_p]
     L.gg_session_add_rules.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(ExternError)]
@@ -140,6 +143,21 @@ def validate_structured(rules, data, output="json"):
     err = ExternError()
     p = lib().cfn_guard_validate_batch_format(D, len(data), R, len(rules), OUTPUT_FORMATS[output], ctypes.byref(code),
                                               ctypes.byref(err))
+    if err.code != 0:
+        _raise(err)
+    return _take_string(p), code.value
+
+
+TEST_OUTPUT_FORMATS = {"text": 4, "json": 0, "yaml": 1, "junit": 3}
+
+
+def run_test(rules_text, rules_name, specs, output="text"):
+    """`cfn-guard test` over one rules file and spec files [(path, text)] -> (report text, exit code)."""
+    S = (ValidateInput * max(1, len(specs)))(*[ValidateInput(_b(t), _b(n)) for n, t in specs])
+    code = ctypes.c_int32(0)
+    err = ExternError()
+    p = lib().cfn_guard_test(ValidateInput(_b(rules_text), _b(rules_name)), S, len(specs), TEST_OUTPUT_FORMATS[output],
+                             ctypes.byref(code), ctypes.byref(err))
     if err.code != 0:
         _raise(err)
     return _take_string(p), code.value

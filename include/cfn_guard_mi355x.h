@@ -52,6 +52,14 @@ char *cfn_guard_validate_batch(const validate_input_t *docs, size_t n_docs, cons
 char *cfn_guard_validate_batch_format(const validate_input_t *docs, size_t n_docs, const validate_input_t *rules,
                                       size_t n_rules, int32_t output_format, int32_t *exit_code, extern_err_t *err);
 
+/* `cfn-guard test -r <rules> -t <spec files> [-o json|yaml|junit]` (commands/test.rs,
+ * reporters/test/generic.rs and structured.rs): one rules file x n_specs test-spec files
+ * (YAML / JSON `Vec<TestSpec>`); output_format CFN_GUARD_OUTPUT_TEXT (the default text report),
+ * _JSON, _YAML or _JUNIT.  *exit_code: 0 / 7 (a test failed) / 1 (a spec file did not parse). */
+#define CFN_GUARD_OUTPUT_TEXT 4
+char *cfn_guard_test(validate_input_t rules, const validate_input_t *specs, size_t n_specs, int32_t output_format,
+                     int32_t *exit_code, extern_err_t *err);
+
 /* ---- session API (documents resident in HBM across evaluations; used by bench.py/tests) ---- */
 typedef struct gg_session gg_session;
 gg_session *gg_session_new(void);

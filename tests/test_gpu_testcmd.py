@@ -1,0 +1,45 @@
+"""`cfn-guard test` on the MI355X path (C ABI cfn_guard_test) against the reference's goldens
+(guard/tests/test_command.rs:157-178, 263-290) and the oracle (oracle/guard_oracle/testcmd.py)."""
+import json
+import os
+
+import pytest
+
+import guard_amd
+from guard_oracle.testcmd import run_test as oracle_test
+
+pytestmark = pytest.mark.gpu
+G = os.path.join(os.path.dirname(__file__), "golden")
+T = os.path.join(G, "test-command")
+RN = "resources/validate/rules-dir/s3_bucket_server_side_encryption_enabled.guard"
+
+
+def _rules():
+    return open(os.path.join(G, "validate", "rules-dir", "s3_bucket_server_side_encryption_enabled.guard")).read()
+
+
+@pytest.mark.parametrize("fmt,gold,spec", [
+    ("text", "test_data_file.out", "json"), ("text", "test_data_file.out", "yaml"),
+    ("json", "structured_single_report_json.out", "yaml"), ("yaml", "structured_single_report_yaml.out", "yaml"),
+    ("junit", "structured_single_report_junit.out", "yaml")])
+def test_test_command_goldens(fmt, gold, spec):
+    sp = "s3_bucket_server_side_encryption_enabled." + spec
+    out, code = guard_amd.run_test(_rules(), RN, [("resources/test-command/data-dir/" + sp, open(os.path.join(T, sp)).read())], fmt)
+    assert code == 0
+    assert out == open(os.path.join(T, gold)).read()
+
+
+def test_reference_example_specs_vs_oracle():
+    """every reference spec in tests/golden/expectations.json, regrouped per (rules file, spec): one
+    `test` run each, all formats, against the oracle"""
+    cases = json.load(open(os.path.join(G, "expectations.json")))
+    groups = {}
+    for c in cases:
+        groups.setdefault((c["rules_name"], c["spec"]), (c["rules_text"], []))[1].append(c)
+    for (rname, spec), (rtext, cs) in sorted(groups.items()):
+        spec_json = json.dumps([{"name": "case %d" % c["case"], "input": json.loads(c["input_json"]),
+                                 "expectations": {"rules": c["expected"]}} for c in cs])
+        for fmt in ("text", "json", "yaml", "junit"):
+            exp = oracle_test(rtext, rname, [(spec, spec_json)], fmt)
+            got = guard_amd.run_test(rtext, rname, [(spec, spec_json)], fmt)
+            assert got == exp, (rname, spec, fmt)
