@@ -78,3 +78,23 @@ def test_config_snapshots_lane_matches_wave():
 
 def test_container_equality_vs_oracle():
     _vs_oracle(synth.cfn_corpus(16, start=300, n_resources=20), _pack("edge_rulepack"), "doc")
+
+
+def test_cfg1_examples_cross_product_vs_oracle():
+    """BASELINE.json configs[0] (the CPU-runnable plumbing case): every guard-examples rules file the
+    reference's own test specs use x every template of guard/resources/validate/data-dir, each
+    (rules file, template) pair through `validate --structured` on the MI355X and on the oracle"""
+    import json
+    cases = json.load(open(os.path.join(G, "expectations.json")))
+    rules = sorted({(c["rules_name"], c["rules_text"]) for c in cases})
+    d = os.path.join(G, "validate", "data-dir")
+    data = [(f, open(os.path.join(d, f)).read()) for f in sorted(os.listdir(d))]
+    for name, text in rules:
+        for dn, dt in data:
+            exp, ecode, _ = oracle_validate([(name, text)], [(dn, dt)])
+            try:
+                out, code = guard_amd.validate_structured([(name, text)], [(dn, dt)])
+            except guard_amd.GuardError as e:
+                assert ecode == -1, (name, dn, e.message)
+                continue
+            assert (out, code) == (exp, ecode), (name, dn)
