@@ -112,7 +112,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
   const uint32_t nbatches = (c1 - c0) * A.nfiles;
   // interpreter state lives in LDS (one Ctx per lane), not in the per-lane stack
   __shared__ Ctx s_ctx[64];
-  __shared__ DevProg s_prog;
   __shared__ uint4 s_blob[LDS_PROG_WORDS / 4];
   LCtx& c = *(LCtx*)&s_ctx[lane];
   uint32_t staged = NONE;
@@ -125,10 +124,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
     const uint32_t file = b % A.nfiles, chunk = c0 + b / A.nfiles;
     const uint32_t doc = chunk * 64u + lane;
     const bool active = doc < A.docs.ndocs;
-    if (file != staged) { P = stage_program(&A.progs[file], &s_prog, s_blob); staged = file; }
+    if (file != staged) { P = stage_program(&A.progs[file], &g_prog, s_blob); staged = file; }
     const uint32_t tile = doc * A.nfiles + file;
     uint32_t status = ST_SKIP, n = 0;
-    if (P != &s_prog) {
+    if (P != &g_prog) {
       // the program did not fit the LDS window: lane mode reads it through LDS-typed pointers only,
       // so the whole batch goes to the wave kernel
       if (active) A.retry_list[atomicAdd(A.retry_count, 1u)] = tile;
