@@ -19,7 +19,7 @@ YAML_LIB = "/opt/conda/lib"
 
 HOST_SRCS = ["doc_loader.cpp", "rules_parser.cpp", "regex_dfa.cpp", "cruet.cpp", "compiler.cpp", "reporter.cpp",
              "synth_corpus.cpp"]
-HIP_SRCS = ["eval_kernel.hip", "capi.cpp"]
+HIP_SRCS = ["eval_kernel.hip", "json_gpu.hip", "capi.cpp"]
 # occupancy target of the lane-mode kernel (waves per SIMD); it caps VGPRs at 512 / N
 LANE_WAVES_PER_EU = os.environ.get("GG_LANE_WAVES_PER_EU", "2")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-I" + YAML_INC, "-Wno-unused-result",

@@ -24,6 +24,7 @@
 #include "doc_loader.h"
 #include "eval_device.h"
 #include "host_format.h"
+#include "json_gpu.h"
 #include "program.h"
 #include "reporter.h"
 #include "synth_corpus.h"
@@ -61,6 +62,13 @@ void set_err(extern_err_t* err, int32_t code, const std::string& msg) {
   if (!err) return;
   err->code = code;
   err->message = code ? dup_str(msg) : nullptr;
+}
+
+// code 0 with a message: an informational verdict (the device loader's refusal / difference)
+void set_note(extern_err_t* err, const std::string& msg) {
+  if (!err) return;
+  err->code = 0;
+  err->message = dup_str(msg);
 }
 
 #define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { throw std::runtime_error(std::string("HIP: ") + hipGetErrorString(e_) + " at " #x); } } while (0)
@@ -988,6 +996,95 @@ int32_t gg_session_add_synthetic(gg_session* s, uint64_t first, size_t n, int32_
     merge_batches(s->docs, parts);
     s->uploaded = false;
     return 0;
+  } catch (std::exception& e) { set_err(err, -1, e.what()); return -1; }
+}
+
+// ---- device loader ----------------------------------------------------------
+static void load_stats(const GpuLoadStats& st, double* out) {
+  if (!out) return;
+  out[0] = st.kernel_ms; out[1] = (double)st.nodes; out[2] = (double)st.distinct_strings;
+  out[3] = (double)st.pool_bytes; out[4] = (double)st.text_bytes; out[5] = st.h2d_ms; out[6] = st.d2h_ms;
+}
+
+int32_t gg_session_add_docs_device(gg_session* s, const char* const* texts, const size_t* lens, const char* const* names,
+                                   size_t n, double* stats, extern_err_t* err) {
+  set_err(err, 0, "");
+  try {
+    std::string why;
+    if (!ensure_device(why)) { set_err(err, -1, why); return -1; }
+    if (s->docs.ndocs()) { set_err(err, 18, "IllegalArguments: the device loader fills an empty session"); return -1; }
+    std::vector<std::string> nm(n);
+    for (size_t i = 0; i < n; i++) nm[i] = names ? names[i] : std::string();
+    GpuLoadStats st;
+    DocBatch b;
+    if (!gpu_load_json(b, texts, lens, nm, n, st, why)) { set_note(err, why); return 1; }
+    s->docs = std::move(b);
+    s->uploaded = false;
+    load_stats(st, stats);
+    return 0;
+  } catch (std::exception& e) { set_err(err, -1, e.what()); return -1; }
+}
+
+int32_t gg_session_add_synthetic_device(gg_session* s, uint64_t first, size_t n, int32_t n_resources, int32_t nthreads,
+                                        double* stats, extern_err_t* err) {
+  set_err(err, 0, "");
+  try {
+    if (nthreads < 1) nthreads = 1;
+    std::vector<std::string> texts(n), names(n);
+    auto work = [&](int t) {
+      for (size_t i = n * t / nthreads; i < n * (t + 1) / nthreads; i++) {
+        cfn_synth_doc(first + i, n_resources, texts[i]);
+        names[i] = "synthetic-" + std::to_string(first + i) + ".json";
+      }
+    };
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthreads; t++) th.emplace_back(work, t);
+    for (auto& x : th) x.join();
+    std::vector<const char*> p(n), nm(n);
+    std::vector<size_t> l(n);
+    for (size_t i = 0; i < n; i++) { p[i] = texts[i].data(); l[i] = texts[i].size(); nm[i] = names[i].c_str(); }
+    return gg_session_add_docs_device(s, p.data(), l.data(), nm.data(), n, stats, err);
+  } catch (std::exception& e) { set_err(err, -1, e.what()); return -1; }
+}
+
+// Parity of the device loader with the host loader on the same documents: 1 = the same arena up
+// to string ids (node kinds, counts, child / parent links, scalars, marks, string bytes, and one
+// pool entry per distinct string), 0 = they differ (`err` says where), -1 = the device refused.
+int32_t gg_loader_device_check(const char* const* texts, const size_t* lens, size_t n, extern_err_t* err) {
+  set_err(err, 0, "");
+  try {
+    std::string why;
+    if (!ensure_device(why)) { set_err(err, -1, why); return -1; }
+    std::vector<std::string> nm(n, "x");
+    DocBatch g, h;
+    GpuLoadStats st;
+    if (!gpu_load_json(g, texts, lens, nm, n, st, why)) { set_note(err, why); return -1; }
+    for (size_t i = 0; i < n; i++) {
+      LoadError le;
+      if (!load_document(h, texts[i], lens[i], "x", LOAD_LIBYAML, le)) { set_note(err, "host loader failed"); return 0; }
+    }
+    auto differ = [&](const std::string& what, size_t at) { set_note(err, what + " at node " + std::to_string(at)); return 0; };
+    if (g.nodes.size() != h.nodes.size()) return differ("node count", 0);
+    if (g.base != h.base || g.roots != h.roots) return differ("document bases", 0);
+    if (g.iused != h.iused) return differ("distinct strings", 0);
+    auto sv = [](const DocBatch& b, uint32_t off, uint32_t len) { return std::string(b.bytes.data() + off, len); };
+    for (size_t k = 0; k < h.nodes.size(); k++) {
+      const DNode &a = g.nodes[k], &b = h.nodes[k];
+      if (a.kind != b.kind || a.count != b.count || a.parent != b.parent || a.key_len != b.key_len) return differ("shape", k);
+      if (g.line[k] != h.line[k] || g.col[k] != h.col[k] || g.kline[k] != h.kline[k] || g.kcol[k] != h.kcol[k]) return differ("marks", k);
+      if ((a.key_off == NONE) != (b.key_off == NONE)) return differ("key presence", k);
+      if (a.key_off != NONE) {
+        if (a.key_hash != a.key_off || sv(g, a.key_off, a.key_len) != sv(h, b.key_off, b.key_len)) return differ("key", k);
+        if (g.find(g.bytes.data() + a.key_off, a.key_len) != a.key_off) return differ("key index", k);
+      }
+      if (a.kind == K_STRING) {
+        if (a.b != a.a || sv(g, a.a, a.count) != sv(h, b.a, b.count)) return differ("string", k);
+        if (g.find(g.bytes.data() + a.a, a.count) != a.a) return differ("string index", k);
+      } else if (a.a != b.a || a.b != b.b) {
+        return differ("scalar / link", k);
+      }
+    }
+    return 1;
   } catch (std::exception& e) { set_err(err, -1, e.what()); return -1; }
 }
 

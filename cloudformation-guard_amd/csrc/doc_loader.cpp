@@ -646,31 +646,43 @@ uint32_t DocBatch::find(const char* p, uint32_t n) const {
   return NONE;
 }
 
-uint32_t DocBatch::intern(const char* p, uint32_t n, uint32_t hash) {
-  if ((iused + 1) * 2 > islots.size()) {
-    size_t cap = islots.empty() ? 4096 : islots.size() * 2;
-    std::vector<uint32_t> ns(cap, 0), nl(cap, 0);
-    for (size_t i = 0; i < islots.size(); i++) {
-      if (!islots[i]) continue;
-      uint32_t off = islots[i] - 1, len = ilen[i];
-      size_t h = fnv1a(bytes.data() + off, len) & (cap - 1);
-      while (ns[h]) h = (h + 1) & (cap - 1);
-      ns[h] = islots[i]; nl[h] = len;
-    }
-    islots.swap(ns); ilen.swap(nl);
+void DocBatch::intern_reserve() {
+  if ((iused + 1) * 2 <= islots.size()) return;
+  size_t cap = islots.empty() ? 4096 : islots.size() * 2;
+  std::vector<uint32_t> ns(cap, 0), nl(cap, 0);
+  for (size_t i = 0; i < islots.size(); i++) {
+    if (!islots[i]) continue;
+    uint32_t off = islots[i] - 1, len = ilen[i];
+    size_t h = fnv1a(bytes.data() + off, len) & (cap - 1);
+    while (ns[h]) h = (h + 1) & (cap - 1);
+    ns[h] = islots[i]; nl[h] = len;
   }
+  islots.swap(ns); ilen.swap(nl);
+}
+
+uint32_t DocBatch::intern(const char* p, uint32_t n, uint32_t hash) {
+  intern_reserve();
   size_t mask = islots.size() - 1;
   size_t h = hash & mask;
   while (islots[h]) {
     if (ilen[h] == n && memcmp(bytes.data() + islots[h] - 1, p, n) == 0) return islots[h] - 1;
     h = (h + 1) & mask;
   }
-  // 16-byte aligned start, zero padding to a 16-byte multiple (device compares in 16-byte chunks)
+  // 16-byte aligned start, zero padding to a 16-byte multiple (device compares in 16-byte chunks);
+  // the empty string takes 16 bytes too, so no two distinct strings share an id
   uint32_t off = (uint32_t)bytes.size();
   bytes.append(p, n);
-  bytes.append((16 - (n & 15)) & 15, '\0');
+  bytes.append(n ? (16 - (n & 15)) & 15 : 16, '\0');
   islots[h] = off + 1; ilen[h] = n; iused++;
   return off;
+}
+
+void DocBatch::adopt(uint32_t off, uint32_t n) {
+  intern_reserve();
+  size_t mask = islots.size() - 1;
+  size_t h = fnv1a(bytes.data() + off, n) & mask;
+  while (islots[h]) h = (h + 1) & mask;
+  islots[h] = off + 1; ilen[h] = n; iused++;
 }
 
 std::string DocBatch::path(uint64_t base, uint32_t node) const {

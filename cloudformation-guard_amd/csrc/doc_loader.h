@@ -37,7 +37,10 @@ struct DocBatch {
   // parts), so a string's pool offset is its id: DNode.b of a string and DNode.key_hash of a map
   // entry carry that id, and the device tests string equality by comparing ids.
   uint32_t intern(const char* p, uint32_t n, uint32_t hash);
+  void intern_reserve();                 // grows islots before one more insertion
   uint32_t find(const char* p, uint32_t n) const;   // pool offset of an interned string, or NONE
+  // indexes a string already in the pool at `off` (a pool built on the device, json_gpu.hip)
+  void adopt(uint32_t off, uint32_t n);
 
   size_t ndocs() const { return roots.size(); }
   std::string path(uint64_t base, uint32_t node) const;  // JSON pointer ("" for a root)

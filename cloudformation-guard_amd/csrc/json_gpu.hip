@@ -1,0 +1,625 @@
+// GPU document loader: strict-JSON text -> columnar node arena (see json_gpu.h).
+//
+// One lane parses one document (documents are a few KB; a lane walks its text through a 16-byte
+// window, so each load serves 16 bytes).  Passes, each a kernel over all documents:
+//   1. count      validate the subset the host fast path accepts (doc_loader.cpp load_json_fast)
+//                 and count nodes, containers, string occurrences;
+//   2. counts     the child count of every container, in pre-order (host: JsonFast::v1);
+//   3. emit       the nodes in the host layout -- each container's children contiguous, blocks in
+//                 DFS pre-order (host: JsonFast::v2) -- with marks, scalar typing, and every
+//                 string inserted into a device hash table keyed by a 64-bit fingerprint of its
+//                 decoded bytes; nodes carry table slots for now; duplicate map keys are refused;
+//   4. own        every occupied slot copies its first occurrence's decoded bytes into the pool
+//                 (16-byte aligned, zero padded: the evaluator compares in 16-byte chunks); the
+//                 pool offset is the string id, as on the host;
+//   5. fix        slots in nodes -> ids;
+//   6. verify     every occurrence's decoded bytes are compared with its id's pool bytes, so a
+//                 fingerprint collision cannot merge two strings silently (the batch is refused).
+// Anything outside the subset refuses the batch; the caller then loads it on the host, so results
+// never depend on which loader ran.
+#include "json_gpu.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <stdexcept>
+
+namespace gg {
+namespace {
+
+#define JCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) throw std::runtime_error(std::string("HIP: ") + hipGetErrorString(e_)); } while (0)
+
+enum : uint32_t { M_COUNT = 0, M_COUNTS = 1, M_EMIT = 2, M_VERIFY = 3 };
+enum : uint32_t {
+  BAD_NONE = 0, BAD_SYNTAX = 1, BAD_DEPTH = 2, BAD_DUPKEY = 3, BAD_NUMBER = 4, BAD_TABLE = 5, BAD_POOL = 6,
+  BAD_VERIFY = 7, BAD_SIZE = 8,
+};
+static const uint32_t kMaxDepth = 64;
+static const uint32_t kMaxPairwiseKeys = 256;
+
+struct JArgs {
+  const uint8_t* text;          // all documents, 16 zero bytes of padding at the end
+  const uint64_t* off;          // [ndocs + 1]
+  uint32_t ndocs;
+  // pass 1 outputs (per document)
+  uint32_t* n_nodes;
+  uint32_t* n_cont;
+  uint32_t* n_str;
+  // pass 2 / 3 inputs
+  const uint64_t* node_base;    // per document: first node
+  const uint64_t* cont_base;    // per document: first container count
+  uint32_t* counts;
+  DNode* nodes;
+  uint32_t* line;
+  uint32_t* col;
+  uint32_t* kline;
+  uint32_t* kcol;
+  // intern table
+  unsigned long long* tkey;     // 0 = empty
+  uint32_t* tlen;
+  unsigned long long* towner;   // doc << 32 | offset of the opening quote in the document
+  uint32_t* tid;
+  uint64_t tmask;
+  uint8_t* pool;
+  unsigned long long* pool_cursor;
+  uint64_t pool_cap;
+  uint32_t* bad;                // first refusal reason (BAD_*), 0 = none
+};
+
+__device__ inline void refuse(const JArgs& A, uint32_t why) { atomicCAS(A.bad, 0u, why); }
+
+struct Text {
+  const uint8_t* s;
+  uint64_t base, n;
+  uint4 w;
+  uint64_t wb;
+  __device__ Text(const uint8_t* t, uint64_t b, uint64_t len) : s(t), base(b), n(len), wb(~0ull) {}
+  // byte i of the document, 256 past its end
+  __device__ uint32_t at(uint64_t i) {
+    if (i >= n) return 256u;
+    const uint64_t g = base + i, a = g & ~15ull;
+    if (a != wb) { w = *(const uint4*)(s + a); wb = a; }
+    const uint32_t k = (uint32_t)(g - a);
+    const uint32_t word = k < 4 ? w.x : (k < 8 ? w.y : (k < 12 ? w.z : w.w));
+    return (word >> ((k & 3u) * 8u)) & 0xFFu;
+  }
+};
+
+__device__ inline uint64_t mix64(uint64_t x) {
+  x ^= x >> 30; x *= 0xbf58476d1ce4e5b9ull;
+  x ^= x >> 27; x *= 0x94d049bb133111ebull;
+  x ^= x >> 31;
+  return x;
+}
+
+// Decodes the JSON string whose opening quote is at `q`; calls sink(byte) per decoded byte.
+// Returns the index after the closing quote, or 0 when the string is outside the subset
+// (raw bytes outside 0x20..0x7E, bad escapes, surrogate \u escapes: the host path rejects them too).
+template <typename Sink>
+__device__ uint64_t decode_string(Text& T, uint64_t q, Sink&& sink) {
+  uint64_t i = q + 1;
+  for (;;) {
+    const uint32_t c = T.at(i);
+    if (c == '"') return i + 1;
+    if (c < 0x20u || c > 0x7Eu) return 0;
+    if (c != '\\') { sink((uint8_t)c); i++; continue; }
+    const uint32_t e = T.at(i + 1);
+    uint32_t out;
+    switch (e) {
+      case '"': out = '"'; break;
+      case '\\': out = '\\'; break;
+      case '/': out = '/'; break;
+      case 'b': out = '\b'; break;
+      case 'f': out = '\f'; break;
+      case 'n': out = '\n'; break;
+      case 'r': out = '\r'; break;
+      case 't': out = '\t'; break;
+      case 'u': {
+        uint32_t cp = 0;
+        for (uint32_t k = 0; k < 4; k++) {
+          const uint32_t h = T.at(i + 2 + k);
+          cp <<= 4;
+          if (h >= '0' && h <= '9') cp |= h - '0';
+          else if (h >= 'a' && h <= 'f') cp |= h - 'a' + 10;
+          else if (h >= 'A' && h <= 'F') cp |= h - 'A' + 10;
+          else return 0;
+        }
+        if (cp >= 0xD800 && cp <= 0xDFFF) return 0;
+        if (cp < 0x80) sink((uint8_t)cp);
+        else if (cp < 0x800) { sink((uint8_t)(0xC0 | (cp >> 6))); sink((uint8_t)(0x80 | (cp & 0x3F))); }
+        else { sink((uint8_t)(0xE0 | (cp >> 12))); sink((uint8_t)(0x80 | ((cp >> 6) & 0x3F))); sink((uint8_t)(0x80 | (cp & 0x3F))); }
+        i += 6;
+        continue;
+      }
+      default: return 0;
+    }
+    sink((uint8_t)out);
+    i += 2;
+  }
+}
+
+struct Fp { uint64_t h = 0xcbf29ce484222325ull; uint32_t len = 0; };
+
+__device__ inline bool is_digit(uint32_t c) { return c >= '0' && c <= '9'; }
+
+// length of the plain token at i (JSON number / true / false / null), 0 if not one
+__device__ uint64_t plain_len(Text& T, uint64_t i) {
+  const uint32_t c0 = T.at(i);
+  if (c0 == 't' || c0 == 'f' || c0 == 'n') {
+    const char* w = c0 == 't' ? "true" : (c0 == 'f' ? "false" : "null");
+    uint64_t L = c0 == 'f' ? 5 : 4;
+    for (uint64_t k = 0; k < L; k++) if (T.at(i + k) != (uint32_t)(uint8_t)w[k]) return 0;
+    return L;
+  }
+  uint64_t j = i;
+  if (T.at(j) == '-') j++;
+  if (T.at(j) == '0') j++;
+  else if (T.at(j) >= '1' && T.at(j) <= '9') { while (is_digit(T.at(j))) j++; }
+  else return 0;
+  if (T.at(j) == '.') { j++; const uint64_t d = j; while (is_digit(T.at(j))) j++; if (j == d) return 0; }
+  if (T.at(j) == 'e' || T.at(j) == 'E') {
+    j++;
+    if (T.at(j) == '+' || T.at(j) == '-') j++;
+    const uint64_t d = j;
+    while (is_digit(T.at(j))) j++;
+    if (j == d) return 0;
+  }
+  return j - i;
+}
+
+__device__ inline bool after_plain_ok(uint32_t c) { return c == 256u || c == ' ' || c == '\n' || c == ',' || c == ']' || c == '}'; }
+
+__constant__ double kPow10[23] = {1e0, 1e1, 1e2, 1e3, 1e4, 1e5, 1e6, 1e7, 1e8, 1e9, 1e10, 1e11,
+                                  1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+
+// Scalar typing of a plain token (host JsonFast::v2: true / false / null, then Rust i64::from_str,
+// then f64): i64 exactly; f64 by Clinger's fast path (<= 15 significant digits, |exponent| <= 22:
+// one correctly rounded multiply or divide of two exact doubles); any other float refuses.
+__device__ bool scalar(Text& T, uint64_t i, uint64_t L, DNode& d) {
+  const uint32_t c0 = T.at(i);
+  if (c0 == 't') { d.kind = K_BOOL; d.a = 1; return true; }
+  if (c0 == 'f') { d.kind = K_BOOL; d.a = 0; return true; }
+  if (c0 == 'n') { d.kind = K_NULL; return true; }
+  bool neg = c0 == '-';
+  uint64_t j = i + (neg ? 1 : 0);
+  bool is_int = true;
+  for (uint64_t k = j; k < i + L; k++) if (!is_digit(T.at(k))) { is_int = false; break; }
+  if (is_int) {
+    uint64_t v = 0;
+    for (uint64_t k = j; k < i + L; k++) {
+      const uint32_t dg = T.at(k) - '0';
+      if (v > (0xFFFFFFFFFFFFFFFFull - dg) / 10ull) return false;   // beyond u64: refuse
+      v = v * 10ull + dg;
+    }
+    if (!neg && v > 0x7FFFFFFFFFFFFFFFull) return false;
+    if (neg && v > 0x8000000000000000ull) return false;
+    const uint64_t u = neg ? (uint64_t)(-(int64_t)(v - 1) - 1) : v;
+    d.kind = K_INT; d.a = (uint32_t)u; d.b = (uint32_t)(u >> 32);
+    return true;
+  }
+  uint64_t m = 0;
+  int32_t digits = 0, exp10 = 0;
+  bool frac = false;
+  uint64_t k = j;
+  for (; k < i + L; k++) {
+    const uint32_t c = T.at(k);
+    if (c == '.') { frac = true; continue; }
+    if (c == 'e' || c == 'E') break;
+    if (m == 0 && c == '0') { if (frac) exp10--; continue; }   // leading zeros
+    if (digits >= 15) return false;
+    m = m * 10ull + (c - '0');
+    digits++;
+    if (frac) exp10--;
+  }
+  if (k < i + L) {
+    k++;
+    bool eneg = false;
+    if (T.at(k) == '+' || T.at(k) == '-') { eneg = T.at(k) == '-'; k++; }
+    int32_t e = 0;
+    for (; k < i + L; k++) { e = e * 10 + (int32_t)(T.at(k) - '0'); if (e > 10000) return false; }
+    exp10 += eneg ? -e : e;
+  }
+  double v;
+  if (m == 0) v = 0.0;
+  else if (exp10 >= 0 && exp10 <= 22) v = (double)m * kPow10[exp10];
+  else if (exp10 < 0 && exp10 >= -22) v = (double)m / kPow10[-exp10];
+  else return false;
+  if (neg) v = -v;
+  const uint64_t u = (uint64_t)__double_as_longlong(v);
+  d.kind = K_FLOAT; d.a = (uint32_t)u; d.b = (uint32_t)(u >> 32);
+  return true;
+}
+
+// insert-or-find a string fingerprint; returns its slot, or ~0u when the table is full
+__device__ uint32_t intern_slot(const JArgs& A, uint64_t key, uint32_t len, uint32_t doc, uint32_t q) {
+  uint64_t idx = mix64(key) & A.tmask;
+  for (uint32_t probe = 0; probe < 1024; probe++) {
+    const unsigned long long k = A.tkey[idx];
+    if (k == key) return (uint32_t)idx;
+    if (k == 0) {
+      const unsigned long long old = atomicCAS(&A.tkey[idx], 0ull, (unsigned long long)key);
+      if (old == 0) {
+        A.tlen[idx] = len;
+        A.towner[idx] = ((unsigned long long)doc << 32) | q;
+        return (uint32_t)idx;
+      }
+      if (old == key) return (uint32_t)idx;
+    }
+    idx = (idx + 1) & A.tmask;
+  }
+  return ~0u;
+}
+
+struct Frame {
+  uint32_t first;   // EMIT / VERIFY: first child (document-relative)
+  uint32_t j;       // elements done
+  uint32_t slot;    // the container's own node (document-relative)
+  uint32_t k;       // pre-order container index
+  uint32_t map;     // 1 map, 0 list
+};
+
+template <uint32_t MODE>
+__device__ void parse_doc(const JArgs& A, uint32_t d) {
+  const uint64_t b0 = A.off[d], b1 = A.off[d + 1];
+  Text T(A.text, b0, b1 - b0);
+  uint64_t i = 0, ls = 0;
+  uint32_t line = 0;
+  auto ws = [&]() {
+    for (;;) {
+      const uint32_t c = T.at(i);
+      if (c == ' ') i++;
+      else if (c == '\n') { i++; line++; ls = i; }
+      else break;
+    }
+  };
+  const uint64_t nb = (MODE >= M_EMIT) ? A.node_base[d] : 0;
+  const uint64_t cb = (MODE >= M_COUNTS) ? A.cont_base[d] : 0;
+  uint32_t nn = 1, nc = 0, ns = 0, ci = 0, next = 1;
+  Frame st[kMaxDepth];
+  uint32_t sp = 0;
+
+  // a string occurrence at i (the opening quote), for node `rel` (key or value): returns the
+  // index after it, 0 on refusal; EMIT -> *slot; VERIFY compares with the pool
+  auto string_at = [&](uint32_t rel, bool key, uint32_t* slot_out, uint32_t* len_out) -> uint64_t {
+    Fp fp;
+    uint32_t h32 = 0;
+    (void)h32;
+    uint64_t end;
+    if (MODE == M_VERIFY) {
+      const DNode& nd = A.nodes[nb + rel];
+      const uint32_t id = key ? nd.key_off : nd.a;
+      const uint32_t want = key ? nd.key_len : nd.count;
+      uint32_t pos = 0;
+      bool same = true;
+      end = decode_string(T, i, [&](uint8_t c) {
+        if (pos >= want || A.pool[(uint64_t)id + pos] != c) same = false;
+        pos++;
+      });
+      if (end && (!same || pos != want)) { refuse(A, BAD_VERIFY); return 0; }
+      return end;
+    }
+    end = decode_string(T, i, [&](uint8_t c) {
+      fp.h = (fp.h ^ c) * 0x100000001b3ull;
+      fp.len++;
+    });
+    if (!end) return 0;
+    if (MODE == M_EMIT) {
+      const uint64_t key64 = mix64(fp.h ^ ((uint64_t)fp.len * 0x9E3779B97F4A7C15ull)) | 1ull;
+      const uint32_t s = intern_slot(A, key64, fp.len, d, (uint32_t)i);
+      if (s == ~0u) { refuse(A, BAD_TABLE); return 0; }
+      *slot_out = s;
+      *len_out = fp.len;
+    }
+    return end;
+  };
+
+  // one value at i for node `rel` whose parent is `parent`; containers push a frame
+  auto value = [&](uint32_t rel, uint32_t parent) -> bool {
+    const uint32_t c = T.at(i);
+    if (c == '"') {
+      uint32_t slot = 0, len = 0;
+      const uint64_t e = string_at(rel, false, &slot, &len);
+      if (!e) return false;
+      i = e;
+      ns++;
+      if (MODE == M_EMIT) {
+        DNode& nd = A.nodes[nb + rel];
+        nd.kind = K_STRING; nd.count = len; nd.a = slot; nd.b = slot; nd.parent = parent;
+      }
+      return true;
+    }
+    if (c == '{' || c == '[') {
+      if (sp >= kMaxDepth) { refuse(A, BAD_DEPTH); return false; }
+      const uint32_t is_map = c == '{';
+      const uint32_t k = ci++;
+      nc++;
+      uint32_t cnt = 0, first = 0;
+      if (MODE >= M_EMIT) {
+        cnt = A.counts[cb + k];
+        first = next;
+        next += cnt;
+      }
+      if (MODE == M_EMIT) {
+        DNode& nd = A.nodes[nb + rel];
+        nd.kind = is_map ? K_MAP : K_LIST; nd.count = cnt; nd.a = first; nd.b = 0; nd.parent = parent;
+      }
+      i++;
+      ws();
+      if (T.at(i) == (is_map ? (uint32_t)'}' : (uint32_t)']')) {
+        i++;
+        if (MODE == M_COUNTS) A.counts[cb + k] = 0;
+        return true;
+      }
+      st[sp].first = first; st[sp].j = 0; st[sp].slot = rel; st[sp].k = k; st[sp].map = is_map;
+      sp++;
+      return true;
+    }
+    const uint64_t L = plain_len(T, i);
+    if (!L || !after_plain_ok(T.at(i + L))) return false;
+    if (MODE == M_EMIT) {
+      DNode& nd = A.nodes[nb + rel];
+      nd.count = 0; nd.a = 0; nd.b = 0; nd.parent = parent;
+      if (!scalar(T, i, L, nd)) { refuse(A, BAD_NUMBER); return false; }
+    }
+    i += L;
+    return true;
+  };
+
+  ws();
+  const uint32_t c0 = T.at(i);
+  if (c0 != '{' && c0 != '[') { refuse(A, BAD_SYNTAX); return; }
+  if (MODE == M_EMIT) {
+    DNode& r = A.nodes[nb];
+    r.key_off = NONE; r.key_len = 0; r.key_hash = 0;
+    const bool list = c0 == '[';
+    A.line[nb] = list ? 0 : line; A.col[nb] = list ? 0 : (uint32_t)(i - ls);   // emit_root: lists keep (0,0)
+    A.kline[nb] = 0; A.kcol[nb] = 0;
+  }
+  if (!value(0, NONE)) { refuse(A, BAD_SYNTAX); return; }
+  while (sp) {
+    Frame& F = st[sp - 1];
+    const uint32_t close = F.map ? '}' : ']';
+    // one element of F
+    const uint32_t cs = F.first + F.j;
+    if (F.map) {
+      if (T.at(i) != '"') { refuse(A, BAD_SYNTAX); return; }
+      const uint64_t kstart = i;
+      const uint32_t kl = line, kc = (uint32_t)(i - ls);
+      uint32_t slot = 0, len = 0;
+      const uint64_t e = string_at(cs, true, &slot, &len);
+      if (!e) { refuse(A, BAD_SYNTAX); return; }
+      i = e;
+      ns++;
+      if (MODE == M_EMIT) {
+        DNode& nd = A.nodes[nb + cs];
+        nd.key_off = slot; nd.key_len = len; nd.key_hash = slot;
+        A.kline[nb + cs] = kl; A.kcol[nb + cs] = kc;
+      }
+      while (T.at(i) == ' ') i++;
+      if (T.at(i) != ':' || line != kl || i - kstart > 1000) { refuse(A, BAD_SYNTAX); return; }
+      i++;
+      ws();
+    } else if (MODE == M_EMIT) {
+      DNode& nd = A.nodes[nb + cs];
+      nd.key_off = NONE; nd.key_len = 0; nd.key_hash = 0;
+      A.kline[nb + cs] = 0; A.kcol[nb + cs] = 0;
+    }
+    if (MODE == M_EMIT) { A.line[nb + cs] = line; A.col[nb + cs] = (uint32_t)(i - ls); }
+    F.j++;
+    nn++;
+    const uint32_t depth_before = sp;
+    if (!value(cs, F.slot)) { refuse(A, BAD_SYNTAX); return; }
+    if (sp > depth_before) continue;   // a nested container: its elements come first
+    // after an element: ',' or the close of this container (and of every container it completes)
+    for (;;) {
+      Frame& G = st[sp - 1];
+      const uint32_t gclose = G.map ? '}' : ']';
+      ws();
+      const uint32_t c = T.at(i);
+      if (c == ',') { i++; ws(); break; }
+      if (c != gclose) { refuse(A, BAD_SYNTAX); return; }
+      i++;
+      // container complete
+      if (MODE == M_COUNTS) A.counts[cb + G.k] = G.j;
+      if (MODE == M_EMIT && G.map) {
+        // duplicate keys (the host fast path refuses them too; IndexMap keeps the last value)
+        if (G.j > kMaxPairwiseKeys) { refuse(A, BAD_DUPKEY); return; }
+        for (uint32_t p = 1; p < G.j; p++) {
+          const uint32_t kp = A.nodes[nb + G.first + p].key_hash;
+          for (uint32_t q = 0; q < p; q++)
+            if (A.nodes[nb + G.first + q].key_hash == kp) { refuse(A, BAD_DUPKEY); return; }
+        }
+      }
+      sp--;
+      if (!sp) break;
+    }
+    (void)close;
+  }
+  ws();
+  if (i != T.n) { refuse(A, BAD_SYNTAX); return; }
+  if (MODE == M_COUNT) { A.n_nodes[d] = nn; A.n_cont[d] = nc; A.n_str[d] = ns; }
+}
+
+template <uint32_t MODE>
+__global__ void __launch_bounds__(256) json_pass_kernel(JArgs A) {
+  for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < A.ndocs; d += gridDim.x * blockDim.x) {
+    if (*A.bad) return;
+    parse_doc<MODE>(A, d);
+  }
+}
+
+// pass 4: every occupied slot copies its first occurrence's decoded bytes into the pool
+__global__ void __launch_bounds__(256) json_own_kernel(JArgs A) {
+  for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s <= A.tmask; s += (uint64_t)gridDim.x * blockDim.x) {
+    if (A.tkey[s] == 0) continue;
+    const uint32_t len = A.tlen[s];
+    const uint64_t need = len ? (len + 15ull) & ~15ull : 16ull;   // as DocBatch::intern
+    const unsigned long long at = atomicAdd(A.pool_cursor, (unsigned long long)need);
+    if (at + need > A.pool_cap || at + need > 0xF0000000ull) { refuse(A, BAD_POOL); A.tid[s] = 0; continue; }
+    A.tid[s] = (uint32_t)at;
+    const uint32_t doc = (uint32_t)(A.towner[s] >> 32), q = (uint32_t)A.towner[s];
+    Text T(A.text, A.off[doc], A.off[doc + 1] - A.off[doc]);
+    uint64_t p = at;
+    decode_string(T, q, [&](uint8_t c) { A.pool[p++] = c; });
+  }
+}
+
+// pass 5: table slots in the nodes -> string ids (pool offsets)
+__global__ void __launch_bounds__(256) json_fix_kernel(JArgs A, uint64_t nnodes) {
+  for (uint64_t n = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; n < nnodes; n += (uint64_t)gridDim.x * blockDim.x) {
+    DNode d = A.nodes[n];
+    bool w = false;
+    if (d.kind == K_STRING) { d.a = A.tid[d.a]; d.b = d.a; w = true; }
+    if (d.key_off != NONE) { d.key_off = A.tid[d.key_off]; d.key_hash = d.key_off; w = true; }
+    if (w) A.nodes[n] = d;
+  }
+}
+
+template <typename T>
+struct DevArr {
+  T* p = nullptr;
+  size_t n = 0;
+  ~DevArr() { if (p) hipFree(p); }
+  void alloc(size_t count) { n = count; JCHK(hipMalloc(&p, std::max<size_t>(count, 1) * sizeof(T))); }
+};
+
+uint32_t grid_for(uint64_t items, uint32_t block) {
+  return (uint32_t)std::min<uint64_t>((items + block - 1) / block, 65536ull);
+}
+
+}  // namespace
+
+bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, const std::vector<std::string>& names,
+                   size_t n, GpuLoadStats& st, std::string& why) {
+  static const char* kWhy[] = {"", "outside the strict-JSON subset", "nesting deeper than 64", "duplicate map keys",
+                               "a float outside the exact fast path", "string table full", "string pool full",
+                               "string fingerprint collision", "batch too large"};
+  if (!out.nodes.empty() || !out.roots.empty()) { why = "the device loader fills an empty batch"; return false; }
+  if (n == 0) return true;
+  if (n > 0xFFFFFFF0ull) { why = kWhy[BAD_SIZE]; return false; }
+  // documents back to back, 16 zero bytes of padding for the 16-byte window
+  std::vector<uint64_t> off(n + 1, 0);
+  for (size_t k = 0; k < n; k++) {
+    if (lens[k] > 0xFFFFFFF0ull) { why = kWhy[BAD_SIZE]; return false; }
+    off[k + 1] = off[k] + lens[k];
+  }
+  const uint64_t total = off[n];
+  std::vector<uint8_t> host(total + 16, 0);
+  for (size_t k = 0; k < n; k++) memcpy(host.data() + off[k], texts[k], lens[k]);
+  st.text_bytes = total;
+
+  hipEvent_t e0, e1;
+  JCHK(hipEventCreate(&e0));
+  JCHK(hipEventCreate(&e1));
+  auto t0 = std::chrono::steady_clock::now();
+  DevArr<uint8_t> d_text; d_text.alloc(total + 16);
+  DevArr<uint64_t> d_off; d_off.alloc(n + 1);
+  JCHK(hipMemcpy(d_text.p, host.data(), total + 16, hipMemcpyHostToDevice));
+  JCHK(hipMemcpy(d_off.p, off.data(), (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice));
+  st.h2d_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  std::vector<uint8_t>().swap(host);
+
+  DevArr<uint32_t> d_nn, d_nc, d_ns, d_bad;
+  d_nn.alloc(n); d_nc.alloc(n); d_ns.alloc(n); d_bad.alloc(1);
+  JCHK(hipMemset(d_bad.p, 0, 4));
+  JArgs A{};
+  A.text = d_text.p; A.off = d_off.p; A.ndocs = (uint32_t)n;
+  A.n_nodes = d_nn.p; A.n_cont = d_nc.p; A.n_str = d_ns.p; A.bad = d_bad.p;
+  const uint32_t dgrid = grid_for(n, 256);
+  float ms_total = 0, ms = 0;
+  auto bad_now = [&]() {
+    uint32_t b = 0;
+    JCHK(hipMemcpy(&b, d_bad.p, 4, hipMemcpyDeviceToHost));
+    if (b) why = b < 9 ? kWhy[b] : "refused";
+    return b != 0;
+  };
+
+  // 1. count
+  JCHK(hipEventRecord(e0));
+  hipLaunchKernelGGL(json_pass_kernel<M_COUNT>, dim3(dgrid), dim3(256), 0, 0, A);
+  JCHK(hipGetLastError());
+  JCHK(hipEventRecord(e1));
+  JCHK(hipEventSynchronize(e1));
+  JCHK(hipEventElapsedTime(&ms, e0, e1)); ms_total += ms;
+  if (bad_now()) return false;
+  std::vector<uint32_t> nn(n), nc(n), ns(n);
+  JCHK(hipMemcpy(nn.data(), d_nn.p, n * 4, hipMemcpyDeviceToHost));
+  JCHK(hipMemcpy(nc.data(), d_nc.p, n * 4, hipMemcpyDeviceToHost));
+  JCHK(hipMemcpy(ns.data(), d_ns.p, n * 4, hipMemcpyDeviceToHost));
+  std::vector<uint64_t> nbase(n), cbase(n);
+  uint64_t N = 0, C = 0, S = 0;
+  for (size_t k = 0; k < n; k++) {
+    if (nn[k] > kMaxDocNodes) { why = kWhy[BAD_SIZE]; return false; }
+    nbase[k] = N; cbase[k] = C;
+    N += nn[k]; C += nc[k]; S += ns[k];
+  }
+  DevArr<uint64_t> d_nbase, d_cbase;
+  d_nbase.alloc(n); d_cbase.alloc(n);
+  JCHK(hipMemcpy(d_nbase.p, nbase.data(), n * 8, hipMemcpyHostToDevice));
+  JCHK(hipMemcpy(d_cbase.p, cbase.data(), n * 8, hipMemcpyHostToDevice));
+  DevArr<uint32_t> d_counts; d_counts.alloc(C);
+  DevArr<DNode> d_nodes; d_nodes.alloc(N);
+  DevArr<uint32_t> d_line, d_col, d_kline, d_kcol;
+  d_line.alloc(N); d_col.alloc(N); d_kline.alloc(N); d_kcol.alloc(N);
+  // intern table: 2 slots per string occurrence, between 2^16 and 2^26 slots
+  uint64_t tslots = 1ull << 16;
+  while (tslots < 2 * S && tslots < (1ull << 26)) tslots <<= 1;
+  DevArr<unsigned long long> d_tkey, d_towner, d_pool_cursor;
+  DevArr<uint32_t> d_tlen, d_tid;
+  d_tkey.alloc(tslots); d_towner.alloc(tslots); d_tlen.alloc(tslots); d_tid.alloc(tslots); d_pool_cursor.alloc(1);
+  JCHK(hipMemset(d_tkey.p, 0, tslots * 8));
+  JCHK(hipMemset(d_pool_cursor.p, 0, 8));
+  const uint64_t pool_cap = std::min<uint64_t>(std::max<uint64_t>(total / 4, 1ull << 20), 0xF0000000ull);
+  DevArr<uint8_t> d_pool; d_pool.alloc(pool_cap + 16);
+  JCHK(hipMemset(d_pool.p, 0, pool_cap + 16));
+  A.node_base = d_nbase.p; A.cont_base = d_cbase.p; A.counts = d_counts.p; A.nodes = d_nodes.p;
+  A.line = d_line.p; A.col = d_col.p; A.kline = d_kline.p; A.kcol = d_kcol.p;
+  A.tkey = d_tkey.p; A.tlen = d_tlen.p; A.towner = d_towner.p; A.tid = d_tid.p; A.tmask = tslots - 1;
+  A.pool = d_pool.p; A.pool_cursor = d_pool_cursor.p; A.pool_cap = pool_cap;
+
+  // 2. counts, 3. emit, 4. own, 5. fix, 6. verify
+  JCHK(hipEventRecord(e0));
+  hipLaunchKernelGGL(json_pass_kernel<M_COUNTS>, dim3(dgrid), dim3(256), 0, 0, A);
+  hipLaunchKernelGGL(json_pass_kernel<M_EMIT>, dim3(dgrid), dim3(256), 0, 0, A);
+  hipLaunchKernelGGL(json_own_kernel, dim3(grid_for(tslots, 256)), dim3(256), 0, 0, A);
+  hipLaunchKernelGGL(json_fix_kernel, dim3(grid_for(N, 256)), dim3(256), 0, 0, A, N);
+  hipLaunchKernelGGL(json_pass_kernel<M_VERIFY>, dim3(dgrid), dim3(256), 0, 0, A);
+  JCHK(hipGetLastError());
+  JCHK(hipEventRecord(e1));
+  JCHK(hipEventSynchronize(e1));
+  JCHK(hipEventElapsedTime(&ms, e0, e1)); ms_total += ms;
+  st.kernel_ms = ms_total;
+  JCHK(hipEventDestroy(e0));
+  JCHK(hipEventDestroy(e1));
+  if (bad_now()) return false;
+
+  // results to the host batch (the host keeps the reporter's columns and the intern index)
+  t0 = std::chrono::steady_clock::now();
+  unsigned long long pool_used = 0;
+  JCHK(hipMemcpy(&pool_used, d_pool_cursor.p, 8, hipMemcpyDeviceToHost));
+  out.nodes.resize(N); out.line.resize(N); out.col.resize(N); out.kline.resize(N); out.kcol.resize(N);
+  JCHK(hipMemcpy(out.nodes.data(), d_nodes.p, N * sizeof(DNode), hipMemcpyDeviceToHost));
+  JCHK(hipMemcpy(out.line.data(), d_line.p, N * 4, hipMemcpyDeviceToHost));
+  JCHK(hipMemcpy(out.col.data(), d_col.p, N * 4, hipMemcpyDeviceToHost));
+  JCHK(hipMemcpy(out.kline.data(), d_kline.p, N * 4, hipMemcpyDeviceToHost));
+  JCHK(hipMemcpy(out.kcol.data(), d_kcol.p, N * 4, hipMemcpyDeviceToHost));
+  out.bytes.resize(pool_used);
+  if (pool_used) JCHK(hipMemcpy(&out.bytes[0], d_pool.p, pool_used, hipMemcpyDeviceToHost));
+  std::vector<unsigned long long> tkey(tslots);
+  std::vector<uint32_t> tlen(tslots), tid(tslots);
+  JCHK(hipMemcpy(tkey.data(), d_tkey.p, tslots * 8, hipMemcpyDeviceToHost));
+  JCHK(hipMemcpy(tlen.data(), d_tlen.p, tslots * 4, hipMemcpyDeviceToHost));
+  JCHK(hipMemcpy(tid.data(), d_tid.p, tslots * 4, hipMemcpyDeviceToHost));
+  st.d2h_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  uint64_t distinct = 0;
+  for (uint64_t s = 0; s < tslots; s++) if (tkey[s]) { out.adopt(tid[s], tlen[s]); distinct++; }
+  out.roots.assign(n, 0);
+  out.base.assign(nbase.begin(), nbase.end());
+  out.names.assign(names.begin(), names.begin() + n);
+  st.nodes = N; st.distinct_strings = distinct; st.pool_bytes = pool_used;
+  return true;
+}
+
+}  // namespace gg

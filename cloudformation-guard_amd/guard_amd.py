@@ -98,8 +98,43 @@ def lib():
     L.gg_synth_cfn_doc.restype = ctypes.c_size_t
     L.gg_session_add_synthetic.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_int32,
                                            ctypes.c_int32, ctypes.POINTER(ExternError)]
+    L.gg_session_add_docs_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_size_t),
+                                             ctypes.POINTER(ctypes.c_char_p), ctypes.c_size_t, ctypes.POINTER(ctypes.c_double),
+                                             ctypes.POINTER(ExternError)]
+    L.gg_session_add_synthetic_device.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_int32,
+                                                  ctypes.c_int32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ExternError)]
+    L.gg_loader_device_check.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_size_t), ctypes.c_size_t,
+                                         ctypes.POINTER(ExternError)]
     _lib = L
     return L
+
+
+LOAD_STATS = ("kernel_ms", "nodes", "distinct_strings", "pool_bytes", "text_bytes", "h2d_ms", "d2h_ms")
+
+
+def _load_result(rc, err, st):
+    if rc < 0:
+        _raise(err)
+    note = _take_string(err.message)
+    if rc == 1:
+        return None
+    out = dict(zip(LOAD_STATS, list(st)))
+    out["note"] = note
+    return out
+
+
+def loader_device_check(texts):
+    """1 = the device loader builds the host loader's arena (up to string ids), 0 = differs, -1 = refused;
+    returns (verdict, message)"""
+    n = len(texts)
+    bufs = [_b(t) for t in texts]
+    T = (ctypes.c_char_p * n)(*bufs)
+    Ls = (ctypes.c_size_t * n)(*[len(b) for b in bufs])
+    err = ExternError()
+    rc = lib().gg_loader_device_check(T, Ls, n, ctypes.byref(err))
+    if err.code != 0:
+        _raise(err)
+    return rc, _take_string(err.message) or ""
 
 
 def _take_string(p):
@@ -196,6 +231,25 @@ class Session:
         lib().gg_session_add_docs(self.s, T, Ls, N, n, mode, threads, ctypes.byref(err))
         if err.code != 0:
             _raise(err)
+
+    def add_docs_device(self, texts, names=None):
+        """Parses and interns strict-JSON documents on the MI355X (empty session only).  Returns the
+        loader statistics, or None when a document is outside the device subset (nothing loaded)."""
+        n = len(texts)
+        bufs = [_b(t) for t in texts]
+        T = (ctypes.c_char_p * n)(*bufs)
+        Ls = (ctypes.c_size_t * n)(*[len(b) for b in bufs])
+        N = (ctypes.c_char_p * n)(*[_b(x) for x in (names or ["" for _ in range(n)])])
+        st = (ctypes.c_double * len(LOAD_STATS))()
+        err = ExternError()
+        rc = lib().gg_session_add_docs_device(self.s, T, Ls, N, n, st, ctypes.byref(err))
+        return _load_result(rc, err, st)
+
+    def add_synthetic_device(self, first, n, n_resources=50, threads=8):
+        st = (ctypes.c_double * len(LOAD_STATS))()
+        err = ExternError()
+        rc = lib().gg_session_add_synthetic_device(self.s, first, n, n_resources, threads, st, ctypes.byref(err))
+        return _load_result(rc, err, st)
 
     def upload(self):
         err = ExternError()

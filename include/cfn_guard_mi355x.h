@@ -107,6 +107,20 @@ size_t gg_synth_cfn_doc(uint64_t index, int32_t n_resources, char *buf, size_t c
 int32_t gg_session_add_synthetic(gg_session *s, uint64_t first, size_t n, int32_t n_resources, int32_t nthreads,
                                  extern_err_t *err);
 
+/* Device loader (replaces, for strict-JSON input, the reference's
+ * Loader::load + PathAwareValue::try_from, guard/src/rules/libyaml/loader.rs:31-195 and
+ * guard/src/rules/path_value.rs:414-478, as called from validate.rs:760-787).  Parses and interns
+ * the documents on the MI355X into an EMPTY session, building the arena gg_session_add_docs builds.
+ * Returns 0 when loaded, 1 when some document is outside the device subset (nothing loaded, err->message
+ * says why; load the batch with gg_session_add_docs), -1 on error.  stats (may be NULL, 7 doubles):
+ * kernel ms, nodes, distinct strings, pool bytes, text bytes, H2D ms, D2H ms. */
+int32_t gg_session_add_docs_device(gg_session *s, const char *const *texts, const size_t *lens, const char *const *names,
+                                   size_t n, double *stats, extern_err_t *err);
+int32_t gg_session_add_synthetic_device(gg_session *s, uint64_t first, size_t n, int32_t n_resources, int32_t nthreads,
+                                        double *stats, extern_err_t *err);
+/* 1 = the device loader builds the host loader's arena (up to string ids), 0 = differs, -1 = refused */
+int32_t gg_loader_device_check(const char *const *texts, const size_t *lens, size_t n, extern_err_t *err);
+
 #ifdef __cplusplus
 }
 #endif

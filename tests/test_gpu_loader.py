@@ -1,0 +1,148 @@
+"""The device loader (csrc/json_gpu.hip) against the host loader and the oracle.
+
+* arena parity: gg_loader_device_check builds the same documents with both loaders and compares
+  every node (kind, count, links, scalars, marks, string bytes, one pool entry per distinct string);
+* refusals: documents outside the device subset refuse the whole batch, so the caller loads it on
+  the host (a YAML document, duplicate keys, nesting past 64, a float beyond the exact fast path);
+* end to end: a session loaded on the device reports byte-identically to one loaded on the host,
+  and to the oracle.
+"""
+import json
+import os
+
+import pytest
+
+import guard_amd
+import synth
+from guard_oracle import validate_structured as oracle_validate
+from rulepack import rule_pack
+
+pytestmark = pytest.mark.gpu
+G = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _pack(d):
+    p = os.path.join(G, d)
+    return [(f, open(os.path.join(p, f)).read()) for f in sorted(os.listdir(p)) if f.endswith(".guard")]
+
+
+EDGE_DOCS = [
+    '{}', '[]', '  {\n  "a" : [ ] ,\n "b":{ } }\n', '[1, -2, 0, -0, 9223372036854775807, -9223372036854775808]',
+    '{"f": [1.5, -0.0, 0.1, 1e3, 2.5E-3, 123456789012345, 0.000123, 1e22, 1e-22, 100.25]}',
+    '{"s": ["", "x", "\\u00e9t\\u00e9", "\\u4e2d", "a\\"b\\\\c\\/d\\b\\f\\n\\r\\t", "\\u0041"], "": "", "e": ""}',
+    '{"Resources": {"r": {"Type": "T", "Properties": {"": 1, "Name": 2}}}}',
+    '[[[[[[[[[[{"deep": [true, false, null]}]]]]]]]]]]',
+    '{"k1": {"k1": {"k1": "k1"}}, "k2": ["k1", "k2", {"k2": "k1"}]}',
+]
+
+
+def _check(docs):
+    rc, msg = guard_amd.loader_device_check(docs)
+    assert rc == 1, msg
+
+
+def test_arena_parity_edge_documents():
+    _check(EDGE_DOCS)
+    for d in EDGE_DOCS:
+        _check([d])
+
+
+def test_arena_parity_corpora():
+    _check(synth.cfn_corpus(64, start=0, n_resources=30))
+    _check(synth.tf_corpus(8, start=5, n_resources=120))
+    _check(synth.config_corpus(16, start=3, n_groups=4))
+
+
+def test_arena_parity_pretty_printed():
+    """multi-line documents: line / column marks of keys and values"""
+    docs = [json.dumps(json.loads(d), indent=k) for k, d in
+            zip([1, 2, 4, 2, 3, 2], synth.cfn_corpus(6, start=40, n_resources=10))]
+    docs += [json.dumps(json.loads(d), indent=2) for d in synth.tf_corpus(2, start=9, n_resources=20)]
+    _check(docs)
+
+
+def test_arena_parity_fixture_json():
+    """the JSON fixtures the reference's tests hold (a test spec, structured reports): pretty-printed"""
+    paths = [os.path.join(G, "test-command", "s3_bucket_server_side_encryption_enabled.json"),
+             os.path.join(G, "validate", "structured.json"), os.path.join(G, "validate", "structured-payload.json")]
+    docs = [open(p).read() for p in paths]
+    good = [t for t in docs if guard_amd.loader_device_check([t])[0] == 1]
+    assert len(good) >= 2
+    _check(good)
+
+
+@pytest.mark.parametrize("doc,why", [
+    ("Resources:\n  a: 1\n", "subset"),
+    ('{"a": 1, "a": 2}', "duplicate"),
+    ("[" * 70 + "]" * 70, "deeper"),
+    ('{"x": 0.12345678901234567890}', "float"),
+    ('{"x": 1e400}', "float"),
+    ('{"x": 99999999999999999999}', "float"),
+    ('{"x": "café"}', "subset"),
+    ('{"x": 1}x', "subset"),
+])
+def test_refusals(doc, why):
+    rc, msg = guard_amd.loader_device_check(synth.cfn_corpus(3, n_resources=5) + [doc])
+    assert rc == -1
+    assert why in msg
+
+
+def _session(rules, texts, names, device):
+    s = guard_amd.Session()
+    for name, text in rules:
+        s.add_rules(text, name)
+    if device:
+        st = s.add_docs_device(texts, names)
+        assert st is not None and st["text_bytes"] == sum(len(t) for t in texts)
+    else:
+        s.add_docs(texts, names)
+    s.eval(1)
+    out = s.report()
+    s.close()
+    return out
+
+
+def test_session_device_load_matches_host_and_oracle():
+    rules = rule_pack()
+    texts = synth.cfn_corpus(40, start=500, n_resources=25)
+    names = ["t%d.json" % i for i in range(len(texts))]
+    dev = _session(rules, texts, names, True)
+    assert dev == _session(rules, texts, names, False)
+    exp, ecode, _ = oracle_validate(rules, list(zip(names, texts)))
+    assert dev == (exp, ecode)
+
+
+def test_session_device_load_workloads():
+    for texts, rules in ((synth.tf_corpus(6, start=11, n_resources=60), _pack("tf_rulepack")),
+                         (synth.config_corpus(10, start=21), _pack("net_rulepack")),
+                         (EDGE_DOCS[2:], _pack("edge_rulepack"))):
+        names = ["d%d.json" % i for i in range(len(texts))]
+        dev = _session(rules, texts, names, True)
+        assert dev == _session(rules, texts, names, False)
+
+
+def test_empty_key_does_not_alias_next_string():
+    """an empty string takes its own pool slot (before: "" and the next interned string shared an id)"""
+    rules = [("empty.guard", "rule names_two { Resources.*.Properties.Name == 2 }\n")]
+    data = [("e.json", EDGE_DOCS[6])]
+    exp, ecode, _ = oracle_validate(rules, data)
+    assert guard_amd.validate_structured(rules, data) == (exp, ecode)
+    assert _session(rules, [EDGE_DOCS[6]], ["e.json"], True) == (exp, ecode)
+
+
+def test_synthetic_device_matches_host():
+    rules = rule_pack()
+    a = guard_amd.Session()
+    b = guard_amd.Session()
+    for name, text in rules:
+        a.add_rules(text, name)
+        b.add_rules(text, name)
+    st = a.add_synthetic_device(1000, 300, n_resources=50)
+    assert st is not None and st["nodes"] == a.stat(2)
+    b.add_synthetic(1000, 300, n_resources=50)
+    assert a.stat(2) == b.stat(2)
+    a.eval(1)
+    b.eval(1)
+    assert a.report() == b.report()
+    a.close()
+    b.close()
