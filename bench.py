@@ -99,6 +99,8 @@ def main():
     ap.add_argument("--docs", type=int, default=1_000_000, help="templates per GPU")
     ap.add_argument("--resources", type=int, default=50)
     ap.add_argument("--threads", type=int, default=0, help="host loader threads (default: CPU share)")
+    ap.add_argument("--loader", choices=("host", "device"), default="host",
+                    help="document loader: host threads, or the MI355X JSON loader (csrc/json_gpu.hip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-per-core", type=int, default=600)
     args = ap.parse_args()
@@ -131,7 +133,14 @@ def main():
         sess.add_rules(text, name)
     t0 = time.time()
     first, count = sharding.shard_range(rank, world, args.docs)
-    sess.add_synthetic(first, count, n_resources=args.resources, threads=threads)
+    load_stats = None
+    if args.loader == "device":
+        load_stats = sess.add_synthetic_device(first, count, n_resources=args.resources, threads=threads)
+        if load_stats is None:
+            raise RuntimeError("device loader refused the synthetic corpus")
+        load_stats["text_GBps"] = round(load_stats["text_bytes"] / (load_stats["kernel_ms"] / 1e3) / 1e9, 2)
+    else:
+        sess.add_synthetic(first, count, n_resources=args.resources, threads=threads)
     t_load = time.time() - t0
     t0 = time.time()
     sess.upload()
@@ -205,7 +214,8 @@ def main():
                        "alg_bytes_per_launch": b_alg, "arena_bytes": arena, "record_bytes": rec_bytes,
                        "nodes": sess.stat(2), "pool_bytes": sess.stat(3),
                        "tiles_fail_pass_skip_err": [n_fail, n_pass, n_skip, n_err],
-                       "host_load_s": round(t_load, 2), "host_threads": threads, "upload_s": round(t_upload, 2),
+                       "loader": args.loader, "load_s": round(t_load, 2), "host_threads": threads,
+                       "upload_s": round(t_upload, 2), "device_loader": load_stats,
                        "rule_tallies_sum": int(sum(tally))},
         }
         line["cpu_baseline"] = cpu
