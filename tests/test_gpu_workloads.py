@@ -98,3 +98,31 @@ def test_cfg1_examples_cross_product_vs_oracle():
                 assert ecode == -1, (name, dn, e.message)
                 continue
             assert (out, code) == (exp, ecode), (name, dn)
+
+
+def test_sharded_sessions_merge_to_single_process_report():
+    """each rank reports its own documents; rank-order concatenation of the
+    per-shard reports (sharding.merge_reports, what gather_report does on rank 0) is the
+    single-process output.  Two sessions on one GPU stand in for two ranks."""
+    import sharding
+    from rulepack import rule_pack
+    rules = rule_pack()
+    texts = synth.cfn_corpus(24, start=100, n_resources=12)
+    names = ["synthetic-%d.json" % (100 + i) for i in range(len(texts))]
+    for fmt in ("json", "yaml"):
+        parts, codes = [], []
+        for lo, hi in ((0, 9), (9, 24)):
+            s = guard_amd.Session()
+            for name, text in rules:
+                s.add_rules(text, name)
+            s.add_docs(texts[lo:hi], names[lo:hi])
+            s.upload()
+            s.eval(1)
+            out, code = s.report(fmt)
+            s.close()
+            parts.append(out)
+            codes.append(code)
+        merged = sharding.merge_reports(parts, fmt)
+        exp, ecode, _ = oracle_validate(rules, list(zip(names, texts)), output=fmt)
+        assert merged == exp
+        assert max(codes, key=lambda c: sharding._SEVERITY[c]) == ecode

@@ -81,3 +81,61 @@ def test_two_rank_tally_reduction_matches_single_process():
         assert p.exitcode == 0
     assert reduced == _tallies(0, 2 * DOCS_PER_RANK).tolist()
     assert sum(reduced) == 2 * DOCS_PER_RANK * len(RULES)
+
+
+# ---- failure-record / report gather to rank 0 ----
+REPORT_DOCS = 3
+
+
+def _shard_report(first, n, output):
+    from guard_oracle import validate_structured
+    docs = [("synthetic-%d.json" % (first + i), t)
+            for i, t in enumerate(synth.cfn_corpus(n, start=first, n_resources=10))]
+    text, code, _ = validate_structured(RULES, docs, output=output)
+    return text, code
+
+
+def _report_worker(rank, world, port, q, codes):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = {}
+    for fmt in ("json", "yaml"):
+        first, n = sharding.shard_range(rank, world, REPORT_DOCS)
+        text, code = _shard_report(first, n, fmt)
+        out[fmt] = sharding.gather_report(text, code, dist, output=fmt)
+    # exit-code precedence with a different code on every rank
+    out["codes"] = [sharding.reduce_exit_code(c[rank], dist) for c in codes]
+    if rank == 0:
+        q.put(out)
+    else:
+        assert out["json"][0] is None and out["yaml"][0] is None
+    dist.destroy_process_group()
+
+
+def test_two_rank_report_gather_matches_single_process():
+    codes = [(0, 19), (5, 19), (19, 5), (0, 5), (0, 0), (-1, 19), (5, -1)]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_report_worker, args=(r, 2, port, q, codes)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for fmt in ("json", "yaml"):
+        full, code = _shard_report(0, 2 * REPORT_DOCS, fmt)
+        assert got[fmt] == (full, code)
+    assert got["codes"] == [19, 19, 19, 5, 0, -1, -1]
+
+
+def test_merge_reports_edge_cases():
+    assert sharding.merge_reports(["[]", "[]"]) == "[]"
+    assert sharding.merge_reports(["[]\n"], "yaml") == "[]\n"
+    assert sharding.merge_reports(["[\n  1\n]", "[]", "[\n  2\n]"]) == "[\n  1,\n  2\n]"
+    with pytest.raises(ValueError):
+        sharding.merge_reports(["{}"])
+    with pytest.raises(ValueError):
+        sharding.merge_reports(["x"], "sarif")
