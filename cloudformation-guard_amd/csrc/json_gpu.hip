@@ -25,6 +25,7 @@
 #include <chrono>
 #include <cstring>
 #include <stdexcept>
+#include <thread>
 
 namespace gg {
 namespace {
@@ -489,6 +490,86 @@ uint32_t grid_for(uint64_t items, uint32_t block) {
   return (uint32_t)std::min<uint64_t>((items + block - 1) / block, 65536ull);
 }
 
+// Host <-> device transfers of the loader's bulk arrays through two pinned bounce buffers: the
+// DMA of one chunk overlaps the host threads' copy of the other (hipMemcpy from / to pageable
+// memory stages through the runtime at a few GB/s, single threaded).
+struct Staging {
+  static constexpr size_t kChunk = 64ull << 20;
+  void* pin[2] = {nullptr, nullptr};
+  hipStream_t s = nullptr;
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  int threads = 1;
+  Staging() {
+    JCHK(hipHostMalloc(&pin[0], kChunk, hipHostMallocDefault));
+    JCHK(hipHostMalloc(&pin[1], kChunk, hipHostMallocDefault));
+    JCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    JCHK(hipEventCreateWithFlags(&ev[0], hipEventDisableTiming));
+    JCHK(hipEventCreateWithFlags(&ev[1], hipEventDisableTiming));
+    threads = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  }
+  ~Staging() {
+    if (s) { hipStreamSynchronize(s); hipStreamDestroy(s); }
+    for (int i = 0; i < 2; i++) { if (pin[i]) hipHostFree(pin[i]); if (ev[i]) hipEventDestroy(ev[i]); }
+  }
+  // fn(t, nthreads) on `threads` host threads
+  template <typename F>
+  void par(F fn) {
+    std::vector<std::thread> th;
+    for (int t = 1; t < threads; t++) th.emplace_back(fn, t, threads);
+    fn(0, threads);
+    for (auto& x : th) x.join();
+  }
+  void copy_par(void* dst, const void* src, size_t n) {
+    par([&](int t, int nt) {
+      size_t a = n * t / nt, b = n * (t + 1) / nt;
+      if (b > a) memcpy((char*)dst + a, (const char*)src + a, b - a);
+    });
+  }
+  void d2h(void* dst, const void* src, size_t bytes) {
+    const size_t nch = (bytes + kChunk - 1) / kChunk;
+    auto issue = [&](size_t i) {
+      const size_t o = i * kChunk, n = std::min(kChunk, bytes - o);
+      JCHK(hipMemcpyAsync(pin[i & 1], (const char*)src + o, n, hipMemcpyDeviceToHost, s));
+      JCHK(hipEventRecord(ev[i & 1], s));
+    };
+    if (nch) issue(0);
+    for (size_t i = 0; i < nch; i++) {
+      JCHK(hipEventSynchronize(ev[i & 1]));
+      if (i + 1 < nch) issue(i + 1);   // the other buffer: its chunk was copied out last iteration
+      const size_t o = i * kChunk;
+      copy_par((char*)dst + o, pin[i & 1], std::min(kChunk, bytes - o));
+    }
+  }
+  // documents packed back to back into device memory `dst` (offsets off[]), 16 zero bytes after
+  void h2d_docs(uint8_t* dst, const char* const* texts, const size_t* lens, const uint64_t* off, size_t n) {
+    const uint64_t total = off[n] + 16;
+    size_t doc = 0;
+    for (size_t i = 0; i * kChunk < total; i++) {
+      const uint64_t lo = i * kChunk, hi = std::min<uint64_t>(total, lo + kChunk);
+      if (i >= 2) JCHK(hipEventSynchronize(ev[i & 1]));   // this buffer's previous DMA is done
+      char* buf = (char*)pin[i & 1];
+      while (doc < n && off[doc + 1] <= lo) doc++;
+      const size_t d0 = doc;
+      par([&](int t, int nt) {
+        // bytes [lo, hi) of the packed stream, split by byte range over the threads
+        const uint64_t a = lo + (hi - lo) * t / nt, b = lo + (hi - lo) * (t + 1) / nt;
+        size_t d = d0;
+        while (d < n && off[d + 1] <= a) d++;
+        for (uint64_t p = a; p < b;) {
+          if (d >= n) { memset(buf + (p - lo), 0, b - p); break; }
+          const uint64_t e = std::min<uint64_t>(b, off[d + 1]);
+          memcpy(buf + (p - lo), texts[d] + (p - off[d]), e - p);
+          p = e;
+          d++;
+        }
+      });
+      JCHK(hipMemcpyAsync(dst + lo, buf, hi - lo, hipMemcpyHostToDevice, s));
+      JCHK(hipEventRecord(ev[i & 1], s));
+    }
+    JCHK(hipStreamSynchronize(s));
+  }
+};
+
 }  // namespace
 
 bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, const std::vector<std::string>& names,
@@ -506,9 +587,8 @@ bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, 
     off[k + 1] = off[k] + lens[k];
   }
   const uint64_t total = off[n];
-  std::vector<uint8_t> host(total + 16, 0);
-  for (size_t k = 0; k < n; k++) memcpy(host.data() + off[k], texts[k], lens[k]);
   st.text_bytes = total;
+  Staging stg;
 
   hipEvent_t e0, e1;
   JCHK(hipEventCreate(&e0));
@@ -516,10 +596,9 @@ bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, 
   auto t0 = std::chrono::steady_clock::now();
   DevArr<uint8_t> d_text; d_text.alloc(total + 16);
   DevArr<uint64_t> d_off; d_off.alloc(n + 1);
-  JCHK(hipMemcpy(d_text.p, host.data(), total + 16, hipMemcpyHostToDevice));
+  stg.h2d_docs(d_text.p, texts, lens, off.data(), n);
   JCHK(hipMemcpy(d_off.p, off.data(), (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice));
   st.h2d_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  std::vector<uint8_t>().swap(host);
 
   DevArr<uint32_t> d_nn, d_nc, d_ns, d_bad;
   d_nn.alloc(n); d_nc.alloc(n); d_ns.alloc(n); d_bad.alloc(1);
@@ -555,6 +634,15 @@ bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, 
     nbase[k] = N; cbase[k] = C;
     N += nn[k]; C += nc[k]; S += ns[k];
   }
+  // the host columns are sized (zero-filled: page faults, seconds at 1M documents) while the
+  // device passes run; one thread per column
+  std::thread resizer([&out, N]() {
+    std::thread a([&]() { out.nodes.resize(N); });
+    std::thread b([&]() { out.line.resize(N); out.col.resize(N); });
+    out.kline.resize(N); out.kcol.resize(N);
+    a.join(); b.join();
+  });
+  struct Joiner { std::thread& t; ~Joiner() { if (t.joinable()) t.join(); } } join_resizer{resizer};
   DevArr<uint64_t> d_nbase, d_cbase;
   d_nbase.alloc(n); d_cbase.alloc(n);
   JCHK(hipMemcpy(d_nbase.p, nbase.data(), n * 8, hipMemcpyHostToDevice));
@@ -593,20 +681,24 @@ bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, 
   st.kernel_ms = ms_total;
   JCHK(hipEventDestroy(e0));
   JCHK(hipEventDestroy(e1));
-  if (bad_now()) return false;
+  if (bad_now()) {
+    resizer.join();
+    out.clear();   // refused: the batch stays empty
+    return false;
+  }
 
   // results to the host batch (the host keeps the reporter's columns and the intern index)
   t0 = std::chrono::steady_clock::now();
   unsigned long long pool_used = 0;
   JCHK(hipMemcpy(&pool_used, d_pool_cursor.p, 8, hipMemcpyDeviceToHost));
-  out.nodes.resize(N); out.line.resize(N); out.col.resize(N); out.kline.resize(N); out.kcol.resize(N);
-  JCHK(hipMemcpy(out.nodes.data(), d_nodes.p, N * sizeof(DNode), hipMemcpyDeviceToHost));
-  JCHK(hipMemcpy(out.line.data(), d_line.p, N * 4, hipMemcpyDeviceToHost));
-  JCHK(hipMemcpy(out.col.data(), d_col.p, N * 4, hipMemcpyDeviceToHost));
-  JCHK(hipMemcpy(out.kline.data(), d_kline.p, N * 4, hipMemcpyDeviceToHost));
-  JCHK(hipMemcpy(out.kcol.data(), d_kcol.p, N * 4, hipMemcpyDeviceToHost));
+  resizer.join();
+  stg.d2h(out.nodes.data(), d_nodes.p, N * sizeof(DNode));
+  stg.d2h(out.line.data(), d_line.p, N * 4);
+  stg.d2h(out.col.data(), d_col.p, N * 4);
+  stg.d2h(out.kline.data(), d_kline.p, N * 4);
+  stg.d2h(out.kcol.data(), d_kcol.p, N * 4);
   out.bytes.resize(pool_used);
-  if (pool_used) JCHK(hipMemcpy(&out.bytes[0], d_pool.p, pool_used, hipMemcpyDeviceToHost));
+  if (pool_used) stg.d2h(&out.bytes[0], d_pool.p, pool_used);
   std::vector<unsigned long long> tkey(tslots);
   std::vector<uint32_t> tlen(tslots), tid(tslots);
   JCHK(hipMemcpy(tkey.data(), d_tkey.p, tslots * 8, hipMemcpyDeviceToHost));
