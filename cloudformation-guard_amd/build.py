@@ -44,6 +44,12 @@ def build(verbose=False, variant=""):
         flags = [f for f in flags if not f.startswith("-DGG_LANE_WAVES_PER_EU=")] + ["-DGG_LANE_WAVES_PER_EU=" + eu]
         if pw:
             flags.append("-DGG_LDS_PROG_WORDS=" + pw)
+    if variant == "iclause":       # call-structure experiments (eval_core.inc CLAUSE_FN / CONJ_FN)
+        flags.append("-DGG_INLINE_CLAUSE=1")
+    if variant == "iconj":
+        flags.append("-DGG_INLINE_CONJ=1")
+    if variant.startswith("g"):    # lane-heap interleave experiments: g<N> = 2^N bytes per lane per heap row
+        flags.append("-DGG_HEAP_GRAIN=" + variant[1:])
     os.makedirs(obj_dir, exist_ok=True)
     headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".h", ".inc"))]
     headers.append(os.path.join(HERE, "..", "include", "cfn_guard_mi355x.h"))

@@ -80,11 +80,16 @@ struct DeviceState {
   int ncu = 256;
   std::string error;
   hipStream_t stream = nullptr;
-  bool init(int dev) {
+  // One device per process (one process per GPU): the device current on the
+  // first calling thread -- torch.cuda.set_device(LOCAL_RANK) in a multi-GPU job -- or GG_DEVICE.
+  bool init() {
     if (ready) return true;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0) { error = "no HIP device available (the MI355X path has no CPU fallback)"; return false; }
-    if (dev >= n) dev = 0;
+    int dev = 0;
+    if (const char* e = getenv("GG_DEVICE")) dev = atoi(e);
+    else if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    if (dev < 0 || dev >= n) { error = "GG_DEVICE / current device out of range"; return false; }
     device = dev;
     if (hipSetDevice(dev) != hipSuccess) { error = "hipSetDevice failed"; return false; }
     hipDeviceProp_t prop;
@@ -247,7 +252,9 @@ namespace {
 
 bool ensure_device(std::string& why) {
   std::lock_guard<std::mutex> lk(g_dev.mu);
-  if (!g_dev.init(0)) { why = g_dev.error; return false; }
+  if (!g_dev.init()) { why = g_dev.error; return false; }
+  // the current device is per host thread: FFI callers may arrive on any thread
+  if (hipSetDevice(g_dev.device) != hipSuccess) { why = "hipSetDevice failed"; return false; }
   return true;
 }
 
@@ -893,12 +900,16 @@ int32_t gg_session_launch(gg_session* s, extern_err_t* err) {
 
 double gg_session_wait(gg_session* s, extern_err_t* err) {
   set_err(err, 0, "");
+  std::string why;
+  if (!ensure_device(why)) { set_err(err, -1, why); return -1; }
   try { return session_wait(s); } catch (std::exception& e) { set_err(err, -1, e.what()); return -1; }
 }
 
 int32_t gg_session_fetch(gg_session* s, extern_err_t* err) {
   set_err(err, 0, "");
   try {
+    std::string why;
+    if (!ensure_device(why)) { set_err(err, -1, why); return -1; }
     session_wait(s);
     if (session_records_wanted(s) > s->rec_cap) { set_err(err, -1, "record arena overflow: run gg_session_eval first"); return -1; }
     session_fetch(s);

@@ -4,6 +4,9 @@
  * guard-ffi/example/cfn_guard.h): same struct layouts, same error codes
  * (guard-ffi/src/errors.rs:12-38), same JSON bytes for non-verbose calls.
  * All entry points evaluate on the GPU; without a HIP device they fail with code -1.
+ * One device per process: the HIP device current on the thread of the first call (a multi-GPU
+ * job sets it per rank, e.g. torch.cuda.set_device(LOCAL_RANK)), or GG_DEVICE=<ordinal>.
+ * Later calls may come from any host thread.
  */
 #ifndef CFN_GUARD_MI355X_H
 #define CFN_GUARD_MI355X_H

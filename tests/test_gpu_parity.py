@@ -181,3 +181,16 @@ def test_output_formats_vs_oracle():
             exp, ecode, _ = oracle_validate(rules, data, output=fmt)
             out, code = guard_amd.validate_structured(rules, data, output=fmt)
             assert (out, code) == (exp, ecode), (fmt, rules[0][0])
+
+
+def test_device_selection_env_out_of_range_fails_loudly():
+    """One device per process: GG_DEVICE (or the caller's current device) picks it; an ordinal past
+    the visible devices is an error (-1), never a silent fallback to another device or the CPU."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r); import guard_amd\n"
+            "try:\n    guard_amd.validate_structured([('r.guard', 'Resources exists')], [('d.json', '{}')])\n"
+            "except guard_amd.GuardError as e:\n    print('ERR', e.code, e.message)\n") % os.path.dirname(guard_amd.__file__)
+    env = dict(os.environ, GG_DEVICE="999")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=120)
+    assert "ERR -1" in r.stdout and "out of range" in r.stdout, r.stdout + r.stderr
