@@ -103,6 +103,8 @@ def main():
                     help="document loader: host threads, or the MI355X JSON loader (csrc/json_gpu.hip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-per-core", type=int, default=600)
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL); gloo only to rehearse N ranks sharing one GPU (GG_BENCH_DEVICE)")
     args = ap.parse_args()
 
     import torch
@@ -121,8 +123,9 @@ def main():
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world)
-    torch.cuda.set_device(local)
+        dist.init_process_group(args.dist_backend, rank=rank, world_size=world)
+    # one GPU per rank; GG_BENCH_DEVICE pins every rank to one device (rehearsal on a 1-GPU box)
+    torch.cuda.set_device(int(os.environ.get("GG_BENCH_DEVICE", local)))
     if not guard_amd.device_available():
         raise RuntimeError("no HIP device: the MI355X evaluator has no CPU fallback")
 
@@ -145,7 +148,10 @@ def main():
     t0 = time.time()
     sess.upload()
     t_upload = time.time() - t0
-    stream = torch.cuda.current_stream()
+    # one non-default stream for the kernels AND the tally all-reduce: torch's default stream has
+    # handle 0, which the library reads as "its own stream" -- unordered with the collective
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
     sess.set_stream(stream.cuda_stream)
     counts = torch.zeros(max(1, sess.ncounts()), dtype=torch.int64, device="cuda")
     sess.bind_counts(counts.data_ptr(), sess.ncounts())
@@ -186,6 +192,7 @@ def main():
     k_mean_ms = sum(kms) / max(1, len(kms))
     achieved = b_alg / (k_mean_ms / 1e3) / 1e9
     tally = sess.counts()
+    tally_sum = int(counts.sum().item())   # the all-reduced tensor: every rank's last-step tallies
     n_fail, n_pass, n_skip, n_err = sess.stat(4), sess.stat(5), sess.stat(6), sess.stat(7)
 
     total_units = ntiles * world * args.steps
@@ -216,7 +223,7 @@ def main():
                        "tiles_fail_pass_skip_err": [n_fail, n_pass, n_skip, n_err],
                        "loader": args.loader, "load_s": round(t_load, 2), "host_threads": threads,
                        "upload_s": round(t_upload, 2), "device_loader": load_stats,
-                       "rule_tallies_sum": int(sum(tally))},
+                       "rule_tallies_sum": tally_sum, "rule_tallies_fetched": int(sum(tally))},
         }
         line["cpu_baseline"] = cpu
         print(json.dumps(line), flush=True)

@@ -1015,6 +1015,7 @@ static void load_stats(const GpuLoadStats& st, double* out) {
   if (!out) return;
   out[0] = st.kernel_ms; out[1] = (double)st.nodes; out[2] = (double)st.distinct_strings;
   out[3] = (double)st.pool_bytes; out[4] = (double)st.text_bytes; out[5] = st.h2d_ms; out[6] = st.d2h_ms;
+  out[7] = (double)st.table_retries;
 }
 
 int32_t gg_session_add_docs_device(gg_session* s, const char* const* texts, const size_t* lens, const char* const* names,

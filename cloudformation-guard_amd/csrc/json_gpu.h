@@ -18,6 +18,7 @@ struct GpuLoadStats {
   double kernel_ms = 0;        // parse + intern kernels (HIP events)
   double h2d_ms = 0, d2h_ms = 0;
   uint64_t text_bytes = 0, nodes = 0, distinct_strings = 0, pool_bytes = 0;
+  uint32_t table_retries = 0;   // intern-table doublings
 };
 
 // Appends `n` documents (texts[i] of lens[i] bytes, named names[i]) to the EMPTY batch `out`.

@@ -23,6 +23,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <thread>
@@ -483,7 +484,11 @@ struct DevArr {
   T* p = nullptr;
   size_t n = 0;
   ~DevArr() { if (p) hipFree(p); }
-  void alloc(size_t count) { n = count; JCHK(hipMalloc(&p, std::max<size_t>(count, 1) * sizeof(T))); }
+  void alloc(size_t count) {
+    if (p) { hipFree(p); p = nullptr; }
+    n = count;
+    JCHK(hipMalloc(&p, std::max<size_t>(count, 1) * sizeof(T)));
+  }
 };
 
 uint32_t grid_for(uint64_t items, uint32_t block) {
@@ -651,33 +656,60 @@ bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, 
   DevArr<DNode> d_nodes; d_nodes.alloc(N);
   DevArr<uint32_t> d_line, d_col, d_kline, d_kcol;
   d_line.alloc(N); d_col.alloc(N); d_kline.alloc(N); d_kcol.alloc(N);
-  // intern table: 2 slots per string occurrence, between 2^16 and 2^26 slots
+  // Intern table: 2 slots per string occurrence, between 2^16 and 2^23 slots to start with (at
+  // most 64 MB of keys, so the probes hit the L2 / Infinity Cache instead of HBM: templates repeat
+  // their keys and values, distinct strings are a few per cent of the occurrences).  A full table
+  // doubles and the table passes run again, up to 2 slots per occurrence or 2^28 slots.
+  uint32_t start_log = 23;
+  if (const char* e = getenv("GG_JSON_TABLE_LOG")) start_log = (uint32_t)std::max(16, std::min(28, atoi(e)));   // tests
   uint64_t tslots = 1ull << 16;
-  while (tslots < 2 * S && tslots < (1ull << 26)) tslots <<= 1;
+  while (tslots < 2 * S && tslots < (1ull << start_log)) tslots <<= 1;
   DevArr<unsigned long long> d_tkey, d_towner, d_pool_cursor;
   DevArr<uint32_t> d_tlen, d_tid;
-  d_tkey.alloc(tslots); d_towner.alloc(tslots); d_tlen.alloc(tslots); d_tid.alloc(tslots); d_pool_cursor.alloc(1);
-  JCHK(hipMemset(d_tkey.p, 0, tslots * 8));
-  JCHK(hipMemset(d_pool_cursor.p, 0, 8));
-  const uint64_t pool_cap = std::min<uint64_t>(std::max<uint64_t>(total / 4, 1ull << 20), 0xF0000000ull);
-  DevArr<uint8_t> d_pool; d_pool.alloc(pool_cap + 16);
-  JCHK(hipMemset(d_pool.p, 0, pool_cap + 16));
+  d_pool_cursor.alloc(1);
+  // pool: a quarter of the text to start with (templates repeat their strings); doubles when full,
+  // up to the bound every distinct string fits in (its bytes + 16 of alignment padding)
+  const uint64_t pool_max = std::min<uint64_t>(total + 16 * S + 16, 0xF0000000ull);
+  uint64_t pool_cap = std::min<uint64_t>(std::max<uint64_t>(total / 4, 1ull << 20), pool_max);
+  DevArr<uint8_t> d_pool;
   A.node_base = d_nbase.p; A.cont_base = d_cbase.p; A.counts = d_counts.p; A.nodes = d_nodes.p;
   A.line = d_line.p; A.col = d_col.p; A.kline = d_kline.p; A.kcol = d_kcol.p;
-  A.tkey = d_tkey.p; A.tlen = d_tlen.p; A.towner = d_towner.p; A.tid = d_tid.p; A.tmask = tslots - 1;
-  A.pool = d_pool.p; A.pool_cursor = d_pool_cursor.p; A.pool_cap = pool_cap;
+  for (;;) {
+    if (d_pool.n != pool_cap + 16) d_pool.alloc(pool_cap + 16);
+    A.pool = d_pool.p; A.pool_cursor = d_pool_cursor.p; A.pool_cap = pool_cap;
+    d_tkey.alloc(tslots); d_towner.alloc(tslots); d_tlen.alloc(tslots); d_tid.alloc(tslots);
+    JCHK(hipMemset(d_tkey.p, 0, tslots * 8));
+    JCHK(hipMemset(d_pool_cursor.p, 0, 8));
+    JCHK(hipMemset(d_pool.p, 0, pool_cap + 16));
+    A.tkey = d_tkey.p; A.tlen = d_tlen.p; A.towner = d_towner.p; A.tid = d_tid.p; A.tmask = tslots - 1;
 
-  // 2. counts, 3. emit, 4. own, 5. fix, 6. verify
-  JCHK(hipEventRecord(e0));
-  hipLaunchKernelGGL(json_pass_kernel<M_COUNTS>, dim3(dgrid), dim3(256), 0, 0, A);
-  hipLaunchKernelGGL(json_pass_kernel<M_EMIT>, dim3(dgrid), dim3(256), 0, 0, A);
-  hipLaunchKernelGGL(json_own_kernel, dim3(grid_for(tslots, 256)), dim3(256), 0, 0, A);
-  hipLaunchKernelGGL(json_fix_kernel, dim3(grid_for(N, 256)), dim3(256), 0, 0, A, N);
-  hipLaunchKernelGGL(json_pass_kernel<M_VERIFY>, dim3(dgrid), dim3(256), 0, 0, A);
-  JCHK(hipGetLastError());
-  JCHK(hipEventRecord(e1));
-  JCHK(hipEventSynchronize(e1));
-  JCHK(hipEventElapsedTime(&ms, e0, e1)); ms_total += ms;
+    // 2. counts, 3. emit, 4. own, 5. fix, 6. verify
+    JCHK(hipEventRecord(e0));
+    hipLaunchKernelGGL(json_pass_kernel<M_COUNTS>, dim3(dgrid), dim3(256), 0, 0, A);
+    hipLaunchKernelGGL(json_pass_kernel<M_EMIT>, dim3(dgrid), dim3(256), 0, 0, A);
+    hipLaunchKernelGGL(json_own_kernel, dim3(grid_for(tslots, 256)), dim3(256), 0, 0, A);
+    hipLaunchKernelGGL(json_fix_kernel, dim3(grid_for(N, 256)), dim3(256), 0, 0, A, N);
+    hipLaunchKernelGGL(json_pass_kernel<M_VERIFY>, dim3(dgrid), dim3(256), 0, 0, A);
+    JCHK(hipGetLastError());
+    JCHK(hipEventRecord(e1));
+    JCHK(hipEventSynchronize(e1));
+    JCHK(hipEventElapsedTime(&ms, e0, e1)); ms_total += ms;
+    uint32_t b = 0;
+    JCHK(hipMemcpy(&b, d_bad.p, 4, hipMemcpyDeviceToHost));
+    if (b == BAD_TABLE && tslots < 2 * S && tslots < (1ull << 28)) {
+      tslots <<= 1;
+      JCHK(hipMemset(d_bad.p, 0, 4));
+      st.table_retries++;
+      continue;
+    }
+    if (b == BAD_POOL && pool_cap < pool_max) {
+      pool_cap = std::min<uint64_t>(pool_cap * 2, pool_max);
+      JCHK(hipMemset(d_bad.p, 0, 4));
+      st.table_retries++;
+      continue;
+    }
+    break;
+  }
   st.kernel_ms = ms_total;
   JCHK(hipEventDestroy(e0));
   JCHK(hipEventDestroy(e1));

@@ -109,7 +109,7 @@ def lib():
     return L
 
 
-LOAD_STATS = ("kernel_ms", "nodes", "distinct_strings", "pool_bytes", "text_bytes", "h2d_ms", "d2h_ms")
+LOAD_STATS = ("kernel_ms", "nodes", "distinct_strings", "pool_bytes", "text_bytes", "h2d_ms", "d2h_ms", "table_retries")
 
 
 def _load_result(rc, err, st):

@@ -80,7 +80,8 @@ int32_t gg_session_tile_status(gg_session *s, uint8_t *out, size_t n);
 double gg_session_last_kernel_ms(gg_session *s);
 int32_t gg_device_available(void);
 
-/* Asynchronous evaluation on a caller stream (bench.py passes torch's current stream). */
+/* Asynchronous evaluation on a caller stream (bench.py passes a non-default torch stream).  NULL
+ * selects the library's own non-blocking stream -- the legacy default stream cannot be named. */
 void gg_session_set_stream(gg_session *s, void *hip_stream);
 /* mode 0 (default): one tile per lane, tiles that outgrow the lane heap re-run one tile per
  * wavefront; mode 1: one tile per wavefront for every tile.  lane_heap_bytes 0 keeps 64 KB. */
@@ -115,8 +116,8 @@ int32_t gg_session_add_synthetic(gg_session *s, uint64_t first, size_t n, int32_
  * guard/src/rules/path_value.rs:414-478, as called from validate.rs:760-787).  Parses and interns
  * the documents on the MI355X into an EMPTY session, building the arena gg_session_add_docs builds.
  * Returns 0 when loaded, 1 when some document is outside the device subset (nothing loaded, err->message
- * says why; load the batch with gg_session_add_docs), -1 on error.  stats (may be NULL, 7 doubles):
- * kernel ms, nodes, distinct strings, pool bytes, text bytes, H2D ms, D2H ms. */
+ * says why; load the batch with gg_session_add_docs), -1 on error.  stats (may be NULL, 8 doubles):
+ * kernel ms, nodes, distinct strings, pool bytes, text bytes, H2D ms, D2H ms, intern-table doublings. */
 int32_t gg_session_add_docs_device(gg_session *s, const char *const *texts, const size_t *lens, const char *const *names,
                                    size_t n, double *stats, extern_err_t *err);
 int32_t gg_session_add_synthetic_device(gg_session *s, uint64_t first, size_t n, int32_t n_resources, int32_t nthreads,

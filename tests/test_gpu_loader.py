@@ -146,3 +146,15 @@ def test_synthetic_device_matches_host():
     assert a.report() == b.report()
     a.close()
     b.close()
+
+
+def test_intern_table_doubles_when_full(monkeypatch):
+    """The device intern table starts small (cache-resident probes) and doubles when a batch has
+    more distinct strings than it holds; the arena is still the host loader's."""
+    monkeypatch.setenv("GG_JSON_TABLE_LOG", "16")
+    docs = ['{"k%d": ["%s"]}' % (i, '", "'.join("v%d-%d" % (i, j) for j in range(60))) for i in range(1500)]
+    _check(docs)
+    s = guard_amd.Session()
+    st = s.add_docs_device(docs, ["d%d.json" % i for i in range(len(docs))])
+    s.close()
+    assert st is not None and st["table_retries"] >= 1 and st["distinct_strings"] == 1500 * 61
