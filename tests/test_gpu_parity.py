@@ -194,3 +194,21 @@ def test_device_selection_env_out_of_range_fails_loudly():
     env = dict(os.environ, GG_DEVICE="999")
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=120)
     assert "ERR -1" in r.stdout and "out of range" in r.stdout, r.stdout + r.stderr
+
+
+def test_reference_validate_resources_vs_oracle():
+    """The reference's validate test resources (template without Resources at the root, a key with
+    '/', comments, DB port rule, count() with and without messages, malformed / empty inputs) in
+    every structured format: byte-identical to the oracle, same exit code; aborting inputs raise."""
+    cases = json.load(open(os.path.join(G, "validate_cases.json")))
+    for c in cases:
+        rules = [tuple(x) for x in c["rules"]]
+        data = [tuple(x) for x in c["data"]]
+        for fmt in ("json", "yaml", "sarif", "junit"):
+            exp, ecode, err = oracle_validate(rules, data, output=fmt)
+            if ecode == -1:
+                with pytest.raises(guard_amd.GuardError):
+                    guard_amd.validate_structured(rules, data, output=fmt)
+                continue
+            out, code = guard_amd.validate_structured(rules, data, output=fmt)
+            assert (code, out) == (ecode, exp), (c["source"], fmt)
