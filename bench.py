@@ -34,7 +34,7 @@ sys.path.insert(0, os.path.join(ROOT, "cloudformation-guard_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E (MI355X_MICROARCH.md)
-DNODE_BYTES = 32
+DNODE_BYTES = 16          # packed device node (guard_types.h DNodeP)
 TILEOUT_BYTES = 32
 REC_BYTES = 48
 

@@ -33,6 +33,7 @@ namespace gg {
 __global__ void guard_eval_kernel(LaunchArgs A);
 __global__ void guard_eval_lanes_kernel(LaunchArgs A);
 __global__ void resource_type_kernel(DevBatch D);
+__global__ void pack_nodes_kernel(const DNode* in, DNodeP* out, uint32_t* klen, uint64_t n, uint32_t* bad);
 __global__ void rule_count_kernel(const TileOut* tiles, const uint8_t* rule_status, const DevProg* progs, uint32_t nfiles,
                                   uint32_t ntiles, uint32_t max_top, unsigned long long* counts);
 }
@@ -200,7 +201,8 @@ struct gg_session {
   std::vector<std::unique_ptr<GpuProgram>> progs;
   std::vector<std::string> parse_errors;   // rules files that failed to parse (exit code 5)
   // device residency
-  DBuf<DNode> d_nodes;
+  DBuf<DNodeP> d_nodes;         // packed device arena
+  DBuf<uint32_t> d_klen;        // per node key length (cold)
   DBuf<char> d_bytes;
   DBuf<uint32_t> d_roots;
   DBuf<uint64_t> d_base;
@@ -260,7 +262,27 @@ bool ensure_device(std::string& why) {
 
 void session_upload(gg_session* s) {
   hipStream_t st = g_dev.stream;
-  s->d_nodes.upload(s->docs.nodes.data(), s->docs.nodes.size(), st);
+  {
+    // host arena (32 B nodes) -> device arena (16 B packed nodes + key-length column)
+    const size_t n = s->docs.nodes.size();
+    DBuf<DNode> tmp;
+    tmp.upload(s->docs.nodes.data(), n, st);
+    s->d_nodes.alloc(std::max<size_t>(n, 1));
+    s->d_klen.alloc(std::max<size_t>(n, 1));
+    DBuf<uint32_t> bad;
+    bad.alloc(1);
+    HIPCHK(hipMemsetAsync(bad.p, 0, 4, st));
+    if (n) {
+      const uint32_t blocks = (uint32_t)std::min<size_t>((n + 255) / 256, (size_t)g_dev.ncu * 64);
+      hipLaunchKernelGGL(pack_nodes_kernel, dim3(blocks), dim3(256), 0, st, tmp.p, s->d_nodes.p, s->d_klen.p, (uint64_t)n, bad.p);
+      HIPCHK(hipGetLastError());
+    }
+    uint32_t b = 0;
+    HIPCHK(hipMemcpyAsync(&b, bad.p, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (b & 1u) throw std::runtime_error("a string or container is too large for the device arena (count >= 2^28)");
+    if (b & 2u) throw std::runtime_error("arena invariant broken: a map entry's key offset is not its key id");
+  }
   s->d_bytes.upload(s->docs.bytes.data(), s->docs.bytes.size() ? s->docs.bytes.size() : 1, st);
   s->d_roots.upload(s->docs.roots.data(), s->docs.roots.size(), st);
   s->d_base.upload(s->docs.base.data(), s->docs.base.size(), st);
@@ -343,7 +365,7 @@ void session_launch(gg_session* s) {
   unsigned long long* counts = s->ext_counts ? s->ext_counts : s->d_counts.p;
   HIPCHK(hipMemsetAsync(counts, 0, s->ncounts * sizeof(unsigned long long), st));
   LaunchArgs A{};
-  A.docs.nodes = s->d_nodes.p; A.docs.bytes = s->d_bytes.p; A.docs.roots = s->d_roots.p; A.docs.base = s->d_base.p; A.docs.ndocs = (uint32_t)s->docs.ndocs();
+  A.docs.nodes = s->d_nodes.p; A.docs.klen = s->d_klen.p; A.docs.bytes = s->d_bytes.p; A.docs.roots = s->d_roots.p; A.docs.base = s->d_base.p; A.docs.ndocs = (uint32_t)s->docs.ndocs();
   A.docs.res_map = s->d_res_map.p; A.docs.tix_off = s->d_tix_off.p; A.docs.tix = s->d_tix.p; A.docs.type_key = s->type_key;
   A.progs = s->d_progs.p; A.nfiles = (uint32_t)s->progs.size();
   A.ntiles = ntiles; A.tile_base = 0;
@@ -1162,7 +1184,7 @@ int64_t gg_session_stat(gg_session* s, int32_t what) {
     }
     case 7: { int64_t c = 0; for (auto& t : s->tiles) if (t.err) c++; return c; }
     case 8: return (int64_t)s->recs.size();
-    case 9: return (int64_t)(s->docs.nodes.size() * sizeof(DNode) + s->docs.bytes.size() + s->docs.roots.size() * 12);
+    case 9: return (int64_t)(s->docs.nodes.size() * sizeof(DNodeP) + s->docs.bytes.size() + s->docs.roots.size() * 12);
     case 10: for (auto& t : s->tiles) if (t.err) return t.err; return 0;
     case 11: return (int64_t)s->recs.size() * (int64_t)sizeof(Rec);
     case 12: return (int64_t)s->rec_cap;

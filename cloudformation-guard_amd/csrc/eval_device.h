@@ -39,7 +39,8 @@ struct DevProg {
 };
 
 struct DevBatch {
-  const DNode* nodes;
+  const DNodeP* nodes;     // packed device arena (guard_types.h DNodeP)
+  const uint32_t* klen;    // per node: DNode.key_len (cold column)
   const char* bytes;
   const uint32_t* roots;   // per doc: root node (document-relative)
   const uint64_t* base;    // per doc: global index of the document's first node

@@ -74,7 +74,7 @@ template <typename CtxT>
 __device__ __attribute__((always_inline)) inline void tile_begin(CtxT& c, const LaunchArgs& A, const DevProg* P,
                                                                  uint32_t doc, uint8_t* heap, uint32_t heap_bytes,
                                                                  uint32_t frames_bytes, uint32_t recs_bytes) {
-  c.P = (decltype(c.P))P; c.dn = A.docs.nodes + A.docs.base[doc]; c.db = A.docs.bytes; c.heap = heap; c.cap = heap_bytes;
+  c.P = (decltype(c.P))P; c.dn = A.docs.nodes + A.docs.base[doc]; c.kl = A.docs.klen + A.docs.base[doc]; c.db = A.docs.bytes; c.heap = heap; c.cap = heap_bytes;
   c.tmp = frames_bytes + recs_bytes; c.pers = heap_bytes; c.fcap = frames_bytes; c.rcap = recs_bytes; c.nframes = 0; c.nrec = 0;
   c.err = 0; c.err_a = 0; c.err_b = 0; c.suppress = 0; c.rec_created = 0; c.depth = 0; c.nsyn = 0;
   c.resmap = A.docs.res_map ? A.docs.res_map[doc] : NONE;
@@ -250,17 +250,18 @@ __global__ void __launch_bounds__(256) resource_type_kernel(DevBatch D) {
   for (uint32_t d = wave; d < D.ndocs; d += nwaves) {
     const uint32_t rm = D.res_map[d];
     if (rm == NONE) continue;
-    const DNode* dn = D.nodes + D.base[d];
-    const DNode m = dn[rm];
+    const DNodeP* dn = D.nodes + D.base[d];
+    const DNodeP m = dn[rm];
     uint32_t* out = D.tix + D.tix_off[d];
-    for (uint32_t j = lane; j < m.count; j += 64u) {
-      const DNode r = dn[m.a + j];
+    for (uint32_t j = lane; j < (m.kc >> 4); j += 64u) {
+      const DNodeP r = dn[m.a + j];
       uint32_t v = TIX_UNDECIDED;
-      if (r.kind == K_MAP) {
-        for (uint32_t k = 0; k < r.count; k++) {
-          const DNode e = dn[r.a + k];
+      if ((r.kc & 15u) == K_MAP) {
+        for (uint32_t k = 0; k < (r.kc >> 4); k++) {
+          const DNodeP e = dn[r.a + k];
           if (e.key_hash != D.type_key) continue;
-          v = e.kind == K_STRING ? e.b : (e.kind == K_LIST ? TIX_UNDECIDED : TIX_NOT_STRING);
+          const uint32_t ek = e.kc & 15u;
+          v = ek == K_STRING ? e.b : (ek == K_LIST ? TIX_UNDECIDED : TIX_NOT_STRING);
           break;
         }
       }
@@ -293,6 +294,21 @@ __global__ void __launch_bounds__(256) rule_count_kernel(const TileOut* tiles, c
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < ncount; i += blockDim.x)
     if (lds_counts[i]) atomicAdd(&counts[i], (unsigned long long)lds_counts[i]);
+}
+
+// Packs the host arena (32 B DNode) into the device arena (16 B DNodeP + key-length column).
+// bad[0] = 1: a count past 2^28; 2: a map entry whose key offset is not its key id.
+__global__ void __launch_bounds__(256) pack_nodes_kernel(const DNode* in, DNodeP* out, uint32_t* klen, uint64_t n,
+                                                         uint32_t* bad) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const DNode d = in[i];
+    if (d.count > kMaxPackedCount) atomicOr(bad, 1u);
+    if (d.key_off != NONE && d.key_off != d.key_hash) atomicOr(bad, 2u);
+    DNodeP p;
+    p.kc = d.kind | (d.count << 4); p.a = d.a; p.b = d.b; p.key_hash = d.key_off != NONE ? d.key_hash : 0u;
+    out[i] = p;
+    klen[i] = d.key_off != NONE ? d.key_len : 0u;
+  }
 }
 
 }  // namespace gg

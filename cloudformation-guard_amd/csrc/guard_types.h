@@ -41,6 +41,17 @@ struct DNode {
   uint32_t parent;   // parent node (NONE for a root); host uses it to rebuild JSON pointers
 };
 
+// Device arena node (16 B): what the evaluator reads of a DNode, half its size so a map's entries
+// and a key scan's batch share fewer cache lines.  kc = kind | count << 4 (count < 2^28); a, b as in
+// DNode; key_hash = the key id of a map entry (DNode.key_hash == DNode.key_off for document nodes;
+// 0 for other nodes).  DNode.key_len lives in a separate cold column (read only when a map key is
+// used as a value); DNode.parent and the marks stay on the host.  Built from the host arena at
+// upload by pack_nodes_kernel.
+struct DNodeP {
+  uint32_t kc, a, b, key_hash;
+};
+static const uint32_t kMaxPackedCount = (1u << 28) - 1;
+
 struct DRange {      // RangeType<T> (values.rs:232-278)
   uint64_t lo, hi;   // i64 / f64 bits / char code point
   uint32_t incl;     // LOWER_INCLUSIVE=1 | UPPER_INCLUSIVE=2
