@@ -26,6 +26,18 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", "-I" + YAML_INC, "-Wno-unused-result",
          "-DGG_LANE_WAVES_PER_EU=" + LANE_WAVES_PER_EU]
 
 
+# per-source flags of a variant: (variant, source) -> extra flags
+SRC_FLAGS = {
+    # MachineLICM hoists loop-invariant immediates (the constant fields of a failure record) out of
+    # the interpreter loops into callee-saved VGPRs, which every call then saves to scratch
+    # (product default, 99.7 -> 95.8 ms per launch A/B'd on one box)
+    ("", "eval_kernel.hip"): ["-mllvm", "-disable-machine-licm"],
+    ("stats", "eval_kernel.hip"): ["-mllvm", "-disable-machine-licm"],
+    # A/B baseline: MachineLICM on
+    ("licm", "eval_kernel.hip"): [],
+}
+
+
 def _needs(src, obj, deps):
     if not os.path.exists(obj):
         return True
@@ -58,7 +70,7 @@ def build(verbose=False, variant=""):
         src = os.path.join(CSRC, s)
         obj = os.path.join(obj_dir, s.replace(".cpp", ".o").replace(".hip", ".o"))
         if _needs(src, obj, headers):
-            cmd = [HIPCC, "--offload-arch=gfx950"] + flags + ["-c", src, "-o", obj]
+            cmd = [HIPCC, "--offload-arch=gfx950"] + flags + SRC_FLAGS.get((variant, s), []) + ["-c", src, "-o", obj]
             jobs.append((s, cmd))
 
     def run(job):
