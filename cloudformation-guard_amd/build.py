@@ -30,11 +30,15 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", "-I" + YAML_INC, "-Wno-unused-result",
 SRC_FLAGS = {
     # MachineLICM hoists loop-invariant immediates (the constant fields of a failure record) out of
     # the interpreter loops into callee-saved VGPRs, which every call then saves to scratch
-    # (product default, 99.7 -> 95.8 ms per launch A/B'd on one box)
-    ("", "eval_kernel.hip"): ["-mllvm", "-disable-machine-licm"],
-    ("stats", "eval_kernel.hip"): ["-mllvm", "-disable-machine-licm"],
+    # (product default, 99.7 -> 95.8 ms per launch A/B'd on one box); -O2 instead of -O3 for the
+    # evaluator: 96.2 -> 94.6 ms (-fno-unroll-loops: 124.9 ms)
+    ("", "eval_kernel.hip"): ["-mllvm", "-disable-machine-licm", "-O2"],
+    ("stats", "eval_kernel.hip"): ["-mllvm", "-disable-machine-licm", "-O2"],
     # A/B baseline: MachineLICM on
     ("licm", "eval_kernel.hip"): [],
+    # codegen experiments on top of the product flags
+    ("nounroll", "eval_kernel.hip"): ["-mllvm", "-disable-machine-licm", "-fno-unroll-loops"],
+    ("o2", "eval_kernel.hip"): ["-mllvm", "-disable-machine-licm", "-O2"],
 }
 
 
