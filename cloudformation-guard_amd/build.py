@@ -39,6 +39,12 @@ SRC_FLAGS = {
     # codegen experiments on top of the product flags
     ("nounroll", "eval_kernel.hip"): ["-mllvm", "-disable-machine-licm", "-fno-unroll-loops"],
     ("o2", "eval_kernel.hip"): ["-mllvm", "-disable-machine-licm", "-O2"],
+    # register-allocation experiments around device calls (callee-saved VGPRs go to scratch)
+    ("ipra", "eval_kernel.hip"): ["-mllvm", "-disable-machine-licm", "-O2", "-mllvm", "-enable-ipra"],
+    ("csr8", "eval_kernel.hip"): ["-mllvm", "-disable-machine-licm", "-O2",
+                                  "-mllvm", "-regalloc-csr-first-time-cost=8"],
+    ("csr64", "eval_kernel.hip"): ["-mllvm", "-disable-machine-licm", "-O2",
+                                   "-mllvm", "-regalloc-csr-first-time-cost=64"],
 }
 
 
