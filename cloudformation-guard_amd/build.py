@@ -26,7 +26,8 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", "-I" + YAML_INC, "-Wno-unused-result",
          "-DGG_LANE_WAVES_PER_EU=" + LANE_WAVES_PER_EU]
 
 
-# per-source flags of a variant: (variant, source) -> extra flags
+# per-source flags of a variant: (variant, source) -> extra flags (a variant not listed for a source
+# gets the product flags of that source)
 SRC_FLAGS = {
     # MachineLICM hoists loop-invariant immediates (the constant fields of a failure record) out of
     # the interpreter loops into callee-saved VGPRs, which every call then saves to scratch
@@ -70,6 +71,10 @@ def build(verbose=False, variant=""):
         flags.append("-DGG_INLINE_CLAUSE=1")
     if variant == "iconj":
         flags.append("-DGG_INLINE_CONJ=1")
+    if variant.startswith("cpad"):  # Ctx LDS stride experiments: cpad<N> = N pad dwords, cpack<N> = 4 B aligned + N pad dwords
+        flags.append("-DGG_CTX_PAD=" + variant[4:])
+    if variant.startswith("cpack"):
+        flags += ["-DGG_CTX_PACK=1", "-DGG_CTX_PAD=" + variant[5:]]
     if variant.startswith("g"):    # lane-heap interleave experiments: g<N> = 2^N bytes per lane per heap row
         flags.append("-DGG_HEAP_GRAIN=" + variant[1:])
     os.makedirs(obj_dir, exist_ok=True)
@@ -80,7 +85,7 @@ def build(verbose=False, variant=""):
         src = os.path.join(CSRC, s)
         obj = os.path.join(obj_dir, s.replace(".cpp", ".o").replace(".hip", ".o"))
         if _needs(src, obj, headers):
-            cmd = [HIPCC, "--offload-arch=gfx950"] + flags + SRC_FLAGS.get((variant, s), []) + ["-c", src, "-o", obj]
+            cmd = [HIPCC, "--offload-arch=gfx950"] + flags + SRC_FLAGS.get((variant, s), SRC_FLAGS.get(("", s), [])) + ["-c", src, "-o", obj]
             jobs.append((s, cmd))
 
     def run(job):
