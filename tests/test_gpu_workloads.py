@@ -80,6 +80,14 @@ def test_container_equality_vs_oracle():
     _vs_oracle(synth.cfn_corpus(16, start=300, n_resources=20), _pack("edge_rulepack"), "doc")
 
 
+def test_case_converter_queries_vs_oracle():
+    # lower-case / snake-case queries over PascalCase templates resolve through the cruet
+    # converters (eval_context.rs:539-568); the first document is the one of the reference's
+    # test_with_converter (eval_context_tests.rs:407-452)
+    from test_oracle_cruet import DOC
+    _vs_oracle([DOC] + synth.cfn_corpus(6, start=500, n_resources=12), _pack("conv_rulepack"), "conv")
+
+
 def test_cfg1_examples_cross_product_vs_oracle():
     """BASELINE.json configs[0] (the CPU-runnable plumbing case): every guard-examples rules file the
     reference's own test specs use x every template of guard/resources/validate/data-dir, each
