@@ -46,6 +46,11 @@ SRC_FLAGS = {
                                   "-mllvm", "-regalloc-csr-first-time-cost=8"],
     ("csr64", "eval_kernel.hip"): ["-mllvm", "-disable-machine-licm", "-O2",
                                    "-mllvm", "-regalloc-csr-first-time-cost=64"],
+    # machine-scheduler / wave-priority experiments
+    ("silp", "eval_kernel.hip"): ["-mllvm", "-disable-machine-licm", "-O2", "-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+    ("smem", "eval_kernel.hip"): ["-mllvm", "-disable-machine-licm", "-O2",
+                                  "-mllvm", "-amdgpu-sched-strategy=max-memory-clause"],
+    ("wprio", "eval_kernel.hip"): ["-mllvm", "-disable-machine-licm", "-O2", "-mllvm", "-amdgpu-set-wave-priority"],
 }
 
 
