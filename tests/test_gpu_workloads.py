@@ -88,6 +88,12 @@ def test_case_converter_queries_vs_oracle():
     _vs_oracle([DOC] + synth.cfn_corpus(6, start=500, n_resources=12), _pack("conv_rulepack"), "conv")
 
 
+def test_operator_coverage_vs_oracle():
+    # ranges, string ordering, regex ==/!=, !in with a custom message, `some` lets, list and map
+    # equality, a named-rule `when` with `not` (tests/golden/ops_rulepack)
+    _vs_oracle(synth.cfn_corpus(8, start=700, n_resources=15), _pack("ops_rulepack"), "ops")
+
+
 def test_cfg1_examples_cross_product_vs_oracle():
     """BASELINE.json configs[0] (the CPU-runnable plumbing case): every guard-examples rules file the
     reference's own test specs use x every template of guard/resources/validate/data-dir, each
