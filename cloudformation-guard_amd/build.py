@@ -2,8 +2,14 @@
 
 The library holds the host loader/compiler/reporter (C++) and the HIP evaluation kernel; it
 links libyaml 0.2.5 (the reference's YAML engine, via unsafe-libyaml) from /opt/conda/lib.
+
+Variants: "" = the product library; "stats" = diagnostic build with evaluator counters
+(libcfnguard_mi355x_stats.so, loaded only when GG_LIB points at it); "ab" = an A/B build of the
+product sources with extra compile flags from $GG_AB_FLAGS (libcfnguard_mi355x_ab.so).  Every
+object records the exact command that produced it (<obj>.cmd), so a flag change rebuilds it.
 """
 import os
+import shlex
 import shutil
 import subprocess
 import sys
@@ -25,90 +31,70 @@ LANE_WAVES_PER_EU = os.environ.get("GG_LANE_WAVES_PER_EU", "2")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-I" + YAML_INC, "-Wno-unused-result",
          "-DGG_LANE_WAVES_PER_EU=" + LANE_WAVES_PER_EU]
 
-
-# per-source flags of a variant: (variant, source) -> extra flags (a variant not listed for a source
-# gets the product flags of that source)
+# Per-source product flags.  MachineLICM hoists loop-invariant immediates (the constant fields of a
+# failure record) out of the interpreter loops into callee-saved VGPRs, which every call then saves
+# to scratch (99.7 -> 95.8 ms per launch, A/B'd on one box); -O2 instead of -O3 for the evaluator:
+# 96.2 -> 94.6 ms (round-1 A/B logs under profiles/r01_ab_*).
 SRC_FLAGS = {
-    # MachineLICM hoists loop-invariant immediates (the constant fields of a failure record) out of
-    # the interpreter loops into callee-saved VGPRs, which every call then saves to scratch
-    # (product default, 99.7 -> 95.8 ms per launch A/B'd on one box); -O2 instead of -O3 for the
-    # evaluator: 96.2 -> 94.6 ms (-fno-unroll-loops: 124.9 ms)
-    ("", "eval_kernel.hip"): ["-mllvm", "-disable-machine-licm", "-O2"],
-    ("stats", "eval_kernel.hip"): ["-mllvm", "-disable-machine-licm", "-O2"],
-    # A/B baseline: MachineLICM on
-    ("licm", "eval_kernel.hip"): [],
-    # codegen experiments on top of the product flags
-    ("nounroll", "eval_kernel.hip"): ["-mllvm", "-disable-machine-licm", "-fno-unroll-loops"],
-    ("o2", "eval_kernel.hip"): ["-mllvm", "-disable-machine-licm", "-O2"],
-    # register-allocation experiments around device calls (callee-saved VGPRs go to scratch)
-    ("ipra", "eval_kernel.hip"): ["-mllvm", "-disable-machine-licm", "-O2", "-mllvm", "-enable-ipra"],
-    ("csr8", "eval_kernel.hip"): ["-mllvm", "-disable-machine-licm", "-O2",
-                                  "-mllvm", "-regalloc-csr-first-time-cost=8"],
-    ("csr64", "eval_kernel.hip"): ["-mllvm", "-disable-machine-licm", "-O2",
-                                   "-mllvm", "-regalloc-csr-first-time-cost=64"],
-    # machine-scheduler / wave-priority experiments
-    ("silp", "eval_kernel.hip"): ["-mllvm", "-disable-machine-licm", "-O2", "-mllvm", "-amdgpu-sched-strategy=max-ilp"],
-    ("smem", "eval_kernel.hip"): ["-mllvm", "-disable-machine-licm", "-O2",
-                                  "-mllvm", "-amdgpu-sched-strategy=max-memory-clause"],
-    ("wprio", "eval_kernel.hip"): ["-mllvm", "-disable-machine-licm", "-O2", "-mllvm", "-amdgpu-set-wave-priority"],
+    "eval_kernel.hip": ["-mllvm", "-disable-machine-licm", "-O2"],
 }
 
 
-def _needs(src, obj, deps):
-    if not os.path.exists(obj):
+def _obj(obj_dir, s):
+    return os.path.join(obj_dir, s.replace(".cpp", ".o").replace(".hip", ".o"))
+
+
+def _needs(src, obj, deps, cmd):
+    stamp = obj + ".cmd"
+    if not os.path.exists(obj) or not os.path.exists(stamp):
         return True
+    with open(stamp) as f:
+        if f.read() != " ".join(cmd):
+            return True
     t = os.path.getmtime(obj)
     return any(os.path.getmtime(d) > t for d in [src] + deps)
 
 
 def build(verbose=False, variant=""):
-    """variant "" = the product library; "stats" = diagnostic build with evaluator counters
-    (libcfnguard_mi355x_stats.so, loaded only when GG_LIB points at it)."""
     out = OUT if not variant else OUT.replace(".so", "_" + variant + ".so")
     obj_dir = OBJ if not variant else OBJ + "_" + variant
-    flags = FLAGS + (["-DGG_STATS"] if variant == "stats" else [])
-    if variant.startswith("eu"):   # occupancy experiments: eu<N>[p<W>] = amdgpu_waves_per_eu(N), W-word LDS program window
-        eu, _, pw = variant[2:].partition("p")
-        flags = [f for f in flags if not f.startswith("-DGG_LANE_WAVES_PER_EU=")] + ["-DGG_LANE_WAVES_PER_EU=" + eu]
-        if pw:
-            flags.append("-DGG_LDS_PROG_WORDS=" + pw)
-    if variant == "iclause":       # call-structure experiments (eval_core.inc CLAUSE_FN / CONJ_FN)
-        flags.append("-DGG_INLINE_CLAUSE=1")
-    if variant == "iconj":
-        flags.append("-DGG_INLINE_CONJ=1")
-    if variant.startswith("cpad"):  # Ctx LDS stride experiments: cpad<N> = N pad dwords, cpack<N> = 4 B aligned + N pad dwords
-        flags.append("-DGG_CTX_PAD=" + variant[4:])
-    if variant.startswith("cpack"):
-        flags += ["-DGG_CTX_PACK=1", "-DGG_CTX_PAD=" + variant[5:]]
-    if variant.startswith("g"):    # lane-heap interleave experiments: g<N> = 2^N bytes per lane per heap row
-        flags.append("-DGG_HEAP_GRAIN=" + variant[1:])
+    flags = list(FLAGS)
+    if variant == "stats":
+        flags.append("-DGG_STATS")
+    elif variant == "ab":
+        flags += shlex.split(os.environ.get("GG_AB_FLAGS", ""))
+    elif variant:
+        raise ValueError("unknown build variant %r" % variant)
     os.makedirs(obj_dir, exist_ok=True)
     headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".h", ".inc"))]
     headers.append(os.path.join(HERE, "..", "include", "cfn_guard_mi355x.h"))
     jobs = []
     for s in HOST_SRCS + HIP_SRCS:
         src = os.path.join(CSRC, s)
-        obj = os.path.join(obj_dir, s.replace(".cpp", ".o").replace(".hip", ".o"))
-        if _needs(src, obj, headers):
-            cmd = [HIPCC, "--offload-arch=gfx950"] + flags + SRC_FLAGS.get((variant, s), SRC_FLAGS.get(("", s), [])) + ["-c", src, "-o", obj]
-            jobs.append((s, cmd))
+        obj = _obj(obj_dir, s)
+        cmd = [HIPCC, "--offload-arch=gfx950"] + flags + SRC_FLAGS.get(s, []) + ["-c", src, "-o", obj]
+        if _needs(src, obj, headers, cmd):
+            jobs.append((s, obj, cmd))
 
     def run(job):
-        name, cmd = job
+        name, obj, cmd = job
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError("compile failed: %s\n%s" % (name, r.stderr[-4000:]))
+        with open(obj + ".cmd", "w") as f:
+            f.write(" ".join(cmd))
         return name
 
     with ThreadPoolExecutor(max_workers=min(8, max(1, len(jobs)))) as ex:
         for name in ex.map(run, jobs):
             if verbose:
                 print("compiled", name)
-    objs = [os.path.join(obj_dir, s.replace(".cpp", ".o").replace(".hip", ".o")) for s in HOST_SRCS + HIP_SRCS]
-    if jobs or not os.path.exists(out):
+    objs = [_obj(obj_dir, s) for s in HOST_SRCS + HIP_SRCS]
+    local_yaml = os.path.join(HERE, "libyaml-0.so.2")
+    if jobs or not os.path.exists(out) or not os.path.exists(local_yaml):
         # libyaml is loaded from the package directory ($ORIGIN): an rpath to /opt/conda/lib would
-        # also pull conda's older libstdc++ in front of the one libamdhip64 needs
-        local_yaml = os.path.join(HERE, "libyaml-0.so.2")
+        # also pull conda's older libstdc++ in front of the one libamdhip64 needs.  Built artefact,
+        # not tracked (.gitignore), shipped to the GPU box with the tree.
         shutil.copyfile(os.path.join(YAML_LIB, "libyaml-0.so.2"), local_yaml)
         cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC"] + objs + [
             "-o", out, local_yaml, "-Wl,-rpath,$ORIGIN", "-lpthread"]

@@ -248,6 +248,9 @@ struct gg_session {
   bool evaluated = false;
   double last_kernel_ms = 0;
   std::string last_error;
+  ~gg_session() {
+    for (auto& pr : evq) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
+  }
 };
 
 namespace {
@@ -445,11 +448,14 @@ size_t session_drain(gg_session* s, double* out, size_t cap) {
 // total records the last launch wanted to publish (may exceed rec_cap)
 uint32_t session_records_wanted(gg_session* s) {
   uint32_t nrec = 0;
+  HIPCHK(hipStreamSynchronize(session_stream(s)));
   HIPCHK(hipMemcpy(&nrec, s->d_counters.p, 4, hipMemcpyDeviceToHost));
   return nrec;
 }
 
 void session_fetch(gg_session* s) {
+  // the tally kernel runs after ev1 on a non-blocking stream: wait for the whole launch
+  HIPCHK(hipStreamSynchronize(session_stream(s)));
   uint32_t ntiles = (uint32_t)(s->docs.ndocs() * s->progs.size());
   s->tiles.resize(ntiles);
   s->rule_status.resize((size_t)ntiles * s->max_top);
@@ -509,21 +515,17 @@ bool session_report(gg_session* s, std::string& out, int32_t& exit_code, ReportE
       tr.out = s->tiles[t];
       tr.rule_status.assign(s->rule_status.begin() + t * s->max_top, s->rule_status.begin() + t * s->max_top + s->max_top);
       tr.recs.assign(s->recs.begin() + tr.out.rec_off, s->recs.begin() + tr.out.rec_off + tr.out.rec_n);
-      if (tr.out.status == ST_FAIL) exit_code = exit_code == 5 ? 5 : 19;
       tp.push_back(&tr);
     }
     if (!writer.add(s->docs, (uint32_t)d, progs, tp, err)) { exit_code = -1; return false; }
   }
   out = writer.finish();
-  // validate.rs: exit code 19 when any rules file FAILed (structured.rs:110-112), 5 on parse errors
-  if (exit_code != 5) {
-    bool anyfail = false;
-    for (auto& t : s->tiles) if (t.status == ST_FAIL) anyfail = true;
-    exit_code = anyfail ? 19 : 0;
-  } else {
-    // parse error keeps exit code 5 unless a FAIL overrides it (StructuredReporter sets 19)
-    for (auto& t : s->tiles) if (t.status == ST_FAIL) exit_code = 19;
-  }
+  // exit code 19 when any rules file FAILed; a rules-file parse error set 5 beforehand
+  // (structured.rs:40-43).  CommonStructuredReporter overwrites it with 19 (structured.rs:110-112);
+  // JunitReporter::update_exit_code keeps 5 (reporters/mod.rs:97-103, validate/xml.rs:62-66).
+  bool anyfail = false;
+  for (auto& t : s->tiles) if (t.status == ST_FAIL) anyfail = true;
+  if (anyfail && !(fmt == OUT_JUNIT && exit_code == 5)) exit_code = 19;
   return true;
 }
 
@@ -793,11 +795,19 @@ char* cfn_guard_test(validate_input_t rules, const validate_input_t* specs, size
     gg_session s;
     const std::string rname = rules.file_name ? rules.file_name : "";
     std::string perr;
-    if (!add_rules(&s, rules.content ? rules.content : "", rname, perr)) {
-      set_err(err, 5, error_display("ParseError", perr));
-      if (exit_code) *exit_code = -1;
-      return nullptr;
+    const char* rtext = rules.content ? rules.content : "";
+    if (!add_rules(&s, rtext, rname, perr)) {
+      // test.rs:300-303 (text) and 345-350 (structured TestResult::Err): a report, exit code 1
+      if (exit_code) *exit_code = 1;
+      if (output_format == OUT_TEXT) return dup_str("Parse Error on ruleset file " + error_display("ParseError", perr) + "\n");
+      std::vector<TestSpecFile> ef(1);
+      ef[0].error = error_display("ParseError", perr);
+      int32_t code = 0;
+      std::string out = test_report(output_format, rname, ef, code);
+      return dup_str(out);
     }
+    // a rules file with no rules (Ok(None)): nothing is written, exit code 0 (test.rs:315, 366)
+    if (s.progs.empty()) return dup_str("");
     std::vector<TestSpecFile> files(n_specs);
     std::vector<std::vector<SpecCase>> cases(n_specs);
     std::vector<std::pair<size_t, size_t>> tile_of;   // (spec, case) of each evaluated document
@@ -892,11 +902,7 @@ char* cfn_guard_test(validate_input_t rules, const validate_input_t* specs, size
 
 // ------------------------------------------------------------- session API ---
 gg_session* gg_session_new(void) { return new gg_session(); }
-void gg_session_free(gg_session* s) {
-  if (!s) return;
-  for (auto& pr : s->evq) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
-  delete s;
-}
+void gg_session_free(gg_session* s) { delete s; }
 
 void gg_session_set_stream(gg_session* s, void* stream) { s->stream = (hipStream_t)stream; }
 
@@ -992,6 +998,75 @@ int32_t gg_session_add_docs(gg_session* s, const char* const* texts, const size_
 }
 
 int32_t gg_loader_selfcheck(const char* text, size_t len) { return loader_selfcheck(text, len); }
+
+static void dump_node(const DocBatch& D, uint64_t base, uint32_t i, std::string& o) {
+  const DNode& n = D.nodes[base + i];
+  auto str = [&](uint32_t off, uint32_t len) { return std::string(D.bytes.data() + off, len); };
+  switch (n.kind) {
+    case K_NULL: o += "Null"; break;
+    case K_STRING: o += "String(" + rust_debug_str(str(n.a, n.count)) + ")"; break;
+    case K_BOOL: o += n.a ? "Bool(true)" : "Bool(false)"; break;
+    case K_INT: o += "Int(" + std::to_string((int64_t)(((uint64_t)n.b << 32) | n.a)) + ")"; break;
+    case K_FLOAT: {
+      uint64_t u = ((uint64_t)n.b << 32) | n.a;
+      double d;
+      memcpy(&d, &u, 8);
+      o += "Float(" + rust_debug_f64(d) + ")";
+      break;
+    }
+    case K_LIST:
+      o += "[";
+      for (uint32_t j = 0; j < n.count; j++) { if (j) o += ", "; dump_node(D, base, n.a + j, o); }
+      o += "]";
+      break;
+    case K_MAP:
+      o += "{";
+      for (uint32_t j = 0; j < n.count; j++) {
+        const DNode& e = D.nodes[base + n.a + j];
+        if (j) o += ", ";
+        o += rust_debug_str(str(e.key_off, e.key_len)) + ": ";
+        dump_node(D, base, n.a + j, o);
+      }
+      o += "}";
+      break;
+    default: o += "?"; break;
+  }
+}
+
+char* gg_load_dump(const char* text, size_t len, int32_t mode, extern_err_t* err) {
+  set_err(err, 0, "");
+  try {
+    DocBatch D;
+    LoadError le;
+    if (!load_document(D, text ? text : "", text ? len : 0, "dump", (LoadMode)mode, le)) {
+      set_err(err, ffi_code(le.kind), error_display(le.kind, le.msg));
+      return nullptr;
+    }
+    std::string o;
+    dump_node(D, D.base[0], D.roots[0], o);
+    return dup_str(o);
+  } catch (std::exception& e) { set_err(err, -1, e.what()); return nullptr; }
+}
+
+int32_t gg_parse_rules(const char* text, const char* name, extern_err_t* err) {
+  set_err(err, 0, "");
+  try {
+    RulesFile rf;
+    bool empty = false;
+    std::string msg;
+    if (!parse_rules_file(text ? text : "", name ? name : "", rf, empty, msg)) {
+      set_err(err, 5, error_display("ParseError", msg));
+      return 5;
+    }
+    if (empty) return 1;
+    Program p;
+    if (!compile_program(rf, name ? name : "", p, msg)) {
+      set_err(err, 5, error_display("ParseError", msg));
+      return 5;
+    }
+    return 0;
+  } catch (std::exception& e) { set_err(err, -1, e.what()); return -1; }
+}
 
 size_t gg_synth_cfn_doc(uint64_t index, int32_t n_resources, char* buf, size_t cap) {
   std::string t;

@@ -604,14 +604,20 @@ void tile_error(const DocBatch& docs, uint32_t doc, const Program& prog, const T
       err.msg = "Arity mismatch for called parameter rule " + prog.ctx[prog.clauses[t.err_a].f] + ", expected " +
                 std::to_string(t.err_b) + ", got " + std::to_string(prog.clauses[t.err_a].c);
       break;
-    case E_INTERP_NON_STRING:
+    case E_INTERP_NON_STRING:   // eval_context.rs:497-518: Debug of key.self_value()
       err.kind = "NotComparable";
-      err.msg = "Variable projections inside Query are returning a non-string value for key";
+      err.msg = "Variable projections inside Query " + slice_display(prog.queries[t.err_b], 0) +
+                ", is returning a non-string value for key " + type_info(r.N(t.err_a).kind) + ", (" +
+                r.dbg_path(r.path(t.err_a), r.line(t.err_a), r.col(t.err_a)) + ", " + r.debug(t.err_a) + ")";
       break;
-    case E_INTERP_QUERY:
+    case E_INTERP_QUERY: {      // eval_context.rs:436-443 (the reference displays query[1])
       err.kind = "IncompatibleError";
-      err.msg = "This type of query based variable interpolation is not supported";
+      const auto& parts = prog.queries[t.err_a];
+      std::vector<QueryPart> one(parts.begin() + (parts.size() > 1 ? 1 : 0), parts.begin() + (parts.size() > 1 ? 2 : parts.size()));
+      err.msg = "This type of query " + slice_display(one, 0) + " based variable interpolation is not supported map, " +
+                slice_display(parts, 0);
       break;
+    }
     case E_REGEX_UNSUPPORTED:
       err.kind = "Unsupported";
       err.msg = "unsupported on MI355X path: regex /" + prog.regex_src[t.err_a] + "/ (" +

@@ -105,8 +105,32 @@ def lib():
                                                   ctypes.c_int32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ExternError)]
     L.gg_loader_device_check.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_size_t), ctypes.c_size_t,
                                          ctypes.POINTER(ExternError)]
+    L.gg_load_dump.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int32, ctypes.POINTER(ExternError)]
+    L.gg_load_dump.restype = ctypes.c_void_p
+    L.gg_parse_rules.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(ExternError)]
+    L.gg_parse_rules.restype = ctypes.c_int32
     _lib = L
     return L
+
+
+def load_dump(text, mode=0):
+    """Host loader diagnostic (no GPU): typed rendering of one document's value tree.
+    mode 0 = libyaml loader (CLI path), 1 = serde loader (FFI path)."""
+    b = _b(text)
+    err = ExternError()
+    p = lib().gg_load_dump(b, len(b), mode, ctypes.byref(err))
+    if err.code != 0:
+        _raise(err)
+    return _take_string(p)
+
+
+def parse_rules(text, name="r.guard"):
+    """Host rules-file parser diagnostic (no GPU): 0 = rules, 1 = no rules; raises GuardError (code 5)."""
+    err = ExternError()
+    rc = lib().gg_parse_rules(_b(text), _b(name), ctypes.byref(err))
+    if err.code != 0:
+        _raise(err)
+    return rc
 
 
 LOAD_STATS = ("kernel_ms", "nodes", "distinct_strings", "pool_bytes", "text_bytes", "h2d_ms", "d2h_ms", "table_retries")

@@ -106,6 +106,14 @@ int32_t gg_session_kernel_stats(gg_session *s, uint64_t *out, size_t n);
  * 0 = they differ, -1 = fast path declined the document. */
 int32_t gg_loader_selfcheck(const char *text, size_t len);
 
+/* Host-side diagnostics (no GPU; tests pin the loader and the grammar with them).
+ * gg_load_dump: loads one document (mode 0 libyaml / 1 serde, as gg_session_add_docs) and returns a
+ * typed rendering of the value tree, e.g. {"check": Bool(true)}; NULL + err on a load error.
+ * gg_parse_rules: parses one rules file like parse_rules (validate.rs:658-664); returns 0 = rules,
+ * 1 = no rules (Ok(None)), 5 = parse error (err->message = the Error Display). */
+char *gg_load_dump(const char *text, size_t len, int32_t mode, extern_err_t *err);
+int32_t gg_parse_rules(const char *text, const char *name, extern_err_t *err);
+
 /* Synthetic CloudFormation corpus (BASELINE configs[1]); byte-identical to synth.py cfn_doc. */
 size_t gg_synth_cfn_doc(uint64_t index, int32_t n_resources, char *buf, size_t cap);
 int32_t gg_session_add_synthetic(gg_session *s, uint64_t first, size_t n, int32_t n_resources, int32_t nthreads,

@@ -323,12 +323,13 @@ def eval_file_report(rules_file, doc, data_name):
     return status, simplified_json_from_root(rec)
 
 
-def validate_structured(rules, data, parsed_docs=None, output="json"):
+def validate_structured(rules, data, parsed_docs=None, output="json", raise_errors=False):
     """``cfn-guard validate --structured -o {json|yaml|sarif|junit} -S none`` over in-memory inputs.
 
     rules: list of (rules_file_name, text); data: list of (data_name, text).
     Returns (stdout_text, exit_code, stderr_text).  Evaluation errors abort the run with
-    no stdout, exit code -1 (main.rs:35-42)."""
+    no stdout, exit code -1 (main.rs:35-42); raise_errors=True re-raises the GuardError instead
+    (its kind gives the guard-ffi code, errors.rs:12-38)."""
     exit_code = SUCCESS
     stderr = []
     parsed_rules = []
@@ -350,7 +351,9 @@ def validate_structured(rules, data, parsed_docs=None, output="json"):
             cases = []
             for rf, rname in parsed_rules:
                 st, rep = eval_file_report(rf, doc, dname)
-                if st == E.FAIL:
+                # CommonStructuredReporter sets 19 over a parse error's 5 (structured.rs:110-112);
+                # JunitReporter::update_exit_code keeps 5 (reporters/mod.rs:97-103, xml.rs:62-66)
+                if st == E.FAIL and not (output == "junit" and exit_code == ERROR_STATUS):
                     exit_code = FAILURE_STATUS
                 fr["status"] = E.status_and(fr["status"], rep["status"])
                 fr["not_compliant"].extend(rep["not_compliant"])
@@ -372,6 +375,8 @@ def validate_structured(rules, data, parsed_docs=None, output="json"):
         else:
             raise ValueError(output)
     except GuardError as e:
+        if raise_errors:
+            raise
         return "", -1, "".join(stderr) + "Error occurred %s" % e.display()
     return out, exit_code, "".join(stderr)
 

@@ -79,8 +79,19 @@ def _compile(pattern: str):
     return _re.compile(translate(pattern), _re.V0)
 
 
+# Patterns the evaluator actually matched (tests use it to tell which inputs reach a regex).
+EVALUATED = set()
+
+
 def is_match(pattern: str, s: str) -> bool:
+    EVALUATED.add(pattern)
     return _compile(pattern).search(s) is not None
+
+
+def fancy_only(pattern: str) -> bool:
+    """constructs only fancy-regex evaluates (look-around, back-references, atomic groups)"""
+    import re
+    return bool(re.search(r"\(\?<?[=!]|\(\?>|\\[1-9]|\\k<", pattern))
 
 
 def is_valid(pattern: str) -> bool:

@@ -79,7 +79,16 @@ def get_status_result(expected, got):
 
 def run_test(rules_text, rules_name, specs, output="text"):
     """specs: [(path, text)].  Returns (stdout text, exit code)."""
-    rf = parse_rules(rules_text, rules_name)
+    try:
+        rf = parse_rules(rules_text, rules_name)
+    except GuardError as e:
+        # test.rs:300-303 (plain text) / 345-350 (structured TestResult::Err), TEST_ERROR_STATUS_CODE
+        if output == "text":
+            return "Parse Error on ruleset file %s\n" % e.display(), TEST_ERROR
+        return _structured_error(rules_name, e.display(), output)
+    if rf is None:
+        # Ok(None): nothing written, SUCCESS_STATUS_CODE (test.rs:315, 366)
+        return "", SUCCESS
     if output == "text":
         return _generic(rf, specs)
     return _structured(rf, rules_name, specs, output)

@@ -30,20 +30,40 @@ def test_structured_json_golden():
     assert out == open(os.path.join(G, "validate", "structured.json")).read()
 
 
-def test_all_data_dir_vs_oracle():
+def _data_dir():
     d = os.path.join(G, "validate", "data-dir")
-    data = [(f, open(os.path.join(d, f)).read()) for f in sorted(os.listdir(d)) if f.endswith(".yaml")]
-    # the lookbehind regex rule is only reached for templates that have the key; keep the rest
-    rules = [r for r in _rules_dir()]
-    exp, ecode, _ = oracle_validate(rules, data)
-    try:
-        out, code = guard_amd.validate_structured(rules, data)
-    except guard_amd.GuardError as e:
-        # evaluating fancy-regex look-around is explicitly unsupported on the MI355X path
-        assert "unsupported on MI355X path" in e.message
-        return
-    assert code == ecode
-    assert out == exp
+    return [(f, open(os.path.join(d, f)).read()) for f in sorted(os.listdir(d)) if f.endswith(".yaml")]
+
+
+def test_all_data_dir_vs_oracle():
+    """validate/rules-dir x validate/data-dir.  The three rules files without look-around x all six
+    templates: byte-identical in every format.  The look-behind rules file alone x each template:
+    byte-identical where the oracle never evaluates the look-behind regex, and the explicit
+    "unsupported on MI355X path" error exactly where it does (SURVEY.md App. B #15)."""
+    from guard_oracle import rxcompat
+    rules = _rules_dir()
+    plain = [r for r in rules if "lookbehind" not in r[0]]
+    fancy = [r for r in rules if "lookbehind" in r[0]]
+    assert len(plain) == 3 and len(fancy) == 1
+    data = _data_dir()
+    assert len(data) == 6
+    for fmt in ("json", "yaml", "sarif", "junit"):
+        exp, ecode, _ = oracle_validate(plain, data, output=fmt)
+        out, code = guard_amd.validate_structured(plain, data, output=fmt)
+        assert (code, out) == (ecode, exp), fmt
+    reached = 0
+    for dn, text in data:
+        rxcompat.EVALUATED.clear()
+        exp, ecode, _ = oracle_validate(fancy, [(dn, text)])
+        if any(rxcompat.fancy_only(p) for p in rxcompat.EVALUATED):
+            reached += 1
+            with pytest.raises(guard_amd.GuardError) as ei:
+                guard_amd.validate_structured(fancy, [(dn, text)])
+            assert ei.value.code == -1 and "unsupported on MI355X path" in ei.value.message
+            continue
+        out, code = guard_amd.validate_structured(fancy, [(dn, text)])
+        assert (code, out) == (ecode, exp), dn
+    assert reached == 2   # the two advanced_regex_negative_lookbehind_* templates
 
 
 def test_structured_payload_golden():
