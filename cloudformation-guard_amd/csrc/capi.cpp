@@ -188,6 +188,7 @@ struct GpuProgram {
     dp.n_top = prog.blob[sizeof(ProgHeader) / 4 + 1];
     dp.n_slots = h.n_name_slots;
     dp.n_rules_total = h.n_rules;
+    dp.n_vars = h.n_vars;
     dp.blob = b;
     dp.lds_words = h.off_dfa;
   }
@@ -510,12 +511,8 @@ bool session_report(gg_session* s, std::string& out, int32_t& exit_code, ReportE
   for (size_t d = 0; d < nd; d++) {
     std::vector<const TileResult*> tp;
     for (size_t f = 0; f < nf; f++) {
-      size_t t = d * nf + f;
-      TileResult& tr = trs[f];
-      tr.out = s->tiles[t];
-      tr.rule_status.assign(s->rule_status.begin() + t * s->max_top, s->rule_status.begin() + t * s->max_top + s->max_top);
-      tr.recs.assign(s->recs.begin() + tr.out.rec_off, s->recs.begin() + tr.out.rec_off + tr.out.rec_n);
-      tp.push_back(&tr);
+      trs[f] = tile_view(s->tiles.data(), s->rule_status.data(), s->max_top, s->recs.data(), d * nf + f);
+      tp.push_back(&trs[f]);
     }
     if (!writer.add(s->docs, (uint32_t)d, progs, tp, err)) { exit_code = -1; return false; }
   }
@@ -654,10 +651,7 @@ char* cfn_guard_run_checks(validate_input_t data, validate_input_t rules, bool v
       set_err(err, ffi_code(re.kind), error_display(re.kind, re.msg));
       return nullptr;
     }
-    TileResult tr;
-    tr.out = s.tiles[0];
-    tr.rule_status.assign(s.rule_status.begin(), s.rule_status.begin() + s.max_top);
-    tr.recs.assign(s.recs.begin() + tr.out.rec_off, s.recs.begin() + tr.out.rec_off + tr.out.rec_n);
+    TileResult tr = tile_view(s.tiles.data(), s.rule_status.data(), s.max_top, s.recs.data(), 0);
     std::string out;
     ReportError re;
     std::vector<const Program*> progs{&s.progs[0]->prog};

@@ -34,6 +34,7 @@ struct DevProg {
   uint32_t n_top;         // number of top-level rules
   uint32_t n_slots;
   uint32_t n_rules_total;
+  uint32_t n_vars;        // variable ids (root-scope resolved-variable table: lets + captures)
   const uint32_t* blob;   // device blob the pointers above index into
   uint32_t lds_words;     // words before the DFA tables (the part the kernels stage in LDS)
 };

@@ -79,7 +79,7 @@ __device__ __attribute__((always_inline)) inline void tile_begin(CtxT& c, const 
   c.err = 0; c.err_a = 0; c.err_b = 0; c.suppress = 0; c.rec_created = 0; c.depth = 0; c.nsyn = 0;
   c.resmap = A.docs.res_map ? A.docs.res_map[doc] : NONE;
   c.tix = c.resmap != NONE ? A.docs.tix + A.docs.tix_off[doc] : nullptr;
-  c.type_key = A.docs.type_key; c.ffok = NONE;
+  c.type_key = A.docs.type_key; c.ffok = NONE; c.naux = 0;
 #ifdef GG_STATS
   for (int i = 0; i < 8; i++) c.st[i] = 0;
 #endif
@@ -140,6 +140,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
       c.wbase = alloc_pers(c, WLEVELS * (uint32_t)sizeof(WLevel)); c.wdepth = 0;
       c.memo = alloc_pers(c, (P->n_slots ? P->n_slots : 1) * 4);
       if (!c.err) for (uint32_t i = 0; i < P->n_slots; i++) u32a(c, c.memo)[i] = 3u;
+      c.vtab = alloc_pers(c, (P->n_vars ? P->n_vars : 1) * 16);
+      if (!c.err) for (uint32_t i = 0; i < P->n_vars; i++) u32a(c, c.vtab)[i * 4] = 0u;
       push_frame(c, F_ROOT, NONE, A.docs.roots[doc], P->root_block);
       uint32_t fails = 0, passes = 0;
       uint8_t* rs = A.rule_status + (size_t)tile * A.max_top;
@@ -150,7 +152,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
         if (st == ST_PASS) passes++; else if (st == ST_FAIL) fails++;
       }
       status = fails ? ST_FAIL : (passes ? ST_PASS : ST_SKIP);
-      n = c.err ? 0 : c.nrec;
+      n = c.err ? 0 : c.nrec + c.naux;
       tile_stats(c, A);
     }
     // wave-aggregated record allocation
@@ -168,10 +170,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
       bool retry = c.err == E_HEAP || c.err == E_RECORDS || c.err == E_DEPTH;
       if (retry) A.retry_list[atomicAdd(A.retry_count, 1u)] = tile;
       if (n && off + n > A.rec_cap) { c.err = E_RECORDS; n = 0; }
-      for (uint32_t i = 0; i < n; i++) A.recs[off + i] = hload<Rec>(c, FRAMES_BYTES + i * (uint32_t)sizeof(Rec));
+      const uint32_t naux = n ? c.naux : 0, nrec = n - naux;
+      for (uint32_t i = 0; i < nrec; i++) A.recs[off + i] = hload<Rec>(c, FRAMES_BYTES + i * (uint32_t)sizeof(Rec));
+      for (uint32_t i = 0; i < naux; i++)
+        A.recs[off + nrec + i] = hload<Rec>(c, FRAMES_BYTES + RECS_BYTES - (i + 1) * (uint32_t)sizeof(Rec));
       TileOut o;
       o.status = status; o.err = c.err; o.err_a = c.err_a; o.err_b = c.err_b;
-      o.rec_off = off; o.rec_n = n; o.pad0 = 0; o.pad1 = 0;
+      o.rec_off = off; o.rec_n = nrec; o.pad0 = naux; o.pad1 = 0;
       A.tiles[tile] = o;
     }
   }
@@ -205,6 +210,8 @@ __global__ void __launch_bounds__(64) guard_eval_kernel(LaunchArgs A) {
       c.wbase = alloc_pers(c, WLEVELS * (uint32_t)sizeof(WLevel)); c.wdepth = 0;
     c.memo = alloc_pers(c, (P->n_slots ? P->n_slots : 1) * 4);
     if (!c.err) for (uint32_t i = 0; i < P->n_slots; i++) u32a(c, c.memo)[i] = 3u;
+    c.vtab = alloc_pers(c, (P->n_vars ? P->n_vars : 1) * 16);
+    if (!c.err) for (uint32_t i = 0; i < P->n_vars; i++) u32a(c, c.vtab)[i * 4] = 0u;
     push_frame(c, F_ROOT, NONE, A.docs.roots[doc], P->root_block);
     uint32_t fails = 0, passes = 0;
     uint8_t* rs = A.rule_status + (size_t)tile * A.max_top;
@@ -221,16 +228,19 @@ __global__ void __launch_bounds__(64) guard_eval_kernel(LaunchArgs A) {
       A.retry2_list[atomicAdd(A.retry2_count, 1u)] = tile;
     // publish records
     uint32_t off = 0;
-    uint32_t n = c.err ? 0 : c.nrec;
+    uint32_t n = c.err ? 0 : c.nrec + c.naux;
     if (lane == 0 && n) off = atomicAdd(A.rec_cursor, n);
     off = __shfl(off, 0);
     if (n && off + n > A.rec_cap) { c.err = E_RECORDS; n = 0; }
+    const uint32_t naux = n ? c.naux : 0, nrec = n - naux;
     const Rec* src = (const Rec*)(heap + c.fcap);
-    for (uint32_t i = lane; i < n; i += 64) A.recs[off + i] = src[i];
+    for (uint32_t i = lane; i < nrec; i += 64) A.recs[off + i] = src[i];
+    const Rec* atop = (const Rec*)(heap + c.fcap + c.rcap);
+    for (uint32_t i = lane; i < naux; i += 64) A.recs[off + nrec + i] = atop[-(int32_t)(i + 1)];
     if (lane == 0) {
       TileOut o;
       o.status = status; o.err = c.err; o.err_a = c.err_a; o.err_b = c.err_b;
-      o.rec_off = off; o.rec_n = n; o.pad0 = 0; o.pad1 = 0;
+      o.rec_off = off; o.rec_n = nrec; o.pad0 = naux; o.pad1 = 0;
       A.tiles[tile] = o;
     }
   }

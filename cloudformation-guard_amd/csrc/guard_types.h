@@ -167,6 +167,7 @@ enum RecKind : uint32_t {
   REC_RULE_OPEN = 1, REC_RULE_CLOSE = 2, REC_DISJ_OPEN = 3, REC_DISJ_CLOSE = 4,
   REC_BLOCK_EMPTY = 5, REC_MISSING_BLOCK_VALUE = 6, REC_UNARY = 7, REC_NOVALUE_EMPTY = 8,
   REC_DEPENDENT_RULE = 9, REC_CMP = 10, REC_IN = 11, REC_LIST = 12,
+  REC_AUX = 13,   // side record (TileOut.pad0 of them after the tile's records): join-key lists of R4 / R5
 };
 
 // NotComparable reasons carried in Rec.x for REC_CMP
@@ -197,7 +198,7 @@ struct TileOut {
   uint32_t err;        // ErrKind
   uint32_t err_a, err_b;
   uint32_t rec_off;    // offset into the global record arena
-  uint32_t rec_n;
+  uint32_t rec_n;      // failure records; then pad0 side records (REC_AUX and their pairs)
   uint32_t pad0, pad1;
 };
 

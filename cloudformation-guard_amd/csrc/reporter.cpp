@@ -93,6 +93,7 @@ struct R {
   const Program& prog;
   bool serde;
   uint64_t dbase;   // global index of the reported document's first node (refs are relative)
+  const RecSpan* aux = nullptr;   // the tile's side records (join-key lists, R4 / R5)
 
   static const uint32_t KEY_BIT = 0x20000000u;   // "the key of map entry X" (MapValue.keys)
   const DocBatch& B(uint32_t ref) const { return (ref & LIT_BIT) ? prog.lit : docs; }
@@ -286,9 +287,46 @@ struct R {
                path_display(cur) + ", type " + type_info(n.kind);
       case R_FILTER_NOT_STRUCT:
         return std::string("Filter on value type that was not a struct or array ") + type_info(n.kind) + " " + path_display(cur);
+      case R_MAPFILTER_NOT_STRUCT:   // eval_context.rs:913-919
+        return std::string("Map Filter for keys was not a struct ") + type_info(n.kind) + " " + path_display(cur);
+      case R_VAR_INDEX_OOB: {
+        // eval_context.rs:432-435: aux[q.aux] = {clause: var, x: #keys, y: index}, then the keys in pairs
+        const Rec& h = aux_at(q.aux);
+        std::string keys;
+        for (uint32_t k = 0; k < h.x; k++) {
+          const Rec& pr = aux_at(q.aux + 1 + k / 2);
+          if (k) keys += ", ";
+          keys += qr_debug(k & 1 ? pr.to : pr.from);
+        }
+        return "Index " + std::to_string(h.y) + " on the set of values returned for variable " + prog.var_names[h.clause] +
+               " on the join, is out of bounds. Length " + std::to_string(h.x) + ", Values = [" + keys + "]";
+      }
+      case R_VAR_KEYS_UNRESOLVED: {
+        // eval_context.rs:452-457: aux[q.aux] = {clause: var, from: the unresolved key}
+        const Rec& h = aux_at(q.aux);
+        return "Keys returned for variable " + prog.var_names[h.clause] + " could not completely resolve. Path traversed until " +
+               path_display(h.from.node) + reason(h.from);
+      }
       default:
         return "";
     }
+  }
+  const Rec& aux_at(uint32_t i) const {
+    if (!aux || i >= aux->size()) throw Fatal{"Unsupported", "MI355X path: side record out of range"};
+    return (*aux)[i];
+  }
+  // Debug of a QueryResult (rules/mod.rs:172-177, derived)
+  std::string qr_debug(const QR& q) const {
+    const uint32_t k = q.meta & 3u;
+    if (k == QR_SYNTH_INT) {
+      std::string p = q.node == NONE ? dbg_path("", 0, 0) : dbg_path(path(q.node), line(q.node), col(q.node));
+      return "Resolved(Int((" + p + ", " + std::to_string(synth_val(q)) + ")))";
+    }
+    if (k == QR_LITERAL) return "Literal(" + debug(q.node) + ")";
+    if (k == QR_RESOLVED) return "Resolved(" + debug(q.node) + ")";
+    const std::string why = reason(q);
+    return "UnResolved(UnResolved { traversed_to: " + debug(q.node) + ", remaining_query: " + rust_debug_str(remaining(q)) +
+           ", reason: " + (why.empty() ? std::string("None") : "Some(" + rust_debug_str(why) + ")") + " })";
   }
   std::string remaining(const QR& q) const { return prog.query_remaining(q.uref >> 12, q.uref & 0xFFF); }
 
@@ -351,7 +389,7 @@ const char* op_msg(uint32_t op, bool neg) {
 
 struct Walker {
   const R& r;
-  const std::vector<Rec>& recs;
+  const RecSpan& recs;
   size_t i = 0;
 
   J clause_wrap(const char* kind, J inner) {
@@ -650,7 +688,7 @@ bool build_file_report(const DocBatch& docs, uint32_t doc, const std::vector<con
       const Program& P = *progs[f];
       const TileResult& T = *tiles[f];
       if (T.out.err) { tile_error(docs, doc, P, T.out, err); return false; }
-      R r{docs, P, docs.serde, docs.base[doc]};
+      R r{docs, P, docs.serde, docs.base[doc], &T.aux};
       Walker w{r, T.recs};
       J items = w.items(0xFFFFFFFFu);
       if (per_file) per_file->push_back(items);

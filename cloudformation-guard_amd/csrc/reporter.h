@@ -12,11 +12,28 @@
 
 namespace gg {
 
-struct TileResult {
-  TileOut out;
-  std::vector<uint8_t> rule_status;  // per top-level rule
-  std::vector<Rec> recs;
+// Non-owning view of one tile's device results (the session's fetched buffers).
+struct RecSpan {
+  const Rec* p = nullptr;
+  size_t n = 0;
+  size_t size() const { return n; }
+  const Rec& operator[](size_t i) const { return p[i]; }
 };
+struct TileResult {
+  TileOut out{};
+  const uint8_t* rule_status = nullptr;  // per top-level rule
+  RecSpan recs;                          // failure records, in evaluation order
+  RecSpan aux;                           // side records (join-key lists of unresolved reasons R4 / R5)
+};
+// the view of tile t inside fetched session buffers (rec_n records, then pad0 aux records)
+inline TileResult tile_view(const TileOut* tiles, const uint8_t* rule_status, size_t max_top, const Rec* recs, size_t t) {
+  TileResult r;
+  r.out = tiles[t];
+  r.rule_status = rule_status + t * max_top;
+  r.recs.p = recs + r.out.rec_off; r.recs.n = r.out.rec_n;
+  r.aux.p = recs + r.out.rec_off + r.out.rec_n; r.aux.n = r.out.pad0;
+  return r;
+}
 
 struct ReportError { bool set = false; std::string kind, msg; };
 

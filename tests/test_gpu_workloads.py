@@ -140,3 +140,22 @@ def test_sharded_sessions_merge_to_single_process_report():
         exp, ecode, _ = oracle_validate(rules, list(zip(names, texts)), output=fmt)
         assert merged == exp
         assert max(codes, key=lambda c: sharding._SEVERITY[c]) == ecode
+
+
+def test_key_captures_and_join_reasons_vs_oracle():
+    """variable / key captures (`Resources[ id ]`, `Resources[ id | filter ]`) accumulate into the
+    root scope and feed joins; join reasons R4 (index past the key list) and R5 (unresolved keys)
+    render with their Debug key lists -- byte-identical with the oracle in every format"""
+    docs = synth.cfn_corpus(12, start=11, n_resources=6) + synth.cfn_corpus(4, start=90, n_resources=30)
+    data = [("cap-%d.json" % i, d) for i, d in enumerate(docs)]
+    rules = _pack("capture_rulepack")
+    for fmt in ("json", "yaml", "sarif", "junit"):
+        exp, ecode, _ = oracle_validate(rules, data, output=fmt)
+        out, code = guard_amd.validate_structured(rules, data, output=fmt)
+        assert (code, out) == (ecode, exp), fmt
+
+
+def test_key_captures_lane_matches_wave():
+    docs = synth.cfn_corpus(130, start=2000, n_resources=20)
+    rules = _pack("capture_rulepack")
+    assert _session_report(docs, rules, 0, "c") == _session_report(docs, rules, 1, "c")
