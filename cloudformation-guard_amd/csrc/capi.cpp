@@ -190,7 +190,8 @@ struct GpuProgram {
     dp.n_rules_total = h.n_rules;
     dp.n_vars = h.n_vars;
     dp.blob = b;
-    dp.lds_words = h.off_dfa;
+    dp.lds_words = h.nwords;   // stage_program falls back to the words before the DFA tables
+    dp.dfa_lds = 0;
   }
 };
 
@@ -1040,6 +1041,13 @@ char* gg_load_dump(const char* text, size_t len, int32_t mode, extern_err_t* err
     dump_node(D, D.base[0], D.roots[0], o);
     return dup_str(o);
   } catch (std::exception& e) { set_err(err, -1, e.what()); return nullptr; }
+}
+
+int32_t gg_regex_match(const char* pattern, const char* text, size_t len, uint32_t* stats) {
+  CompiledRegex rx = compile_regex(pattern ? pattern : "");
+  if (stats) { stats[0] = rx.nstates; stats[1] = rx.ncls; }
+  if (!rx.valid) return -2;
+  return dfa_match(rx, text ? text : "", text ? len : 0);
 }
 
 int32_t gg_parse_rules(const char* text, const char* name, extern_err_t* err) {

@@ -86,15 +86,24 @@ struct Compiler {
     if (it != regex_ids.end()) return it->second;
     CompiledRegex cr = compile_regex(src);
     if (!cr.valid) { err = "Could not parse regular expression: " + src + " (" + cr.why + ")"; }
-    PRegex pr;
-    pr.table = (uint32_t)dfa.size();
+    PRegex pr{};
     pr.nstates = cr.nstates;
     pr.start = cr.start;
-    pr.flags = (cr.unsupported ? 1u : 0u) | (cr.ascii_only ? 2u : 0u) | (cr.end_anchored ? 4u : 0u);
+    pr.ncls = cr.ncls;
+    pr.flags = (cr.unsupported ? 1u : 0u) | ((uint32_t)cr.bounds.size() << 8);
+    pr.table = (uint32_t)dfa.size();
     for (uint16_t t : cr.table) dfa.push_back(t);
-    // accept flags: encode as a second table row block (one u16 per state)
-    pr.table = pr.table;  // table rows first
+    pr.accept = (uint32_t)dfa.size();
     for (uint8_t a : cr.accept) dfa.push_back(a);
+    while (dfa.size() & 1) dfa.push_back(0);
+    pr.ascii = (uint32_t)dfa.size();
+    for (int k = 0; k < 128; k += 2) dfa.push_back((uint16_t)(cr.ascii[k] | (cr.ascii[k + 1] << 8)));
+    pr.bounds = (uint32_t)dfa.size();
+    for (auto& b : cr.bounds) {
+      const uint32_t w = (b.first << 8) | b.second;
+      dfa.push_back((uint16_t)(w & 0xFFFFu));
+      dfa.push_back((uint16_t)(w >> 16));
+    }
     regexes.push_back(pr);
     P.regex.push_back(cr);
     P.regex_src.push_back(src);

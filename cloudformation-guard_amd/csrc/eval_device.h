@@ -36,7 +36,9 @@ struct DevProg {
   uint32_t n_rules_total;
   uint32_t n_vars;        // variable ids (root-scope resolved-variable table: lets + captures)
   const uint32_t* blob;   // device blob the pointers above index into
-  uint32_t lds_words;     // words before the DFA tables (the part the kernels stage in LDS)
+  uint32_t lds_words;     // words the kernels stage in LDS: the whole blob when it fits the window,
+                          // else everything before the regex DFA tables
+  uint32_t dfa_lds;       // set by stage_program: the DFA tables were staged (dfa points into LDS)
 };
 
 struct DevBatch {

@@ -48,7 +48,10 @@ static const uint32_t LDS_PROG_WORDS = GG_LDS_PROG_WORDS;   // 8 KB per workgrou
 __device__ __attribute__((always_inline)) inline const DevProg* stage_program(const DevProg* G, DevProg* sp, uint4* sblob) {
   const uint32_t lane = __lane_id();
   __syncthreads();   // the previous batch's reads of the window are complete
-  const uint32_t n = G->lds_words;
+  uint32_t n = G->lds_words;
+  // the whole blob (regex DFA tables included) when it fits the window, else all but the tables
+  const uint32_t dfa_off = (uint32_t)((const uint32_t*)G->dfa - G->blob);
+  if (n > LDS_PROG_WORDS) n = dfa_off;
   if (n > LDS_PROG_WORDS) return G;
   const uint4* src = (const uint4*)G->blob;
   for (uint32_t i = lane; i < (n + 3u) / 4u; i += 64u) sblob[i] = src[i];
@@ -62,6 +65,8 @@ __device__ __attribute__((always_inline)) inline const DevProg* stage_program(co
     GG_REBASE(clause_refs); GG_REBASE(disj_refs); GG_REBASE(blocks); GG_REBASE(lets); GG_REBASE(rules);
     GG_REBASE(name_rules); GG_REBASE(name_rule_ids); GG_REBASE(funcs); GG_REBASE(params); GG_REBASE(param_vars);
     GG_REBASE(alts); GG_REBASE(regex); GG_REBASE(lit_nodes); GG_REBASE(lit_ranges); GG_REBASE(bytes);
+    d.dfa_lds = 0;
+    if ((size_t)dfa_off * 4u < lim && G->dfa) { GG_REBASE(dfa); d.dfa_lds = 1; }
 #undef GG_REBASE
     *sp = d;
   }

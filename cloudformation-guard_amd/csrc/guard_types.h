@@ -110,7 +110,12 @@ struct PLet { uint32_t var, kind, id, pad; };   // id: literal node ref | query 
 struct PRule { uint32_t name_slot, cond, block, pad; };
 struct PFunc { uint32_t fname, first_arg, nargs, pad; };   // args: PLet (var unused)
 struct PParamRule { uint32_t rule, first_param, nparams, pad; }; // params: var ids in vars[]
-struct PRegex { uint32_t table, nstates, start, flags; };  // flags: 1=unsupported, 2=ascii-only
+// regex DFA (regex_dfa.h) over code-point classes, in the program's u16 DFA section (offsets in
+// u16 units): next-state table at `table` (nstates x ncls), accept flags at `accept` (u16 per state:
+// 1 = match decided, 2 = match at the end of the haystack), the ASCII class map at `ascii` (128
+// bytes) and, at `bounds`, flags >> 8 u32 words (first code point << 8 | class) sorted by code point
+// for the classes above U+007F.  flags bit 0: unsupported on the MI355X path.
+struct PRegex { uint32_t table, nstates, start, flags, ncls, accept, ascii, bounds; };
 
 enum FuncName : uint32_t { F_COUNT = 0, F_OTHER = 1 };
 

@@ -2,9 +2,14 @@
 #include "regex_dfa.h"
 
 #include <algorithm>
+#include <array>
 #include <map>
 #include <memory>
+#include <functional>
 #include <set>
+#include <unordered_map>
+
+#include "unicode_tables.h"
 
 namespace gg {
 
@@ -15,7 +20,7 @@ struct RxErr { std::string why; bool unsupported; };
 struct Rng { uint32_t lo, hi; };
 
 struct RNode {
-  enum K { Empty, Set, Concat, Alt, Repeat } k = Empty;
+  enum K { Empty, Set, Concat, Alt, Repeat, AssertStart, AssertEnd } k = Empty;
   std::vector<Rng> set;                      // code point ranges
   std::vector<std::unique_ptr<RNode>> kids;
   int min = 0, max = -1;                     // Repeat
@@ -43,12 +48,40 @@ std::vector<Rng> negate(std::vector<Rng> v) {
   return out;
 }
 
+std::vector<Rng> table_set(const uint32_t (*t)[2], uint32_t n) {
+  std::vector<Rng> v(n);
+  for (uint32_t i = 0; i < n; i++) v[i] = {t[i][0], t[i][1]};
+  return v;
+}
+
+// members of cp's simple-case-folding class (CaseFolding.txt C + S), cp included
+void add_fold(std::vector<Rng>& out, uint32_t cp) {
+  size_t lo = 0, hi = uni::kFoldCp_N;
+  while (lo < hi) { size_t m = (lo + hi) / 2; if (uni::kFoldCp[m][0] < cp) lo = m + 1; else hi = m; }
+  if (lo < uni::kFoldCp_N && uni::kFoldCp[lo][0] == cp) {
+    const uint32_t* cl = uni::kFoldClass[uni::kFoldCp[lo][1]];
+    for (uint32_t k = 0; k < cl[1]; k++) { uint32_t m = uni::kFoldMembers[cl[0] + k]; out.push_back({m, m}); }
+  }
+}
+
+// ClassUnicode::case_fold_simple (regex-syntax hir::ClassUnicode): every member of the set widened
+// to its folding class
+void fold_closure(std::vector<Rng>& set) {
+  normalize(set);
+  std::vector<Rng> add;
+  for (const Rng& r : set) {
+    size_t lo = 0, hi = uni::kFoldCp_N;
+    while (lo < hi) { size_t m = (lo + hi) / 2; if (uni::kFoldCp[m][0] < r.lo) lo = m + 1; else hi = m; }
+    for (size_t k = lo; k < uni::kFoldCp_N && uni::kFoldCp[k][0] <= r.hi; k++) add_fold(add, uni::kFoldCp[k][0]);
+  }
+  set.insert(set.end(), add.begin(), add.end());
+  normalize(set);
+}
+
 struct RxParser {
   const std::string& p;
   size_t i = 0;
   bool icase = false, dotall = false;
-  bool ascii_only = false;
-  bool start_anchor = false, end_anchor = false;
   int depth = 0;
   explicit RxParser(const std::string& s) : p(s) {}
 
@@ -69,21 +102,18 @@ struct RxParser {
 
   void add_literal(std::vector<Rng>& set, uint32_t cp) {
     set.push_back({cp, cp});
-    if (icase) {
-      if (cp >= 'a' && cp <= 'z') set.push_back({cp - 32, cp - 32});
-      else if (cp >= 'A' && cp <= 'Z') set.push_back({cp + 32, cp + 32});
-      if (cp >= 0x80 || cp == 'k' || cp == 'K' || cp == 's' || cp == 'S') ascii_only = true;
-    }
+    if (icase) add_fold(set, cp);   // (?i): simple case folding (regex-syntax hir translate)
   }
 
+  // Unicode perl classes (regex-syntax unicode::perl_digit / perl_space / perl_word); they are
+  // closed under simple case folding, so (?i) leaves them unchanged
   std::vector<Rng> perl_class(char c) {
     std::vector<Rng> s;
     switch (c) {
-      case 'd': case 'D': s = {{'0', '9'}}; break;
-      case 'w': case 'W': s = {{'0', '9'}, {'A', 'Z'}, {'_', '_'}, {'a', 'z'}}; break;
-      case 's': case 'S': s = {{'\t', '\r'}, {' ', ' '}}; break;
+      case 'd': case 'D': s = table_set(uni::kDigit, uni::kDigit_N); break;
+      case 'w': case 'W': s = table_set(uni::kWord, uni::kWord_N); break;
+      case 's': case 'S': s = table_set(uni::kSpace, uni::kSpace_N); break;
     }
-    ascii_only = true;
     if (c == 'D' || c == 'W' || c == 'S') s = negate(s);
     return s;
   }
@@ -206,19 +236,16 @@ struct RxParser {
         else hi = next_cp();
         if (hi < lo) invalid("bad range");
         set.push_back({lo, hi});
-        if (icase) {
-          for (uint32_t c = std::max<uint32_t>(lo, 'a'); c <= std::min<uint32_t>(hi, 'z'); c++) set.push_back({c - 32, c - 32});
-          for (uint32_t c = std::max<uint32_t>(lo, 'A'); c <= std::min<uint32_t>(hi, 'Z'); c++) set.push_back({c + 32, c + 32});
-          if (hi >= 0x80 || (lo <= 'k' && hi >= 'k') || (lo <= 's' && hi >= 's') || (lo <= 'K' && hi >= 'K') || (lo <= 'S' && hi >= 'S')) ascii_only = true;
-        }
       } else if (is_lit) {
         add_literal(set, lo);
       } else {
         set.insert(set.end(), item.begin(), item.end());
       }
     }
+    // unicode_fold_and_negate: fold the whole class under (?i), then negate
+    if (icase) fold_closure(set);
     normalize(set);
-    if (neg) { set = negate(set); if (icase) ascii_only = true; }
+    if (neg) set = negate(set);
     return set;
   }
 
@@ -276,6 +303,17 @@ struct RxParser {
     return n;
   }
 
+  std::unique_ptr<RNode> assert_node(RNode::K k) {
+    auto n = std::make_unique<RNode>(); n->k = k; return n;
+  }
+  std::unique_ptr<RNode> end_node() {
+    size_t j = i;
+    int d = depth;
+    while (j < p.size() && p[j] == ')' && d > 0) { j++; d--; }
+    if (!(j == p.size() || (p[j] == '|' && d == 0))) unsup("mid-pattern end anchor");
+    return assert_node(RNode::AssertEnd);
+  }
+
   std::unique_ptr<RNode> set_node(std::vector<Rng> s) {
     auto n = std::make_unique<RNode>(); n->k = RNode::Set; normalize(s); n->set = s; return n;
   }
@@ -331,18 +369,16 @@ struct RxParser {
       if (dotall) return set_node({{0, 0x10FFFF}});
       return set_node({{0, 9}, {11, 0x10FFFF}});
     }
-    if (c == '^') {
-      if (i == 0) { start_anchor = true; i++; return nullptr; }
-      unsup("mid-pattern ^");
-    }
-    if (c == '$') {
-      if (i + 1 == p.size() && depth == 0) { end_anchor = true; i++; return nullptr; }
-      unsup("mid-pattern $");
-    }
+    // `^` / `\A`: an assertion the NFA passes only at offset 0 (closure at_start); `$` / `\z`
+    // (non-multiline: end of text) only where nothing can follow it -- the end of the pattern or
+    // of a top-level alternative, possibly through closing groups -- where it marks the state as
+    // accepting at the end of the haystack
+    if (c == '^') { i++; return assert_node(RNode::AssertStart); }
+    if (c == '$') { i++; return end_node(); }
     if (c == '\\') {
       i++;
-      if (i < p.size() && p[i] == 'A') { if (i == 1) { start_anchor = true; i++; return nullptr; } unsup("mid-pattern \\A"); }
-      if (i < p.size() && p[i] == 'z') { if (i + 1 == p.size() && depth == 0) { end_anchor = true; i++; return nullptr; } unsup("mid-pattern \\z"); }
+      if (i < p.size() && p[i] == 'A') { i++; return assert_node(RNode::AssertStart); }
+      if (i < p.size() && p[i] == 'z') { i++; return end_node(); }
       return set_node(escape(false));
     }
     if (c == '*' || c == '+' || c == '?') invalid("repetition operator missing expression");
@@ -353,51 +389,31 @@ struct RxParser {
 };
 
 // ------------------------------------------------------------------ NFA ----
-struct NState { int type; uint8_t lo, hi; int out, out2; };  // type 0 byte, 1 split, 2 match, 3 eps
+// The automaton runs over code-point classes, not bytes: the code points are partitioned into
+// classes whose members every character set of the regex treats alike (\\w + literals: a handful
+// of classes), so the DFA table is nstates x nclasses and stays small enough for LDS even for the
+// Unicode perl classes.  The matcher decodes UTF-8 and maps a code point to its class through a
+// 128-entry ASCII table, or a binary search over the class boundaries above U+007F.
+// type 0 class set, 1 split, 2 match, 3 epsilon, 4 start-of-text assertion, 5 match at end of text
+struct NState { int type; int cset; int out, out2; };
 struct Nfa {
   std::vector<NState> s;
-  int add(int type, uint8_t lo = 0, uint8_t hi = 0, int out = -1, int out2 = -1) {
-    s.push_back({type, lo, hi, out, out2});
+  std::vector<std::vector<uint8_t>> csets;   // per class-set state: membership per class
+  int add(int type, int cset = -1, int out = -1, int out2 = -1) {
+    s.push_back({type, cset, out, out2});
     return (int)s.size() - 1;
   }
 };
-struct Frag { int start; std::vector<int*> outs; };
 
-void utf8_encode(uint32_t cp, uint8_t* b, int& n) {
-  if (cp < 0x80) { b[0] = (uint8_t)cp; n = 1; }
-  else if (cp < 0x800) { b[0] = 0xC0 | (cp >> 6); b[1] = 0x80 | (cp & 0x3F); n = 2; }
-  else if (cp < 0x10000) { b[0] = 0xE0 | (cp >> 12); b[1] = 0x80 | ((cp >> 6) & 0x3F); b[2] = 0x80 | (cp & 0x3F); n = 3; }
-  else { b[0] = 0xF0 | (cp >> 18); b[1] = 0x80 | ((cp >> 12) & 0x3F); b[2] = 0x80 | ((cp >> 6) & 0x3F); b[3] = 0x80 | (cp & 0x3F); n = 4; }
-}
-
-void utf8_seqs(uint32_t lo, uint32_t hi, std::vector<std::vector<std::pair<uint8_t, uint8_t>>>& out) {
-  if (lo > hi) return;
-  if (lo <= 0xDFFF && hi >= 0xD800) {
-    if (lo < 0xD800) utf8_seqs(lo, 0xD7FF, out);
-    if (hi > 0xDFFF) utf8_seqs(0xE000, hi, out);
-    return;
-  }
-  const uint32_t maxes[] = {0x7F, 0x7FF, 0xFFFF};
-  for (uint32_t m : maxes) if (lo <= m && hi > m) { utf8_seqs(lo, m, out); utf8_seqs(m + 1, hi, out); return; }
-  if (hi <= 0x7F) { out.push_back({{(uint8_t)lo, (uint8_t)hi}}); return; }
-  for (int k = 1; k < 4; k++) {
-    uint32_t m = (1u << (6 * k)) - 1;
-    if ((lo & ~m) != (hi & ~m)) {
-      if ((lo & m) != 0) { utf8_seqs(lo, lo | m, out); utf8_seqs((lo | m) + 1, hi, out); return; }
-      if ((hi & m) != m) { utf8_seqs(lo, (hi & ~m) - 1, out); utf8_seqs(hi & ~m, hi, out); return; }
-    }
-  }
-  uint8_t a[4], b[4]; int na, nb;
-  utf8_encode(lo, a, na); utf8_encode(hi, b, nb);
-  std::vector<std::pair<uint8_t, uint8_t>> seq;
-  for (int k = 0; k < na; k++) seq.push_back({a[k], b[k]});
-  out.push_back(seq);
+void collect_sets(const RNode& n, std::vector<const RNode*>& out) {
+  if (n.k == RNode::Set) out.push_back(&n);
+  for (auto& k : n.kids) collect_sets(*k, out);
 }
 
 struct Builder {
   Nfa& nfa;
-  // returns (start, list of dangling out pointers as state indices + which field)
-  struct F { int start; std::vector<std::pair<int, int>> outs; };  // (state, field 0/1)
+  const std::map<const RNode*, int>& cset_of;
+  struct F { int start; std::vector<std::pair<int, int>> outs; };  // dangling (state, field 0/1)
   void patch(const F& f, int target) {
     for (auto& o : f.outs) { if (o.second == 0) nfa.s[o.first].out = target; else nfa.s[o.first].out2 = target; }
   }
@@ -405,27 +421,9 @@ struct Builder {
   F build(const RNode& n) {
     switch (n.k) {
       case RNode::Empty: return eps();
-      case RNode::Set: {
-        std::vector<std::vector<std::pair<uint8_t, uint8_t>>> seqs;
-        for (auto& r : n.set) utf8_seqs(r.lo, r.hi, seqs);
-        if (seqs.empty()) {  // empty class never matches
-          int s = nfa.add(0, 1, 0);  // lo > hi: impossible
-          return F{s, {{s, 0}}};
-        }
-        // alternation of byte sequences
-        std::vector<F> alts;
-        for (auto& sq : seqs) {
-          int first = -1, prev = -1;
-          for (auto& br : sq) {
-            int st = nfa.add(0, br.first, br.second);
-            if (first < 0) first = st;
-            if (prev >= 0) nfa.s[prev].out = st;
-            prev = st;
-          }
-          alts.push_back(F{first, {{prev, 0}}});
-        }
-        return alt_of(alts);
-      }
+      case RNode::Set: { int s = nfa.add(0, cset_of.at(&n)); return F{s, {{s, 0}}}; }
+      case RNode::AssertStart: { int s = nfa.add(4); return F{s, {{s, 0}}}; }
+      case RNode::AssertEnd: { int s = nfa.add(5); return F{s, {}}; }
       case RNode::Concat: {
         if (n.kids.empty()) return eps();
         F f = build(*n.kids[0]);
@@ -447,14 +445,14 @@ struct Builder {
         for (int k = 0; k < n.min; k++) { F g = build(c); patch(acc, g.start); acc.outs = g.outs; }
         if (n.max < 0) {
           F g = build(c);
-          int sp = nfa.add(1, 0, 0, g.start, -1);
+          int sp = nfa.add(1, -1, g.start, -1);
           patch(g, sp);
           patch(acc, sp);
           return F{acc.start, {{sp, 1}}};
         }
         for (int k = n.min; k < n.max; k++) {
           F g = build(c);
-          int sp = nfa.add(1, 0, 0, g.start, -1);
+          int sp = nfa.add(1, -1, g.start, -1);
           patch(acc, sp);
           std::vector<std::pair<int, int>> outs = g.outs;
           outs.push_back({sp, 1});
@@ -469,7 +467,7 @@ struct Builder {
     if (alts.size() == 1) return alts[0];
     F cur = alts.back();
     for (int k = (int)alts.size() - 2; k >= 0; k--) {
-      int sp = nfa.add(1, 0, 0, alts[k].start, cur.start);
+      int sp = nfa.add(1, -1, alts[k].start, cur.start);
       std::vector<std::pair<int, int>> outs = alts[k].outs;
       outs.insert(outs.end(), cur.outs.begin(), cur.outs.end());
       cur = F{sp, outs};
@@ -478,18 +476,36 @@ struct Builder {
   }
 };
 
-void closure(const Nfa& nfa, std::set<int>& st) {
-  std::vector<int> stack(st.begin(), st.end());
-  while (!stack.empty()) {
-    int x = stack.back(); stack.pop_back();
-    const NState& s = nfa.s[x];
-    if (s.type == 1 || s.type == 3) {
-      for (int o : {s.out, s.out2}) if (o >= 0 && !st.count(o)) { st.insert(o); stack.push_back(o); }
-    }
+// epsilon closure, in place; `mark` is a scratch bitmap over NFA states (cleared on return).
+// Start-of-text assertions pass only for the closure taken at offset 0.
+void closure(const Nfa& nfa, std::vector<int>& st, std::vector<uint8_t>& mark, bool at_start) {
+  for (int x : st) mark[x] = 1;
+  for (size_t k = 0; k < st.size(); k++) {
+    const NState& s = nfa.s[st[k]];
+    if (s.type == 1 || s.type == 3 || (s.type == 4 && at_start))
+      for (int o : {s.out, s.out2}) if (o >= 0 && !mark[o]) { mark[o] = 1; st.push_back(o); }
   }
+  for (int x : st) mark[x] = 0;
+  std::sort(st.begin(), st.end());
 }
 
+struct VecHash {
+  size_t operator()(const std::vector<int>& v) const {
+    size_t h = 1469598103934665603ull;
+    for (int x : v) h = (h ^ (size_t)x) * 1099511628211ull;
+    return h;
+  }
+};
+
 }  // namespace
+
+uint32_t regex_class_of(const CompiledRegex& rx, uint32_t cp) {
+  if (cp < 128) return rx.ascii[cp];
+  // last boundary whose start <= cp (bounds[0].first == 128)
+  size_t lo = 0, hi = rx.bounds.size();
+  while (hi - lo > 1) { size_t m = (lo + hi) / 2; if (rx.bounds[m].first <= cp) lo = m; else hi = m; }
+  return rx.bounds[lo].second;
+}
 
 CompiledRegex compile_regex(const std::string& pattern) {
   CompiledRegex out;
@@ -503,67 +519,155 @@ CompiledRegex compile_regex(const std::string& pattern) {
     if (e.unsupported) { out.unsupported = true; return out; }
     out.valid = false; return out;
   }
-  out.ascii_only = ps.ascii_only;
-  out.end_anchored = ps.end_anchor;
+  // ---- code-point classes: elementary intervals keyed by the set of Set nodes containing them
+  std::vector<const RNode*> sets_n;
+  collect_sets(*ast, sets_n);
+  std::vector<uint32_t> cuts = {0, 128, 0x110000};
+  for (auto* n : sets_n) for (auto& r : n->set) { cuts.push_back(r.lo); cuts.push_back(r.hi + 1); }
+  for (uint32_t c = 1; c < 128; c++) cuts.push_back(c);   // ASCII: one interval per code point
+  std::sort(cuts.begin(), cuts.end());
+  cuts.erase(std::unique(cuts.begin(), cuts.end()), cuts.end());
+  std::map<std::vector<uint8_t>, uint32_t> sig_cls;
+  std::vector<std::vector<uint8_t>> cls_sig;
+  std::vector<std::pair<uint32_t, uint32_t>> ivals;   // (start, class)
+  for (size_t k = 0; k + 1 < cuts.size(); k++) {
+    const uint32_t lo = cuts[k];
+    std::vector<uint8_t> sig(sets_n.size(), 0);
+    for (size_t j = 0; j < sets_n.size(); j++) {
+      const auto& v = sets_n[j]->set;   // normalized, sorted
+      auto it = std::upper_bound(v.begin(), v.end(), lo, [](uint32_t x, const Rng& r) { return x < r.lo; });
+      if (it != v.begin() && (it - 1)->hi >= lo) sig[j] = 1;
+    }
+    auto it = sig_cls.find(sig);
+    if (it == sig_cls.end()) {
+      it = sig_cls.emplace(sig, (uint32_t)cls_sig.size()).first;
+      cls_sig.push_back(sig);
+    }
+    ivals.push_back({lo, it->second});
+  }
+  const uint32_t ncls0 = (uint32_t)cls_sig.size();
+  if (ncls0 > 250) { out.unsupported = true; out.why = "too many character classes"; return out; }
   Nfa nfa;
-  Builder b{nfa};
+  std::map<const RNode*, int> cset_of;
+  for (size_t j = 0; j < sets_n.size(); j++) {
+    std::vector<uint8_t> mem(ncls0, 0);
+    for (uint32_t c = 0; c < ncls0; c++) mem[c] = cls_sig[c][j];
+    cset_of[sets_n[j]] = (int)nfa.csets.size();
+    nfa.csets.push_back(mem);
+  }
+  Builder b{nfa, cset_of};
   Builder::F f = b.build(*ast);
   int m = nfa.add(2);
   b.patch(f, m);
-  int nstart = f.start;
+  const int nstart = f.start;
 
-  // subset construction; state 0 = dead
-  std::map<std::set<int>, uint32_t> ids;
-  std::vector<std::set<int>> sets;
+  // ---- subset construction over the classes (state 0 = dead)
+  std::vector<uint8_t> mark(nfa.s.size(), 0);
+  std::unordered_map<std::vector<int>, uint32_t, VecHash> ids;
+  std::vector<std::vector<int>> sets;
   sets.push_back({});
   ids[{}] = 0;
-  std::set<int> s0 = {nstart};
-  closure(nfa, s0);
-  auto intern = [&](const std::set<int>& s) -> uint32_t {
-    auto it = ids.find(s);
+  std::vector<int> s0 = {nstart};
+  closure(nfa, s0, mark, true);
+  auto intern = [&](std::vector<int>& st) -> uint32_t {
+    auto it = ids.find(st);
     if (it != ids.end()) return it->second;
     uint32_t id = (uint32_t)sets.size();
-    ids[s] = id; sets.push_back(s);
+    ids.emplace(st, id);
+    sets.push_back(st);
     return id;
   };
-  out.start = intern(s0);
-  std::vector<std::array<uint16_t, 256>> table;
-  table.push_back({});
-  table[0].fill(0);
+  uint32_t start = intern(s0);
+  std::vector<std::vector<uint32_t>> table(1, std::vector<uint32_t>(ncls0, 0));
   for (size_t cur = 1; cur < sets.size(); cur++) {
     if (sets.size() > 4000) { out.unsupported = true; out.why = "DFA too large"; return out; }
-    std::array<uint16_t, 256> row;
-    for (int byte = 0; byte < 256; byte++) {
-      std::set<int> nx;
-      for (int x : sets[cur]) {
+    const std::vector<int> here = sets[cur];
+    std::vector<uint32_t> row(ncls0);
+    for (uint32_t c = 0; c < ncls0; c++) {
+      std::vector<int> nx;
+      for (int x : here) {
         const NState& s = nfa.s[x];
-        if (s.type == 0 && byte >= s.lo && byte <= s.hi) nx.insert(s.out);
+        if (s.type == 0 && nfa.csets[s.cset][c]) nx.push_back(s.out);
       }
-      if (!ps.start_anchor) nx.insert(nstart);   // unanchored search
-      closure(nfa, nx);
-      row[byte] = (uint16_t)intern(nx);
+      nx.push_back(nstart);   // unanchored search: a match may start at every offset
+      std::sort(nx.begin(), nx.end());
+      nx.erase(std::unique(nx.begin(), nx.end()), nx.end());
+      closure(nfa, nx, mark, false);
+      row[c] = intern(nx);
     }
-    if (table.size() <= cur) table.resize(cur + 1);
-    table[cur] = row;
+    table.push_back(row);
   }
-  out.nstates = (uint32_t)sets.size();
-  out.table.resize((size_t)out.nstates * 256);
-  for (uint32_t st = 0; st < out.nstates; st++)
-    for (int byte = 0; byte < 256; byte++) out.table[(size_t)st * 256 + byte] = st < table.size() ? table[st][byte] : 0;
-  out.accept.resize(out.nstates);
-  for (uint32_t st = 0; st < out.nstates; st++) out.accept[st] = sets[st].count(m) ? 1 : 0;
+  // accept flags: 1 = a match ends here (is_match is decided), 2 = a match ends here if the
+  // haystack ends here (`$`)
+  const size_t nd = sets.size();
+  std::vector<uint8_t> acc(nd, 0);
+  for (size_t st = 0; st < nd; st++)
+    for (int x : sets[st]) { if (nfa.s[x].type == 2) acc[st] |= 1; else if (nfa.s[x].type == 5) acc[st] |= 2; }
+  // ---- Moore minimisation (block 0 stays the dead state)
+  std::vector<uint32_t> blk(nd);
+  for (size_t st = 0; st < nd; st++) blk[st] = st == 0 ? 0 : 1 + acc[st];
+  size_t nblk = std::set<uint32_t>(blk.begin(), blk.end()).size();
+  for (;;) {
+    std::map<std::vector<uint32_t>, uint32_t> ids2;
+    std::vector<uint32_t> nb(nd), key(ncls0 + 1);
+    for (size_t st = 0; st < nd; st++) {
+      key[0] = blk[st];
+      for (uint32_t c = 0; c < ncls0; c++) key[c + 1] = blk[table[st][c]];
+      auto it = ids2.find(key);
+      if (it == ids2.end()) it = ids2.emplace(key, (uint32_t)ids2.size()).first;
+      nb[st] = it->second;
+    }
+    const uint32_t dead = nb[0];
+    for (auto& x : nb) x = x == dead ? 0 : (x < dead ? x + 1 : x);
+    blk = nb;
+    if (ids2.size() == nblk) break;
+    nblk = ids2.size();
+  }
+  // ---- merge classes that every minimal state treats alike; emit
+  const uint32_t nmin = (uint32_t)nblk;
+  std::vector<std::vector<uint32_t>> mt(nmin, std::vector<uint32_t>(ncls0, 0));
+  std::vector<uint8_t> macc(nmin, 0);
+  for (size_t st = 0; st < nd; st++) {
+    for (uint32_t c = 0; c < ncls0; c++) mt[blk[st]][c] = blk[table[st][c]];
+    macc[blk[st]] = acc[st];
+  }
+  std::map<std::vector<uint32_t>, uint32_t> col_ids;
+  std::vector<uint32_t> cmap(ncls0);
+  for (uint32_t c = 0; c < ncls0; c++) {
+    std::vector<uint32_t> col(nmin);
+    for (uint32_t st = 0; st < nmin; st++) col[st] = mt[st][c];
+    auto it = col_ids.find(col);
+    if (it == col_ids.end()) it = col_ids.emplace(col, (uint32_t)col_ids.size()).first;
+    cmap[c] = it->second;
+  }
+  out.nstates = nmin;
+  out.start = blk[start];
+  out.accept = macc;
+  out.ncls = (uint32_t)col_ids.size();
+  out.table.assign((size_t)nmin * out.ncls, 0);
+  for (uint32_t st = 0; st < nmin; st++)
+    for (uint32_t c = 0; c < ncls0; c++) out.table[(size_t)st * out.ncls + cmap[c]] = (uint16_t)mt[st][c];
+  for (auto& iv : ivals) {
+    const uint32_t c = cmap[iv.second];
+    if (iv.first < 128) out.ascii[iv.first] = (uint8_t)c;
+    else if (out.bounds.empty() || out.bounds.back().second != c) out.bounds.push_back({iv.first, c});
+  }
   return out;
 }
 
 int dfa_match(const CompiledRegex& rx, const char* s, size_t n) {
   if (!rx.valid || rx.unsupported) return -1;
-  if (rx.ascii_only) for (size_t k = 0; k < n; k++) if ((unsigned char)s[k] >= 0x80) return -1;
   uint32_t st = rx.start;
-  if (!rx.end_anchored && rx.accept[st]) return 1;
+  if (rx.accept[st] & 1) return 1;
+  uint32_t cp = 0, need = 0;
   for (size_t k = 0; k < n; k++) {
-    st = rx.table[(size_t)st * 256 + (unsigned char)s[k]];
+    const uint8_t by = (uint8_t)s[k];
+    if (by < 0x80) { cp = by; need = 0; }
+    else if (by >= 0xC0) { need = by >= 0xF0 ? 3 : by >= 0xE0 ? 2 : 1; cp = by & (0x3Fu >> need); continue; }
+    else { cp = (cp << 6) | (by & 0x3Fu); if (--need) continue; }
+    st = rx.table[(size_t)st * rx.ncls + regex_class_of(rx, cp)];
     if (st == 0) return 0;
-    if (!rx.end_anchored && rx.accept[st]) return 1;
+    if (rx.accept[st] & 1) return 1;
   }
   return rx.accept[st] ? 1 : 0;
 }

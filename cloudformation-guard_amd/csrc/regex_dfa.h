@@ -8,9 +8,8 @@
 // Constructs fancy-regex supports but a DFA cannot (look-around, back-references, atomic
 // groups, \b, mid-pattern anchors) are NOT silently approximated: the regex is marked
 // unsupported and evaluating it raises an explicit "unsupported on MI355X path" error.
-// Unicode-dependent classes (\d \w \s, case folding beyond ASCII) are compiled for ASCII and
-// marked "ascii_only": matching a haystack that contains non-ASCII bytes raises the same
-// explicit error instead of guessing.
+// Perl classes \d \w \s and (?i) are Unicode-aware as in regex-syntax (unicode_tables.h).  The
+// DFA runs over code-point classes (table = nstates x nclasses); the matcher decodes UTF-8.
 #pragma once
 #include <cstdint>
 #include <string>
@@ -21,17 +20,19 @@ namespace gg {
 struct CompiledRegex {
   bool valid = true;          // syntactically valid (else: rules parse error)
   bool unsupported = false;   // valid but not DFA-compilable here
-  bool ascii_only = false;
-  bool end_anchored = false;
   uint32_t nstates = 0;       // state 0 = dead
   uint32_t start = 0;
-  std::vector<uint16_t> table;   // nstates * 256
-  std::vector<uint8_t> accept;   // nstates
+  uint32_t ncls = 0;          // code-point classes
+  uint8_t ascii[128] = {0};   // class of each ASCII code point
+  std::vector<std::pair<uint32_t, uint32_t>> bounds;   // (first code point, class) runs above U+007F
+  std::vector<uint16_t> table;   // nstates * ncls
+  std::vector<uint8_t> accept;   // nstates: 1 = match (decided), 2 = match if the haystack ends here
   std::string why;
 };
 
 CompiledRegex compile_regex(const std::string& pattern);
 
+uint32_t regex_class_of(const CompiledRegex& rx, uint32_t cp);
 // host reference matcher over the compiled DFA (used by host-side unit tests)
 int dfa_match(const CompiledRegex& rx, const char* s, size_t n);  // 1 match, 0 no, -1 unsupported
 

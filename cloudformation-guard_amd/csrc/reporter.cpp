@@ -658,8 +658,7 @@ void tile_error(const DocBatch& docs, uint32_t doc, const Program& prog, const T
     }
     case E_REGEX_UNSUPPORTED:
       err.kind = "Unsupported";
-      err.msg = "unsupported on MI355X path: regex /" + prog.regex_src[t.err_a] + "/ (" +
-                (prog.regex[t.err_a].unsupported ? prog.regex[t.err_a].why : std::string("Unicode-dependent class on non-ASCII input")) + ")";
+      err.msg = "unsupported on MI355X path: regex /" + prog.regex_src[t.err_a] + "/ (" + prog.regex[t.err_a].why + ")";
       break;
     case E_HEAP: err.kind = "Unsupported"; err.msg = "MI355X path: per-tile scratch heap exhausted"; break;
     case E_RECORDS: err.kind = "Unsupported"; err.msg = "MI355X path: failure-record buffer exhausted"; break;

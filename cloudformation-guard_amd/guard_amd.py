@@ -109,8 +109,18 @@ def lib():
     L.gg_load_dump.restype = ctypes.c_void_p
     L.gg_parse_rules.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(ExternError)]
     L.gg_parse_rules.restype = ctypes.c_int32
+    L.gg_regex_match.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint32)]
+    L.gg_regex_match.restype = ctypes.c_int32
     _lib = L
     return L
+
+
+def regex_match(pattern, text):
+    """Host run of the rules-file regex DFA (no GPU): (1 / 0 / -1 unsupported / -2 invalid, states, classes)."""
+    b = _b(text)
+    st = (ctypes.c_uint32 * 2)()
+    rc = lib().gg_regex_match(_b(pattern), b, len(b), st)
+    return rc, st[0], st[1]
 
 
 def load_dump(text, mode=0):

@@ -113,6 +113,10 @@ int32_t gg_loader_selfcheck(const char *text, size_t len);
  * 1 = no rules (Ok(None)), 5 = parse error (err->message = the Error Display). */
 char *gg_load_dump(const char *text, size_t len, int32_t mode, extern_err_t *err);
 int32_t gg_parse_rules(const char *text, const char *name, extern_err_t *err);
+/* The rule-regex DFA (compiled as for a rules file) run on the host over one haystack: 1 match,
+ * 0 no match, -1 unsupported on the MI355X path (look-around, back-references, ...), -2 invalid.
+ * stats (may be NULL, 2 values): DFA states, byte classes. */
+int32_t gg_regex_match(const char *pattern, const char *text, size_t len, uint32_t *stats);
 
 /* Synthetic CloudFormation corpus (BASELINE configs[1]); byte-identical to synth.py cfn_doc. */
 size_t gg_synth_cfn_doc(uint64_t index, int32_t n_resources, char *buf, size_t cap);

@@ -10,11 +10,33 @@ module by translating the syntax differences that matter for ``is_match``:
 * ``$`` (outside a class, non-multiline) matches only at the very end of the haystack in
   Rust; Python's ``$`` also matches before a trailing newline, so it becomes ``\\Z``.
 * ``\\z`` (Rust end of text) becomes ``\\Z``; ``\\A`` is the same in both.
-* Classes like ``\\d``/``\\w``/``\\s`` are Unicode in both engines.
+* Perl classes are Unicode in Rust regex-syntax with fixed definitions -- ``\\d`` = ``\\p{Nd}``,
+  ``\\w`` = ``[\\p{Alphabetic}\\p{M}\\p{Nd}\\p{Pc}\\p{Join_Control}]`` (UTS #18), ``\\s`` =
+  ``\\p{White_Space}`` -- while the Python module's V0 ``\\w`` / ``\\s`` follow ``str.isalnum`` /
+  ``str.isspace`` (``\\w`` would take No such as "½" and miss combining marks, ``\\s`` would take
+  U+001C..U+001F), so they are spelled out as those property classes.
+* ``(?i)`` is simple case folding in both (V0 without FULLCASE).
 """
 import functools
 
 import regex as _re
+
+
+_WORD = r"\p{Alphabetic}\p{M}\p{Nd}\p{Pc}\p{Join_Control}"
+# perl class -> (outside a class, inside a class); `\W` inside a class has no V0 spelling (kept)
+_PERL = {
+    "d": (r"\p{Nd}", r"\p{Nd}"), "D": (r"\P{Nd}", r"\P{Nd}"),
+    "s": (r"\p{White_Space}", r"\p{White_Space}"), "S": (r"\P{White_Space}", r"\P{White_Space}"),
+    "w": ("[" + _WORD + "]", _WORD), "W": ("[^" + _WORD + "]", None),
+}
+
+
+# regex-syntax ast::ClassAsciiKind (ASCII-only POSIX classes)
+_ASCII_CLASSES = {
+    "alnum": "0-9A-Za-z", "alpha": "A-Za-z", "ascii": "\\x00-\\x7F", "blank": "\\t ", "cntrl": "\\x00-\\x1F\\x7F",
+    "digit": "0-9", "graph": "!-~", "lower": "a-z", "print": " -~", "punct": "!-/:-@\\[-`{-~",
+    "space": "\\t\\n\\x0B\\f\\r ", "upper": "A-Z", "word": "0-9A-Za-z_", "xdigit": "0-9A-Fa-f",
+}
 
 
 def translate(pattern: str) -> str:
@@ -29,6 +51,16 @@ def translate(pattern: str) -> str:
             nxt = pattern[i + 1]
             if nxt == "z" and not in_class:
                 out.append("\\Z")
+            elif nxt in "xuU" and i + 2 < n and pattern[i + 2] == "{":
+                # Rust \x{...} / \u{...} / \U{...}: the code point itself
+                j = pattern.find("}", i + 3)
+                if j < 0:
+                    raise ValueError("bad escape")
+                out.append(_re.escape(chr(int(pattern[i + 3:j], 16))))
+                i = j + 1
+                continue
+            elif nxt in _PERL and not (in_class and nxt == "W"):
+                out.append(_PERL[nxt][1 if in_class else 0])
             else:
                 out.append(c + nxt)
             i += 2
@@ -39,7 +71,9 @@ def translate(pattern: str) -> str:
             elif c == "[" and i + 1 < n and pattern[i + 1] == ":":
                 j = pattern.find(":]", i + 2)
                 if j > 0:
-                    out.append(pattern[i:j + 2])
+                    # regex-syntax ASCII classes are ASCII-only (Python's are Unicode)
+                    name = pattern[i + 2:j]
+                    out.append(_ASCII_CLASSES.get(name, pattern[i:j + 2]))
                     i = j + 2
                     continue
             out.append(c)

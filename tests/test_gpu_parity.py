@@ -232,3 +232,33 @@ def test_reference_validate_resources_vs_oracle():
                 continue
             out, code = guard_amd.validate_structured(rules, data, output=fmt)
             assert (code, out) == (ecode, exp), (c["source"], fmt)
+
+
+def _unicode_docs():
+    vals = [("١٢٣", "ñandú-κ", "PROD", "😀"), ("123", "plain_name", "STRASSE", "ab"), ("12 3", "a b", "Straẞe", "é"),
+            ("߀߁", "ǅungla", "KELVIN", "😀😀"), ("²", "x½", "ΣΑΣ", ""), ("٣", "日本語", "prod\n", "ſ")]
+    docs = []
+    for i, (serial, name, env, icon) in enumerate(vals):
+        docs.append(json.dumps({"Resources": {
+            "r%d" % i: {"Type": "AWS::S3::Bucket" if i % 2 else "AWS::EC2::Volume",
+                        "Properties": {"Serial": serial, "Name": name, "Icon": icon,
+                                       "Tags": [{"Key": "env", "Value": env}]}}}}, ensure_ascii=False))
+    return docs
+
+
+def test_unicode_regex_pack_vs_oracle():
+    """non-ASCII haystacks against \\d \\w \\s (?i) . and anchored alternations, byte-identical with the
+    oracle in every format (SURVEY.md App. B #13); the DFA tables are LDS-staged (tiny class DFAs)"""
+    p = os.path.join(G, "unicode_rulepack")
+    rules = [(f, open(os.path.join(p, f)).read()) for f in sorted(os.listdir(p)) if f.endswith(".guard")]
+    data = [("u%d.json" % i, d) for i, d in enumerate(_unicode_docs())]
+    for fmt in ("json", "yaml", "sarif", "junit"):
+        exp, ecode, _ = oracle_validate(rules, data, output=fmt)
+        out, code = guard_amd.validate_structured(rules, data, output=fmt)
+        assert (code, out) == (ecode, exp), fmt
+
+
+def test_app_b13_unicode_digit_class_on_gpu():
+    rules = [("d.guard", "a == /^\\d+$/")]
+    out, code = guard_amd.validate_structured(rules, [("d.json", '{"a": "١٢٣"}')])
+    assert code == 0 and '"status": "PASS"' in out
