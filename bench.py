@@ -20,8 +20,18 @@ current stream).  `traffic` is filled from a separate rocprofv3 --pmc pass when
 profiles/pmc_<round>.json exists for the same workload, else null.
 
 cpu_baseline: the CPU oracle (oracle/guard_oracle, a pure-Python restatement of the reference
-evaluator) run end to end (load + evaluate + structured report) on a bounded sample of the same
-templates x the same rule pack, in one process per core on the host cores of this box.
+evaluator -- NOT the reference binary, which cannot be built here) run on a bounded sample of the
+same documents x the same rule pack, in one process per core on the host cores of this box:
+`value` end to end (load + evaluate + structured report), `eval_only_value` evaluation alone.
+
+e2e (N = 1): the whole job a `validate --structured` user pays for, on the same workload -- host
+load (text -> arena, synthetic text generation included), upload (PCIe + device packing), one
+evaluation with statuses and records fetched to the host, and the structured JSON report rendered
+on the host (report_bytes, discarded) -- and the evaluations/s that total gives.
+
+--workload: cfg2 (default; BASELINE.json configs[1], the metric's config), cfg3 (the same corpus x
+the 22-file full-registry stand-in, configs[2]) or cfg5 (AWS Config snapshots x the
+network-reachability regex / join pack, configs[4]; --docs snapshots of ~33 CIs each).
 """
 import argparse
 import json
@@ -39,6 +49,11 @@ TILEOUT_BYTES = 32
 REC_BYTES = 48
 
 
+def log(msg):
+    """progress on stderr (a long phase must keep writing: gpurun takes 3 silent minutes for a hang)"""
+    print("[bench %s] %s" % (time.strftime("%H:%M:%S"), msg), file=sys.stderr, flush=True)
+
+
 def _cpu_share():
     try:
         n = len(os.sched_getaffinity(0))
@@ -47,47 +62,85 @@ def _cpu_share():
     return max(1, min(16, n))
 
 
-def _oracle_worker(args):
-    first, n, n_resources = args
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+def _workload_docs(workload, first, n, n_resources):
     import synth
+    if workload == "cfg5":
+        return synth.config_corpus(n, start=first)
+    return synth.cfn_corpus(n, start=first, n_resources=n_resources)
+
+
+def _oracle_worker(args):
+    workload, first, n, n_resources = args
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import rulepack
     from guard_oracle import validate_structured
-    rules = rulepack.rule_pack()
-    docs = synth.cfn_corpus(n, start=first, n_resources=n_resources)
+    from guard_oracle import evaluator as E
+    from guard_oracle.loader import load_document
+    from guard_oracle.parser import parse_rules
+    rules = rulepack.rule_pack(workload)
+    docs = _workload_docs(workload, first, n, n_resources)
+    names = ["synthetic-%d.json" % (first + i) for i in range(n)]
     t = time.time()
-    for i, d in enumerate(docs):
-        validate_structured(rules, [("synthetic-%d.json" % (first + i), d)])
-    return time.time() - t, n * len(rules)
+    for name, d in zip(names, docs):
+        validate_structured(rules, [(name, d)])
+    t_e2e = time.time() - t
+    parsed = [load_document(d, name) for name, d in zip(names, docs)]
+    prs = [parse_rules(text, rn) for rn, text in rules]
+    t = time.time()
+    for name, doc in zip(names, parsed):
+        for rf in prs:
+            E.eval_rules_file(rf, E.RootScope(rf, doc), name)
+    t_eval = time.time() - t
+    return t_e2e, t_eval, n * len(rules)
 
 
-def cpu_baseline(n_resources, per_core=600):
+def cpu_baseline(workload, n_resources, per_core):
     import multiprocessing as mp
     cores = _cpu_share()
     ctx = mp.get_context("spawn")
-    jobs = [(c * per_core, per_core, n_resources) for c in range(cores)]
+    jobs = [(workload, c * per_core, per_core, n_resources) for c in range(cores)]
     t0 = time.time()
     with ctx.Pool(cores) as pool:
         res = pool.map(_oracle_worker, jobs)
     wall = time.time() - t0
-    evals = sum(r[1] for r in res)
+    evals = sum(r[2] for r in res)
     busy = max(r[0] for r in res)
+    busy_eval = max(r[1] for r in res)
     return {"value": round(evals / busy, 2), "unit": "evals/s", "cores": cores, "kind": "port",
-            "sample": "%d synthetic templates x %d rules files (%d evals), oracle end to end (load + evaluate + "
-                      "structured report), one process per core; %.1f s wall" % (cores * per_core, evals // max(1, cores * per_core),
-                                                                                    evals, wall)}
+            "eval_only_value": round(evals / busy_eval, 2),
+            "sample": "%d %s documents x %d rules files (%d evals) through the Python restatement of the reference "
+                      "(oracle/guard_oracle, not the reference binary), one process per core; value = load + evaluate + "
+                      "structured report, eval_only_value = evaluation alone; %.1f s wall"
+                      % (cores * per_core, workload, evals // max(1, cores * per_core), evals, wall)}
+
+
+def _gen_chunk(args):
+    workload, first, n, n_resources = args
+    sys.path.insert(0, os.path.join(ROOT, "cloudformation-guard_amd"))
+    return _workload_docs(workload, first, n, n_resources)
+
+
+def generate_docs(workload, first, n, n_resources, procs):
+    """document texts of a workload without a native generator (cfg5), in worker processes"""
+    import multiprocessing as mp
+    step = max(1, (n + procs - 1) // procs)
+    jobs = [(workload, first + k, min(step, n - k), n_resources) for k in range(0, n, step)]
+    with mp.get_context("spawn").Pool(procs) as pool:
+        parts = pool.map(_gen_chunk, jobs)
+    return [d for p in parts for d in p]
 
 
 def load_pmc(workload):
-    path = os.path.join(ROOT, "profiles", "pmc_r01.json")
-    if not os.path.exists(path):
-        return None
-    try:
-        d = json.load(open(path))
+    """HBM bytes per launch of the dominant kernel from the newest profiles/pmc_r<NN>.json recorded for
+    this exact workload (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes), else None"""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_r*.json")), reverse=True):
+        try:
+            d = json.load(open(path))
+        except Exception:
+            continue
         if d.get("workload") == workload:
             return d.get("hbm_bytes_per_launch")
-    except Exception:
-        return None
     return None
 
 
@@ -96,16 +149,26 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--docs", type=int, default=1_000_000, help="templates per GPU")
+    ap.add_argument("--workload", choices=("cfg2", "cfg3", "cfg5"), default="cfg2")
+    ap.add_argument("--docs", type=int, default=0, help="documents per GPU (default: 1M templates; cfg5 303031 "
+                                                         "snapshots = 10M configuration items)")
+    ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--e2e-report-docs", type=int, default=50_000,
+                    help="documents whose structured report is rendered for e2e (0: all); the report time is "
+                         "scaled to the whole job")
     ap.add_argument("--resources", type=int, default=50)
     ap.add_argument("--threads", type=int, default=0, help="host loader threads (default: CPU share)")
     ap.add_argument("--loader", choices=("host", "device"), default="host",
                     help="document loader: host threads, or the MI355X JSON loader (csrc/json_gpu.hip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-per-core", type=int, default=600)
+    ap.add_argument("--cpu-per-core", type=int, default=0)
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL); gloo only to rehearse N ranks sharing one GPU (GG_BENCH_DEVICE)")
     args = ap.parse_args()
+    if not args.docs:
+        args.docs = 303_031 if args.workload == "cfg5" else 1_000_000
+    if not args.cpu_per_core:
+        args.cpu_per_core = {"cfg2": 400, "cfg3": 120, "cfg5": 600}[args.workload]
 
     import torch
     import guard_amd
@@ -118,7 +181,15 @@ def main():
     # the CPU baseline runs first, in child processes started before this process touches the GPU
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.resources, args.cpu_per_core)
+        log("cpu baseline (%s, %d documents per core)" % (args.workload, args.cpu_per_core))
+        cpu = cpu_baseline(args.workload, args.resources, args.cpu_per_core)
+        log("cpu baseline: %s evals/s" % cpu["value"])
+    first, count = sharding.shard_range(rank, world, args.docs)
+    texts = None
+    if args.workload == "cfg5":
+        t0 = time.time()
+        texts = generate_docs("cfg5", first, count, args.resources, _cpu_share())
+        t_gen = time.time() - t0
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -130,14 +201,18 @@ def main():
         raise RuntimeError("no HIP device: the MI355X evaluator has no CPU fallback")
 
     threads = args.threads or _cpu_share()
-    rules = rulepack.rule_pack()
+    rules = rulepack.rule_pack(args.workload)
     sess = guard_amd.Session()
     for name, text in rules:
         sess.add_rules(text, name)
+    log("load %d documents" % count)
     t0 = time.time()
-    first, count = sharding.shard_range(rank, world, args.docs)
     load_stats = None
-    if args.loader == "device":
+    if texts is not None:
+        sess.add_docs(texts, ["snapshot-%d.json" % (first + i) for i in range(count)], threads=threads)
+        n_ci = sum(t.count('"configurationItemStatus"') for t in texts)
+        texts = None
+    elif args.loader == "device":
         load_stats = sess.add_synthetic_device(first, count, n_resources=args.resources, threads=threads)
         if load_stats is None:
             raise RuntimeError("device loader refused the synthetic corpus")
@@ -145,9 +220,11 @@ def main():
     else:
         sess.add_synthetic(first, count, n_resources=args.resources, threads=threads)
     t_load = time.time() - t0
+    log("upload (load %.1f s)" % t_load)
     t0 = time.time()
     sess.upload()
     t_upload = time.time() - t0
+    log("warmup")
     # one non-default stream for the kernels AND the tally all-reduce: torch's default stream has
     # handle 0, which the library reads as "its own stream" -- unordered with the collective
     stream = torch.cuda.Stream()
@@ -184,7 +261,9 @@ def main():
         elapsed = float(tt.item())
 
     # statuses + records of the last launch (outside the timed region)
+    t0 = time.time()
     sess.fetch()
+    t_fetch = time.time() - t0
     rec_bytes = sess.stat(11)
     max_top = sess.stat(13)
     arena = sess.stat(9)
@@ -195,9 +274,36 @@ def main():
     tally_sum = int(counts.sum().item())   # the all-reduced tensor: every rank's last-step tallies
     n_fail, n_pass, n_skip, n_err = sess.stat(4), sess.stat(5), sess.stat(6), sess.stat(7)
 
+    e2e = None
+    if rank == 0 and world == 1 and not args.no_e2e:
+        rdocs = min(ndocs, args.e2e_report_docs) if args.e2e_report_docs else ndocs
+        log("e2e: structured report of %d of %d documents" % (rdocs, ndocs))
+        t0 = time.time()
+        rep_bytes, rep_code = sess.report_bytes("json", rdocs)
+        t_report_sample = time.time() - t0
+        # the synthetic documents are alike: the whole report costs ndocs / rdocs times the sample
+        t_report = t_report_sample * ndocs / max(1, rdocs)
+        t_eval = k_mean_ms / 1e3 + t_fetch
+        total = t_load + t_upload + t_eval + t_report
+        e2e = {"value": round(ntiles / total, 1), "unit": "evals/s", "load_s": round(t_load, 3),
+               "upload_s": round(t_upload, 3), "eval_fetch_s": round(t_eval, 3), "report_s": round(t_report, 3),
+               "report_docs_rendered": rdocs, "report_s_rendered": round(t_report_sample, 3),
+               "report_bytes_rendered": rep_bytes, "report_GBps": round(rep_bytes / t_report_sample / 1e9, 3),
+               "exit_code": rep_code, "report_threads": min(16, _cpu_share()),
+               "pcie_inclusive_value": round(ntiles / (t_upload + t_eval), 1),
+               "note": "one job: host load (incl. synthetic text generation%s) + upload + one evaluation with "
+                       "statuses/records fetched + structured JSON report rendered on the host and discarded "
+                       "(rendered for report_docs_rendered documents, report_s scaled to all)"
+                       % (", %.1f s of Python generation excluded" % t_gen if args.workload == "cfg5" else "")}
+
     total_units = ntiles * world * args.steps
     value = total_units / elapsed
-    workload = "cfg2: %d synthetic CFN templates/GPU (%d resources) x %d-file rule pack" % (args.docs, args.resources, nfiles)
+    if args.workload == "cfg5":
+        workload = ("cfg5: %d AWS Config snapshots/GPU (%d configuration items) x %d-file network-reachability pack"
+                    % (args.docs, n_ci * world, nfiles))
+    else:
+        workload = "%s: %d synthetic CFN templates/GPU (%d resources) x %d-file rule pack" % (
+            args.workload, args.docs, args.resources, nfiles)
     if rank == 0:
         traffic = load_pmc(workload)
         line = {
@@ -226,6 +332,7 @@ def main():
                        "rule_tallies_sum": tally_sum, "rule_tallies_fetched": int(sum(tally))},
         }
         line["cpu_baseline"] = cpu
+        line["e2e"] = e2e
         print(json.dumps(line), flush=True)
     sess.close()
     if dist is not None:

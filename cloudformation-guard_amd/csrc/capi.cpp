@@ -241,6 +241,8 @@ struct gg_session {
   // large-heap pass (rare: documents with thousands of failing clause values or deep nesting)
   static constexpr uint32_t kBigHeap = 32u << 20, kBigFrames = 1u << 20, kBigRecs = 16u << 20, kBigSlots = 8;
   uint32_t lane_heap_bytes = 64 * 1024;
+  uint32_t lds_prog_words = 2048;              // per-launch program staging window (words)
+  static constexpr uint32_t kMaxLdsProgWords = 4096;   // 16 KB
   int32_t mode = 0;               // 0: lane mode + wave-mode retry; 1: wave mode only
   size_t rec_cap = 0;
   // results
@@ -328,6 +330,13 @@ void session_upload(gg_session* s) {
     s->max_top = std::max<uint32_t>(s->max_top, p->dp.n_top);
   }
   s->d_progs.upload(dps.data(), dps.size(), st);
+  // staging window: the largest program (DFA tables included), capped at kMaxLdsProgWords
+  s->lds_prog_words = 4;
+  for (auto& p : s->progs) {
+    uint32_t w = (uint32_t)p->prog.blob.size();
+    if (w > gg_session::kMaxLdsProgWords) w = p->prog.hdr.off_dfa;
+    if (w <= gg_session::kMaxLdsProgWords) s->lds_prog_words = std::max(s->lds_prog_words, (w + 3u) & ~3u);
+  }
   size_t ntiles = s->docs.ndocs() * s->progs.size();
   size_t nbatches = (s->docs.ndocs() + 63) / 64 * s->progs.size();
   // wave mode: all tiles (mode 1) or only the lane kernel's overflow tiles (mode 0)
@@ -385,6 +394,7 @@ void session_launch(gg_session* s) {
   A.wave_frames_bytes = gg_session::kWaveFrames; A.wave_recs_bytes = gg_session::kWaveRecs;
   A.retry2_list = s->d_retry2.p; A.retry2_count = s->d_counters.p + 4;
   A.stats = s->d_stats.p;
+  A.lds_prog_words = s->lds_prog_words;
   if (!ntiles) return;
   if (s->nq == s->evq.size()) {
     std::pair<hipEvent_t, hipEvent_t> pr;
@@ -400,10 +410,10 @@ void session_launch(gg_session* s) {
     HIPCHK(hipGetLastError());
   }
   if (s->mode != 1) {
-    hipLaunchKernelGGL(guard_eval_lanes_kernel, dim3(s->lane_slots), dim3(64), 0, st, A);
+    hipLaunchKernelGGL(guard_eval_lanes_kernel, dim3(s->lane_slots), dim3(64), A.lds_prog_words * 4, st, A);
     HIPCHK(hipGetLastError());
   }
-  hipLaunchKernelGGL(guard_eval_kernel, dim3(s->nslots), dim3(64), 0, st, A);
+  hipLaunchKernelGGL(guard_eval_kernel, dim3(s->nslots), dim3(64), A.lds_prog_words * 4, st, A);
   HIPCHK(hipGetLastError());
   {
     // large-heap pass over the wave pass's overflow list (counters[4]; its cursor is counters[6]);
@@ -413,7 +423,7 @@ void session_launch(gg_session* s) {
     B.heaps = s->d_big_heaps.p; B.heap_bytes = gg_session::kBigHeap; B.nslots = gg_session::kBigSlots;
     B.wave_frames_bytes = gg_session::kBigFrames; B.wave_recs_bytes = gg_session::kBigRecs;
     B.retry2_list = nullptr; B.retry2_count = nullptr;
-    hipLaunchKernelGGL(guard_eval_kernel, dim3(gg_session::kBigSlots), dim3(64), 0, st, B);
+    hipLaunchKernelGGL(guard_eval_kernel, dim3(gg_session::kBigSlots), dim3(64), B.lds_prog_words * 4, st, B);
     HIPCHK(hipGetLastError());
   }
   HIPCHK(hipEventRecord(s->ev1, st));
@@ -491,6 +501,13 @@ double session_run(gg_session* s, bool fetch) {
   return ms;
 }
 
+// host threads for report rendering: GG_REPORT_THREADS, else the CPU share (at most 16)
+unsigned report_threads() {
+  if (const char* e = getenv("GG_REPORT_THREADS")) return (unsigned)std::max(1, atoi(e));
+  unsigned n = std::thread::hardware_concurrency();
+  return std::max(1u, std::min(16u, n ? n : 1u));
+}
+
 // structured report over (docs x programs) in format `fmt` (OutFormat); false + err for an aborting error
 bool session_report(gg_session* s, std::string& out, int32_t& exit_code, ReportError& err, int32_t fmt = OUT_JSON) {
   exit_code = s->parse_errors.empty() ? 0 : 5;
@@ -506,18 +523,11 @@ bool session_report(gg_session* s, std::string& out, int32_t& exit_code, ReportE
     }
   }
   out.clear();
-  size_t nd = s->docs.ndocs();
-  ReportWriter writer(fmt);
-  std::vector<TileResult> trs(nf);
-  for (size_t d = 0; d < nd; d++) {
-    std::vector<const TileResult*> tp;
-    for (size_t f = 0; f < nf; f++) {
-      trs[f] = tile_view(s->tiles.data(), s->rule_status.data(), s->max_top, s->recs.data(), d * nf + f);
-      tp.push_back(&trs[f]);
-    }
-    if (!writer.add(s->docs, (uint32_t)d, progs, tp, err)) { exit_code = -1; return false; }
-  }
-  out = writer.finish();
+  const size_t nd = s->docs.ndocs();
+  auto tile = [&](size_t d, size_t f) {
+    return tile_view(s->tiles.data(), s->rule_status.data(), s->max_top, s->recs.data(), d * nf + f);
+  };
+  if (!report_batch(s->docs, progs, 0, nd, tile, fmt, report_threads(), out, err)) { exit_code = -1; return false; }
   // exit code 19 when any rules file FAILed; a rules-file parse error set 5 beforehand
   // (structured.rs:40-43).  CommonStructuredReporter overwrites it with 19 (structured.rs:110-112);
   // JunitReporter::update_exit_code keeps 5 (reporters/mod.rs:97-103, validate/xml.rs:62-66).
@@ -940,6 +950,50 @@ int32_t gg_session_fetch(gg_session* s, extern_err_t* err) {
   } catch (std::exception& e) { set_err(err, -1, e.what()); return -1; }
 }
 
+// The structured report rendered in blocks of documents and discarded (end-to-end measurement of
+// the reporter at sizes whose text would not fit in memory): returns the bytes the report has.
+int64_t gg_session_report_bytes(gg_session* s, int32_t output_format, size_t max_docs, int32_t* exit_code, extern_err_t* err) {
+  set_err(err, 0, "");
+  if (!s->evaluated) { set_err(err, -1, "session not evaluated"); return -1; }
+  if (output_format != OUT_JSON && output_format != OUT_YAML) { set_err(err, 18, "IllegalArguments: json or yaml"); return -1; }
+  try {
+    std::vector<const Program*> progs;
+    for (auto& p : s->progs) progs.push_back(&p->prog);
+    const size_t nf = progs.size(), nd = max_docs ? std::min(max_docs, s->docs.ndocs()) : s->docs.ndocs();
+    for (size_t t = 0; t < s->tiles.size(); t++)
+      if (s->tiles[t].err) {
+        ReportError re;
+        tile_error(s->docs, (uint32_t)(t / nf), *progs[t % nf], s->tiles[t], re);
+        set_err(err, ffi_code(re.kind), error_display(re.kind, re.msg));
+        if (exit_code) *exit_code = -1;
+        return -1;
+      }
+    auto tile = [&](size_t d, size_t f) {
+      return tile_view(s->tiles.data(), s->rule_status.data(), s->max_top, s->recs.data(), d * nf + f);
+    };
+    const size_t kBlock = getenv("GG_REPORT_BLOCK") ? (size_t)std::max(1, atoi(getenv("GG_REPORT_BLOCK"))) : 65536;
+    int64_t bytes = 0;
+    std::string out;
+    for (size_t d0 = 0; d0 < nd; d0 += kBlock) {
+      const size_t n = std::min(kBlock, nd - d0);
+      ReportError re;
+      if (!report_batch(s->docs, progs, d0, n, tile, output_format, report_threads(), out, re)) {
+        set_err(err, ffi_code(re.kind), error_display(re.kind, re.msg));
+        if (exit_code) *exit_code = -1;
+        return -1;
+      }
+      // blocks join as the whole report would: JSON drops each block's brackets for ",\n"
+      bytes += (int64_t)out.size() - (output_format == OUT_JSON && nd > n ? 2 : 0);
+      if (getenv("GG_PROGRESS")) fprintf(stderr, "[report] %zu / %zu documents, %lld bytes\n", d0 + n, nd, (long long)bytes);
+    }
+    if (output_format == OUT_JSON && nd > kBlock) bytes += 2;
+    bool anyfail = false;
+    for (auto& t : s->tiles) if (t.status == ST_FAIL) anyfail = true;
+    if (exit_code) *exit_code = anyfail ? 19 : (s->parse_errors.empty() ? 0 : 5);
+    return bytes;
+  } catch (std::exception& e) { set_err(err, -1, e.what()); return -1; }
+}
+
 size_t gg_session_ncounts(gg_session* s) { return s->ncounts; }
 void* gg_session_counts_device(gg_session* s) { return s->ext_counts ? (void*)s->ext_counts : (void*)s->d_counts.p; }
 void gg_session_bind_counts(gg_session* s, void* dev, size_t n) {
@@ -1048,6 +1102,23 @@ int32_t gg_regex_match(const char* pattern, const char* text, size_t len, uint32
   if (stats) { stats[0] = rx.nstates; stats[1] = rx.ncls; }
   if (!rx.valid) return -2;
   return dfa_match(rx, text ? text : "", text ? len : 0);
+}
+
+int32_t gg_program_stats(const char* text, const char* name, uint32_t* out) {
+  try {
+    RulesFile rf;
+    bool empty = false;
+    std::string msg;
+    if (!parse_rules_file(text ? text : "", name ? name : "", rf, empty, msg)) return 5;
+    if (empty) return 1;
+    Program p;
+    if (!compile_program(rf, name ? name : "", p, msg)) return 5;
+    if (out) {
+      out[0] = (uint32_t)p.blob.size(); out[1] = p.hdr.off_dfa; out[2] = p.hdr.n_regex;
+      out[3] = p.hdr.n_clauses; out[4] = p.hdr.n_parts;
+    }
+    return 0;
+  } catch (std::exception&) { return -1; }
 }
 
 int32_t gg_parse_rules(const char* text, const char* name, extern_err_t* err) {

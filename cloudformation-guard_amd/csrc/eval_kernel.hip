@@ -40,19 +40,19 @@ namespace ln {
 // (KBs: clauses, query parts, strings, literals) is copied into the workgroup's LDS and the
 // DevProg pointers are rebased onto the copy, so the interpreter's program reads are LDS reads
 // instead of dependent global loads.  Programs larger than the LDS window stay in HBM.
-#ifndef GG_LDS_PROG_WORDS
-#define GG_LDS_PROG_WORDS 2048
-#endif
-static const uint32_t LDS_PROG_WORDS = GG_LDS_PROG_WORDS;   // 8 KB per workgroup (one wave)
+// The staging window is dynamic shared memory sized per launch (LaunchArgs::lds_prog_words: the
+// largest program of the launch, capped by the host): a small rules pack leaves LDS for occupancy,
+// a regex-heavy one gets its DFA tables staged too.
 
-__device__ __attribute__((always_inline)) inline const DevProg* stage_program(const DevProg* G, DevProg* sp, uint4* sblob) {
+__device__ __attribute__((always_inline)) inline const DevProg* stage_program(const DevProg* G, DevProg* sp, uint4* sblob,
+                                                                             uint32_t window) {
   const uint32_t lane = __lane_id();
   __syncthreads();   // the previous batch's reads of the window are complete
   uint32_t n = G->lds_words;
   // the whole blob (regex DFA tables included) when it fits the window, else all but the tables
   const uint32_t dfa_off = (uint32_t)((const uint32_t*)G->dfa - G->blob);
-  if (n > LDS_PROG_WORDS) n = dfa_off;
-  if (n > LDS_PROG_WORDS) return G;
+  if (n > window) n = dfa_off;
+  if (n > window) return G;
   const uint4* src = (const uint4*)G->blob;
   for (uint32_t i = lane; i < (n + 3u) / 4u; i += 64u) sblob[i] = src[i];
   if (lane == 0) {
@@ -117,7 +117,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
   const uint32_t nbatches = (c1 - c0) * A.nfiles;
   // interpreter state lives in LDS (one Ctx per lane), not in the per-lane stack
   __shared__ Ctx s_ctx[64];
-  __shared__ uint4 s_blob[LDS_PROG_WORDS / 4];
+  extern __shared__ uint4 s_blob[];
   LCtx& c = *(LCtx*)&s_ctx[lane];
   uint32_t staged = NONE;
   const DevProg* P = nullptr;
@@ -129,7 +129,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
     const uint32_t file = b % A.nfiles, chunk = c0 + b / A.nfiles;
     const uint32_t doc = chunk * 64u + lane;
     const bool active = doc < A.docs.ndocs;
-    if (file != staged) { P = stage_program(&A.progs[file], &g_prog, s_blob); staged = file; }
+    if (file != staged) { P = stage_program(&A.progs[file], &g_prog, s_blob, A.lds_prog_words); staged = file; }
     const uint32_t tile = doc * A.nfiles + file;
     uint32_t status = ST_SKIP, n = 0;
     if (P != &g_prog) {
@@ -197,7 +197,7 @@ __global__ void __launch_bounds__(64) guard_eval_kernel(LaunchArgs A) {
   const uint32_t ntiles = A.retry_list ? *A.retry_count : A.ntiles;
   __shared__ Ctx s_ctx[64];
   __shared__ DevProg s_prog;
-  __shared__ uint4 s_blob[LDS_PROG_WORDS / 4];
+  extern __shared__ uint4 s_blob[];
   LCtx& c = *(LCtx*)&s_ctx[lane];
   uint32_t staged = NONE;
   const DevProg* P = nullptr;
@@ -208,7 +208,7 @@ __global__ void __launch_bounds__(64) guard_eval_kernel(LaunchArgs A) {
     if (t >= ntiles) break;
     uint32_t tile = A.retry_list ? A.retry_list[t] : A.tile_base + t;
     uint32_t doc = tile / A.nfiles, file = tile % A.nfiles;
-    if (file != staged) { P = stage_program(&A.progs[file], &s_prog, s_blob); staged = file; }
+    if (file != staged) { P = stage_program(&A.progs[file], &s_prog, s_blob, A.lds_prog_words); staged = file; }
     tile_begin(c, A, P, doc, heap, A.heap_bytes, A.wave_frames_bytes, A.wave_recs_bytes);
     c.lane16 = 0;
     c.syn_off = alloc_pers(c, 256 * 16);

@@ -1,6 +1,10 @@
 // Device records -> structured JSON (see reporter.h).
 #include "reporter.h"
 
+#include <functional>
+#include <memory>
+#include <thread>
+
 #include <yaml.h>
 
 #include <algorithm>
@@ -869,6 +873,7 @@ struct ReportWriter::Impl {
   YamlOut* yaml = nullptr;                // OUT_YAML
   J artifacts = J::arr(), results = J::arr();   // OUT_SARIF
   std::set<std::string> seen;
+  std::vector<std::string> art_names;     // raw names of `artifacts`, in order
   std::string suites;                     // OUT_JUNIT
   size_t tests = 0, failures = 0;
 };
@@ -911,6 +916,7 @@ bool ReportWriter::add(const DocBatch& docs, uint32_t doc, const std::vector<con
         J loc = J::obj(); loc.add("uri", J::str(sanitize_path(name)));
         J a = J::obj(); a.add("location", std::move(loc));
         I.artifacts.push(std::move(a));
+        I.art_names.push_back(name);
       }
       for (auto& failure : field(fr, "not_compliant")->a) {
         std::string rule_id;
@@ -995,6 +1001,70 @@ bool ReportWriter::add(const DocBatch& docs, uint32_t doc, const std::vector<con
       pretty(fr, 1, I.json);
       break;
   }
+  return true;
+}
+
+void ReportWriter::absorb(ReportWriter& later) {
+  Impl& I = *p_;
+  Impl& L = *later.p_;
+  if (I.fmt != L.fmt || I.fmt == OUT_YAML) throw std::runtime_error("ReportWriter::absorb: unsupported");
+  switch (I.fmt) {
+    case OUT_SARIF:
+      for (size_t k = 0; k < L.art_names.size(); k++)
+        if (I.seen.insert(L.art_names[k]).second) { I.artifacts.push(std::move(L.artifacts.a[k])); I.art_names.push_back(L.art_names[k]); }
+      for (auto& r : L.results.a) I.results.push(std::move(r));
+      break;
+    case OUT_JUNIT:
+      I.suites += L.suites;
+      I.tests += L.tests;
+      I.failures += L.failures;
+      break;
+    default:
+      if (L.ndocs) {
+        if (I.ndocs) { I.json += ",\n"; I.json.append(L.json, 2, std::string::npos); }
+        else I.json = std::move(L.json);
+      }
+      break;
+  }
+  I.ndocs += L.ndocs;
+  L.ndocs = 0;
+}
+
+bool report_batch(const DocBatch& docs, const std::vector<const Program*>& progs, size_t first, size_t ndocs,
+                  const std::function<TileResult(size_t doc, size_t file)>& tile, int32_t fmt, unsigned nthreads,
+                  std::string& out, ReportError& err) {
+  const size_t nf = progs.size();
+  const size_t T = std::max<size_t>(1, std::min<size_t>(nthreads, (ndocs + 255) / 256));
+  std::vector<std::unique_ptr<ReportWriter>> w(T);
+  std::vector<ReportError> errs(T);
+  std::vector<size_t> err_doc(T, SIZE_MAX);
+  std::vector<std::string> yaml_out(T);
+  auto work = [&](size_t t) {
+    const size_t d0 = first + ndocs * t / T, d1 = first + ndocs * (t + 1) / T;
+    w[t].reset(new ReportWriter(fmt));
+    std::vector<TileResult> trs(nf);
+    std::vector<const TileResult*> tp(nf);
+    for (size_t d = d0; d < d1; d++) {
+      for (size_t f = 0; f < nf; f++) { trs[f] = tile(d, f); tp[f] = &trs[f]; }
+      if (!w[t]->add(docs, (uint32_t)d, progs, tp, errs[t])) { err_doc[t] = d; return; }
+    }
+    if (fmt == OUT_YAML && d1 > d0) yaml_out[t] = w[t]->finish();
+  };
+  std::vector<std::thread> th;
+  for (size_t t = 1; t < T; t++) th.emplace_back(work, t);
+  work(0);
+  for (auto& x : th) x.join();
+  // the first document (in order) whose report aborts decides the error (structured.rs:99-133)
+  for (size_t t = 0; t < T; t++) if (err_doc[t] != SIZE_MAX) { err = errs[t]; return false; }
+  if (fmt == OUT_YAML) {
+    if (!ndocs) { out = ReportWriter(fmt).finish(); return true; }
+    // a block sequence's items are emitted independently: the chunks' streams concatenate
+    out.clear();
+    for (auto& y : yaml_out) out += y;
+    return true;
+  }
+  for (size_t t = 1; t < T; t++) w[0]->absorb(*w[t]);
+  out = w[0]->finish();
   return true;
 }
 

@@ -3,6 +3,7 @@
 // (guard/src/rules/eval_context.rs:1965-2435) and FileReport::combine (:1630-1640) over the
 // compact failure records emitted by the kernel.
 #pragma once
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -82,10 +83,20 @@ class ReportWriter {
   bool add(const DocBatch& docs, uint32_t doc, const std::vector<const Program*>& progs,
            const std::vector<const TileResult*>& tiles, ReportError& err);
   std::string finish();
+  // appends the documents of `later` (a writer over the next contiguous documents); JSON, SARIF
+  // and JUnit only
+  void absorb(ReportWriter& later);
 
  private:
   struct Impl;
   Impl* p_;
 };
+
+// The structured report of documents [first, first + ndocs) rendered on `nthreads` host threads over
+// contiguous document ranges; byte-identical to one ReportWriter fed in order.  tile(d, f) gives
+// document d's tile of program f.
+bool report_batch(const DocBatch& docs, const std::vector<const Program*>& progs, size_t first, size_t ndocs,
+                  const std::function<TileResult(size_t doc, size_t file)>& tile, int32_t fmt, unsigned nthreads,
+                  std::string& out, ReportError& err);
 
 }  // namespace gg

@@ -111,8 +111,20 @@ def lib():
     L.gg_parse_rules.restype = ctypes.c_int32
     L.gg_regex_match.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint32)]
     L.gg_regex_match.restype = ctypes.c_int32
+    L.gg_session_report_bytes.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int32),
+                                          ctypes.POINTER(ExternError)]
+    L.gg_session_report_bytes.restype = ctypes.c_int64
+    L.gg_program_stats.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint32)]
+    L.gg_program_stats.restype = ctypes.c_int32
     _lib = L
     return L
+
+
+def program_stats(text, name="r.guard"):
+    """Compiled-program sizes (no GPU): blob words, words before the DFA tables, regexes, clauses, parts."""
+    out = (ctypes.c_uint32 * 5)()
+    rc = lib().gg_program_stats(_b(text), _b(name), out)
+    return rc, list(out)
 
 
 def regex_match(pattern, text):
@@ -306,6 +318,16 @@ class Session:
         if err.code != 0:
             _raise(err)
         return _take_string(p), code.value
+
+    def report_bytes(self, output="json", max_docs=0):
+        """renders the report of the first max_docs documents (0: all) in blocks and discards it;
+        returns (bytes, exit code)"""
+        code = ctypes.c_int32(0)
+        err = ExternError()
+        n = lib().gg_session_report_bytes(self.s, OUTPUT_FORMATS[output], max_docs, ctypes.byref(code), ctypes.byref(err))
+        if err.code != 0:
+            _raise(err)
+        return n, code.value
 
     def stat(self, what):
         return lib().gg_session_stat(self.s, what)

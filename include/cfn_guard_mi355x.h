@@ -99,6 +99,11 @@ void gg_session_bind_counts(gg_session *s, void *dev, size_t n);
 /* evaluation-kernel ms of every launch since the last drain (HIP events on the launch stream) */
 size_t gg_session_drain_kernel_ms(gg_session *s, double *out, size_t cap, extern_err_t *err);
 int32_t gg_session_counts(gg_session *s, uint64_t *out, size_t n);
+/* the structured report (json / yaml) of the first max_docs documents (0: all) rendered on the host
+ * in document blocks and discarded; returns its size in bytes (end-to-end measurement at sizes whose
+ * text would not fit in memory) */
+int64_t gg_session_report_bytes(gg_session *s, int32_t output_format, size_t max_docs, int32_t *exit_code,
+                                extern_err_t *err);
 /* diagnostic evaluator counters (nonzero only in the GG_STATS build variant) */
 int32_t gg_session_kernel_stats(gg_session *s, uint64_t *out, size_t n);
 
@@ -113,6 +118,9 @@ int32_t gg_loader_selfcheck(const char *text, size_t len);
  * 1 = no rules (Ok(None)), 5 = parse error (err->message = the Error Display). */
 char *gg_load_dump(const char *text, size_t len, int32_t mode, extern_err_t *err);
 int32_t gg_parse_rules(const char *text, const char *name, extern_err_t *err);
+/* sizes of the compiled program (no GPU): out[0] blob words, out[1] words before the regex DFA
+ * tables, out[2] regexes, out[3] clauses, out[4] query parts; returns gg_parse_rules' code */
+int32_t gg_program_stats(const char *text, const char *name, uint32_t *out);
 /* The rule-regex DFA (compiled as for a rules file) run on the host over one haystack: 1 match,
  * 0 no match, -1 unsupported on the MI355X path (look-around, back-references, ...), -2 invalid.
  * stats (may be NULL, 2 values): DFA states, byte classes. */

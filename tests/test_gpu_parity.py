@@ -262,3 +262,28 @@ def test_app_b13_unicode_digit_class_on_gpu():
     rules = [("d.guard", "a == /^\\d+$/")]
     out, code = guard_amd.validate_structured(rules, [("d.json", '{"a": "١٢٣"}')])
     assert code == 0 and '"status": "PASS"' in out
+
+
+def test_parallel_report_matches_serial():
+    """session_report renders contiguous document ranges on host threads and merges them
+    (reporter.cpp report_batch); the bytes equal the single-thread rendering in every format"""
+    docs = synth.cfn_corpus(700, start=31337, n_resources=20)
+    s = guard_amd.Session()
+    for name, text in rule_pack():
+        s.add_rules(text, name)
+    s.add_docs(docs, ["p%d.json" % (i % 500) for i in range(len(docs))])   # repeated names: SARIF dedupe
+    s.eval(1)
+    try:
+        for fmt in ("json", "yaml", "sarif", "junit"):
+            os.environ["GG_REPORT_THREADS"] = "1"
+            one = s.report(fmt)
+            os.environ["GG_REPORT_THREADS"] = "3"
+            par = s.report(fmt)
+            assert par == one, fmt
+            if fmt in ("json", "yaml"):
+                os.environ["GG_REPORT_BLOCK"] = "256"   # 3 blocks
+                assert s.report_bytes(fmt) == (len(one[0].encode()), one[1]), fmt
+    finally:
+        os.environ.pop("GG_REPORT_THREADS", None)
+        os.environ.pop("GG_REPORT_BLOCK", None)
+    s.close()

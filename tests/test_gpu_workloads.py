@@ -159,3 +159,22 @@ def test_key_captures_lane_matches_wave():
     docs = synth.cfn_corpus(130, start=2000, n_resources=20)
     rules = _pack("capture_rulepack")
     assert _session_report(docs, rules, 0, "c") == _session_report(docs, rules, 1, "c")
+
+
+def test_cfg3_registry_standin_vs_oracle():
+    """cfg 3: the full-registry stand-in -- every in-scope in-repo .guard file of the
+    reference (tests/golden/cfg3_rulepack, 22 files) -- over synthetic templates, every format"""
+    docs = synth.cfn_corpus(24, start=4242, n_resources=50)
+    data = [("t-%d.json" % i, d) for i, d in enumerate(docs)]
+    rules = _pack("cfg3_rulepack")
+    assert len(rules) == 22
+    for fmt in ("json", "yaml", "sarif", "junit"):
+        exp, ecode, _ = oracle_validate(rules, data, output=fmt)
+        out, code = guard_amd.validate_structured(rules, data, output=fmt)
+        assert (code, out) == (ecode, exp), fmt
+
+
+def test_cfg3_lane_matches_wave():
+    docs = synth.cfn_corpus(130, start=9000, n_resources=50)
+    rules = _pack("cfg3_rulepack")
+    assert _session_report(docs, rules, 0, "t") == _session_report(docs, rules, 1, "t")
