@@ -107,16 +107,23 @@ template <class T>
 struct DBuf {
   T* p = nullptr;
   size_t n = 0;
+  size_t cap = 0;
+  // ensures room for `count` elements (contents undefined); an allocation large enough is kept, so
+  // pooled buffers serve later calls without hipMalloc / hipFree
   void alloc(size_t count) {
+    n = count;
+    if (count <= cap && p) return;
     release();
     n = count;
+    cap = count;
     if (count) HIPCHK(hipMalloc((void**)&p, count * sizeof(T)));
   }
   void upload(const T* src, size_t count, hipStream_t s) {
     alloc(count);
     if (count) HIPCHK(hipMemcpyAsync(p, src, count * sizeof(T), hipMemcpyHostToDevice, s));
   }
-  void release() { if (p) hipFree(p); p = nullptr; n = 0; }
+  void release() { if (p) hipFree(p); p = nullptr; n = 0; cap = 0; }
+  size_t bytes() const { return cap * sizeof(T); }
   ~DBuf() { release(); }
 };
 
@@ -195,14 +202,11 @@ struct GpuProgram {
   }
 };
 
-}  // namespace
-
-// ------------------------------------------------------------------ session ---
-struct gg_session {
-  DocBatch docs;
-  std::vector<std::unique_ptr<GpuProgram>> progs;
-  std::vector<std::string> parse_errors;   // rules files that failed to parse (exit code 5)
-  // device residency
+// Device state of one evaluation: arena, programs, scratch heaps, records, tallies, a stream and
+// launch events.  Borrowed by a session at upload and returned to a small pool when it ends, so
+// repeated FFI calls (guard-lambda, the fuzzers: one document per call) reuse allocations, events
+// and streams instead of hipMalloc'ing ~100 MB per call; concurrent callers each hold their own.
+struct DeviceBufs {
   DBuf<DNodeP> d_nodes;         // packed device arena
   DBuf<uint32_t> d_klen;        // per node key length (cold)
   DBuf<char> d_bytes;
@@ -211,12 +215,11 @@ struct gg_session {
   DBuf<uint32_t> d_res_map;     // per doc: root.Resources node (resource-type column, DevBatch)
   DBuf<uint32_t> d_tix_off;
   DBuf<uint32_t> d_tix;
-  uint32_t type_key = NONE;
   DBuf<DevProg> d_progs;
   DBuf<uint8_t> d_heaps;        // wave mode: one heap per wave slot
   DBuf<uint8_t> d_lane_heaps;   // lane mode: one heap per lane
   DBuf<uint32_t> d_retry;       // tiles handed from lane mode to wave mode
-  DBuf<uint8_t> d_big_heaps;    // large-heap wave pass: tiles that outgrow the wave heap
+  DBuf<uint8_t> d_big_heaps;    // large-heap wave pass (allocated the first time a tile needs it)
   DBuf<uint32_t> d_retry2;      // tiles handed from the wave pass to the large-heap pass
   DBuf<TileOut> d_tiles;
   DBuf<uint8_t> d_rule_status;
@@ -224,10 +227,61 @@ struct gg_session {
   DBuf<uint32_t> d_counters;
   DBuf<unsigned long long> d_counts;   // per (file, top rule) x {PASS, FAIL, SKIP, error}
   DBuf<unsigned long long> d_stats;    // diagnostic counters (stats build variant)
+  hipStream_t stream = nullptr;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> evq;   // launch brackets, reused
+  DeviceBufs() { HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking)); }
+  ~DeviceBufs() {
+    for (auto& pr : evq) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
+    if (stream) hipStreamDestroy(stream);
+  }
+  size_t bytes() const {
+    return d_nodes.bytes() + d_klen.bytes() + d_bytes.bytes() + d_roots.bytes() + d_base.bytes() + d_res_map.bytes() +
+           d_tix_off.bytes() + d_tix.bytes() + d_progs.bytes() + d_heaps.bytes() + d_lane_heaps.bytes() + d_retry.bytes() +
+           d_big_heaps.bytes() + d_retry2.bytes() + d_tiles.bytes() + d_rule_status.bytes() + d_recs.bytes() +
+           d_counters.bytes() + d_counts.bytes() + d_stats.bytes();
+  }
+};
+
+struct BufPool {
+  std::mutex mu;
+  std::vector<DeviceBufs*> free;
+  static constexpr size_t kMaxFree = 8;               // idle sets kept
+  static constexpr size_t kMaxKeepBytes = 1ull << 30; // larger sets (batch jobs) are freed, not kept
+};
+BufPool g_pool;
+
+DeviceBufs* acquire_bufs() {
+  {
+    std::lock_guard<std::mutex> lk(g_pool.mu);
+    if (!g_pool.free.empty()) { DeviceBufs* b = g_pool.free.back(); g_pool.free.pop_back(); return b; }
+  }
+  return new DeviceBufs();
+}
+
+void release_bufs(DeviceBufs* b) {
+  if (!b) return;
+  if (b->bytes() <= BufPool::kMaxKeepBytes) {
+    if (hipStreamSynchronize(b->stream) == hipSuccess) {
+      std::lock_guard<std::mutex> lk(g_pool.mu);
+      if (g_pool.free.size() < BufPool::kMaxFree) { g_pool.free.push_back(b); return; }
+    }
+  }
+  delete b;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ session ---
+struct gg_session {
+  DocBatch docs;
+  std::vector<std::unique_ptr<GpuProgram>> progs;
+  std::vector<std::string> parse_errors;   // rules files that failed to parse (exit code 5)
+  // device residency: buffers borrowed from the device-state pool at upload (DeviceBufs)
+  DeviceBufs* dv = nullptr;
+  uint32_t type_key = NONE;
   size_t ncounts = 0;
-  hipStream_t stream = nullptr;        // caller stream (e.g. torch's current stream); null = library stream
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;   // brackets of the most recent launch (= evq[nq - 1])
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> evq;   // one pair per launch since the last drain
+  hipStream_t stream = nullptr;        // caller stream (e.g. torch's current stream); null = the buffers' own stream
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;   // brackets of the most recent launch (= dv->evq[nq - 1])
   size_t nq = 0;
   unsigned long long* ext_counts = nullptr;   // caller-owned device tally buffer (RCCL all-reduce)
   bool launched = false;
@@ -252,9 +306,7 @@ struct gg_session {
   bool evaluated = false;
   double last_kernel_ms = 0;
   std::string last_error;
-  ~gg_session() {
-    for (auto& pr : evq) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
-  }
+  ~gg_session() { release_bufs(dv); }
 };
 
 namespace {
@@ -268,20 +320,21 @@ bool ensure_device(std::string& why) {
 }
 
 void session_upload(gg_session* s) {
-  hipStream_t st = g_dev.stream;
+  if (!s->dv) s->dv = acquire_bufs();
+  hipStream_t st = s->dv->stream;
   {
     // host arena (32 B nodes) -> device arena (16 B packed nodes + key-length column)
     const size_t n = s->docs.nodes.size();
     DBuf<DNode> tmp;
     tmp.upload(s->docs.nodes.data(), n, st);
-    s->d_nodes.alloc(std::max<size_t>(n, 1));
-    s->d_klen.alloc(std::max<size_t>(n, 1));
+    s->dv->d_nodes.alloc(std::max<size_t>(n, 1));
+    s->dv->d_klen.alloc(std::max<size_t>(n, 1));
     DBuf<uint32_t> bad;
     bad.alloc(1);
     HIPCHK(hipMemsetAsync(bad.p, 0, 4, st));
     if (n) {
       const uint32_t blocks = (uint32_t)std::min<size_t>((n + 255) / 256, (size_t)g_dev.ncu * 64);
-      hipLaunchKernelGGL(pack_nodes_kernel, dim3(blocks), dim3(256), 0, st, tmp.p, s->d_nodes.p, s->d_klen.p, (uint64_t)n, bad.p);
+      hipLaunchKernelGGL(pack_nodes_kernel, dim3(blocks), dim3(256), 0, st, tmp.p, s->dv->d_nodes.p, s->dv->d_klen.p, (uint64_t)n, bad.p);
       HIPCHK(hipGetLastError());
     }
     uint32_t b = 0;
@@ -290,9 +343,9 @@ void session_upload(gg_session* s) {
     if (b & 1u) throw std::runtime_error("a string or container is too large for the device arena (count >= 2^28)");
     if (b & 2u) throw std::runtime_error("arena invariant broken: a map entry's key offset is not its key id");
   }
-  s->d_bytes.upload(s->docs.bytes.data(), s->docs.bytes.size() ? s->docs.bytes.size() : 1, st);
-  s->d_roots.upload(s->docs.roots.data(), s->docs.roots.size(), st);
-  s->d_base.upload(s->docs.base.data(), s->docs.base.size(), st);
+  s->dv->d_bytes.upload(s->docs.bytes.data(), s->docs.bytes.size() ? s->docs.bytes.size() : 1, st);
+  s->dv->d_roots.upload(s->docs.roots.data(), s->docs.roots.size(), st);
+  s->dv->d_base.upload(s->docs.base.data(), s->docs.base.size(), st);
   {
     // resource-type column layout: root.Resources of every document and its entry count
     const DocBatch& D = s->docs;
@@ -316,9 +369,9 @@ void session_upload(gg_session* s) {
       }
     }
     if (total > 0xFFFFFFF0u) { std::fill(rmap.begin(), rmap.end(), NONE); total = 0; }
-    s->d_res_map.upload(rmap.data(), std::max<size_t>(nd, 1), st);
-    s->d_tix_off.upload(toff.data(), std::max<size_t>(nd, 1), st);
-    s->d_tix.alloc(std::max<size_t>(total, 1));
+    s->dv->d_res_map.upload(rmap.data(), std::max<size_t>(nd, 1), st);
+    s->dv->d_tix_off.upload(toff.data(), std::max<size_t>(nd, 1), st);
+    s->dv->d_tix.alloc(std::max<size_t>(total, 1));
     HIPCHK(hipStreamSynchronize(st));   // the host vectors above die at the end of this scope
   }
   std::vector<DevProg> dps;
@@ -329,7 +382,7 @@ void session_upload(gg_session* s) {
     dps.push_back(p->dp);
     s->max_top = std::max<uint32_t>(s->max_top, p->dp.n_top);
   }
-  s->d_progs.upload(dps.data(), dps.size(), st);
+  s->dv->d_progs.upload(dps.data(), dps.size(), st);
   // staging window: the largest program (DFA tables included), capped at kMaxLdsProgWords
   s->lds_prog_words = 4;
   for (auto& p : s->progs) {
@@ -343,66 +396,65 @@ void session_upload(gg_session* s) {
   size_t wave_slots = s->mode == 1 ? (size_t)g_dev.ncu * 8 : (size_t)g_dev.ncu * 2;
   uint32_t slots = (uint32_t)std::min<size_t>(std::max<size_t>(ntiles, 1), wave_slots);
   s->nslots = slots;
-  s->d_heaps.alloc((size_t)slots * s->heap_bytes);
+  s->dv->d_heaps.alloc((size_t)slots * s->heap_bytes);
   // lane-mode grid: waves per CU (default 8 = the kernel's occupancy at 2 waves/SIMD)
   size_t lane_waves_per_cu = 8;
   if (const char* e = getenv("GG_LANE_WAVES_PER_CU")) lane_waves_per_cu = std::max(1, atoi(e));
   s->lane_slots = s->mode == 1 ? 0 : (uint32_t)std::min<size_t>(std::max<size_t>(nbatches, 1), (size_t)g_dev.ncu * lane_waves_per_cu);
   // every one of the 8 per-XCD queues needs waves (block b serves queue b % 8)
   if (s->lane_slots) s->lane_slots = (std::max<uint32_t>(s->lane_slots, 8u) + 7u) & ~7u;
-  s->d_lane_heaps.alloc((size_t)s->lane_slots * 64 * s->lane_heap_bytes);
-  s->d_retry.alloc(std::max<size_t>(ntiles, 1));
-  s->d_retry2.alloc(std::max<size_t>(ntiles, 1));
-  s->d_big_heaps.alloc((size_t)gg_session::kBigSlots * gg_session::kBigHeap);
-  s->d_tiles.alloc(std::max<size_t>(ntiles, 1));
-  s->d_rule_status.alloc(std::max<size_t>(ntiles * s->max_top, 1));
+  s->dv->d_lane_heaps.alloc((size_t)s->lane_slots * 64 * s->lane_heap_bytes);
+  s->dv->d_retry.alloc(std::max<size_t>(ntiles, 1));
+  s->dv->d_retry2.alloc(std::max<size_t>(ntiles, 1));
+  s->dv->d_tiles.alloc(std::max<size_t>(ntiles, 1));
+  s->dv->d_rule_status.alloc(std::max<size_t>(ntiles * s->max_top, 1));
   s->rec_cap = std::min<size_t>(std::max<size_t>(ntiles * 48, 4096), (size_t)96 * 1024 * 1024);
-  s->d_recs.alloc(s->rec_cap);
-  s->d_counters.alloc(32);   // [0..6] cursors / counts, [16..23] per-XCD lane-mode queues
-  s->d_stats.alloc(16);
-  HIPCHK(hipMemsetAsync(s->d_stats.p, 0, 16 * sizeof(unsigned long long), st));
+  s->dv->d_recs.alloc(s->rec_cap);
+  s->dv->d_counters.alloc(32);   // [0..6] cursors / counts, [16..23] per-XCD lane-mode queues
+  s->dv->d_stats.alloc(16);
+  HIPCHK(hipMemsetAsync(s->dv->d_stats.p, 0, 16 * sizeof(unsigned long long), st));
   s->ncounts = s->progs.size() * (s->max_top + 1) * 4;
   if (s->ncounts * sizeof(uint32_t) > 60 * 1024)
     throw std::runtime_error("too many (rules file x rule) tallies for one LDS block; split the rules files across sessions");
-  s->d_counts.alloc(std::max<size_t>(s->ncounts, 1));
+  s->dv->d_counts.alloc(std::max<size_t>(s->ncounts, 1));
   HIPCHK(hipStreamSynchronize(st));
   s->uploaded = true;
 }
 
-hipStream_t session_stream(gg_session* s) { return s->stream ? s->stream : g_dev.stream; }
+hipStream_t session_stream(gg_session* s) { return s->stream ? s->stream : s->dv->stream; }
 
 // enqueues one evaluation of every tile (and the per-rule tally) on the session stream; no host sync
 void session_launch(gg_session* s) {
   hipStream_t st = session_stream(s);
   uint32_t ntiles = (uint32_t)(s->docs.ndocs() * s->progs.size());
-  HIPCHK(hipMemsetAsync(s->d_counters.p, 0, 32 * sizeof(uint32_t), st));
-  unsigned long long* counts = s->ext_counts ? s->ext_counts : s->d_counts.p;
+  HIPCHK(hipMemsetAsync(s->dv->d_counters.p, 0, 32 * sizeof(uint32_t), st));
+  unsigned long long* counts = s->ext_counts ? s->ext_counts : s->dv->d_counts.p;
   HIPCHK(hipMemsetAsync(counts, 0, s->ncounts * sizeof(unsigned long long), st));
   LaunchArgs A{};
-  A.docs.nodes = s->d_nodes.p; A.docs.klen = s->d_klen.p; A.docs.bytes = s->d_bytes.p; A.docs.roots = s->d_roots.p; A.docs.base = s->d_base.p; A.docs.ndocs = (uint32_t)s->docs.ndocs();
-  A.docs.res_map = s->d_res_map.p; A.docs.tix_off = s->d_tix_off.p; A.docs.tix = s->d_tix.p; A.docs.type_key = s->type_key;
-  A.progs = s->d_progs.p; A.nfiles = (uint32_t)s->progs.size();
+  A.docs.nodes = s->dv->d_nodes.p; A.docs.klen = s->dv->d_klen.p; A.docs.bytes = s->dv->d_bytes.p; A.docs.roots = s->dv->d_roots.p; A.docs.base = s->dv->d_base.p; A.docs.ndocs = (uint32_t)s->docs.ndocs();
+  A.docs.res_map = s->dv->d_res_map.p; A.docs.tix_off = s->dv->d_tix_off.p; A.docs.tix = s->dv->d_tix.p; A.docs.type_key = s->type_key;
+  A.progs = s->dv->d_progs.p; A.nfiles = (uint32_t)s->progs.size();
   A.ntiles = ntiles; A.tile_base = 0;
-  A.heaps = s->d_heaps.p; A.heap_bytes = s->heap_bytes; A.nslots = s->nslots;
-  A.tiles = s->d_tiles.p; A.rule_status = s->d_rule_status.p; A.max_top = s->max_top;
-  A.recs = s->d_recs.p; A.rec_cap = (uint32_t)s->rec_cap;
-  A.rec_cursor = s->d_counters.p; A.tile_cursor = s->d_counters.p + 1;   // [1] lane batches, [2] wave tiles
-  A.retry_count = s->d_counters.p + 3;
-  A.xcd_cursor = s->d_counters.p + 16;
-  A.lane_heaps = s->d_lane_heaps.p; A.lane_heap_bytes = s->lane_heap_bytes;
-  A.retry_list = s->mode == 1 ? nullptr : s->d_retry.p;
+  A.heaps = s->dv->d_heaps.p; A.heap_bytes = s->heap_bytes; A.nslots = s->nslots;
+  A.tiles = s->dv->d_tiles.p; A.rule_status = s->dv->d_rule_status.p; A.max_top = s->max_top;
+  A.recs = s->dv->d_recs.p; A.rec_cap = (uint32_t)s->rec_cap;
+  A.rec_cursor = s->dv->d_counters.p; A.tile_cursor = s->dv->d_counters.p + 1;   // [1] lane batches, [2] wave tiles
+  A.retry_count = s->dv->d_counters.p + 3;
+  A.xcd_cursor = s->dv->d_counters.p + 16;
+  A.lane_heaps = s->dv->d_lane_heaps.p; A.lane_heap_bytes = s->lane_heap_bytes;
+  A.retry_list = s->mode == 1 ? nullptr : s->dv->d_retry.p;
   A.wave_frames_bytes = gg_session::kWaveFrames; A.wave_recs_bytes = gg_session::kWaveRecs;
-  A.retry2_list = s->d_retry2.p; A.retry2_count = s->d_counters.p + 4;
-  A.stats = s->d_stats.p;
+  A.retry2_list = s->dv->d_retry2.p; A.retry2_count = s->dv->d_counters.p + 4;
+  A.stats = s->dv->d_stats.p;
   A.lds_prog_words = s->lds_prog_words;
   if (!ntiles) return;
-  if (s->nq == s->evq.size()) {
+  if (s->nq == s->dv->evq.size()) {
     std::pair<hipEvent_t, hipEvent_t> pr;
     HIPCHK(hipEventCreate(&pr.first));
     HIPCHK(hipEventCreate(&pr.second));
-    s->evq.push_back(pr);
+    s->dv->evq.push_back(pr);
   }
-  s->ev0 = s->evq[s->nq].first; s->ev1 = s->evq[s->nq].second; s->nq++;
+  s->ev0 = s->dv->evq[s->nq].first; s->ev1 = s->dv->evq[s->nq].second; s->nq++;
   HIPCHK(hipEventRecord(s->ev0, st));
   if (s->type_key != NONE && A.docs.ndocs) {
     uint32_t blocks = std::min<uint32_t>((A.docs.ndocs + 3) / 4, g_dev.ncu * 16);
@@ -415,12 +467,13 @@ void session_launch(gg_session* s) {
   }
   hipLaunchKernelGGL(guard_eval_kernel, dim3(s->nslots), dim3(64), A.lds_prog_words * 4, st, A);
   HIPCHK(hipGetLastError());
-  {
+  if (s->dv->d_big_heaps.p) {
     // large-heap pass over the wave pass's overflow list (counters[4]; its cursor is counters[6]);
-    // normally empty, so its waves exit at once
+    // normally empty, so its waves exit at once.  Its 256 MB of heaps exist only once a tile of
+    // this session has needed them (session_run)
     LaunchArgs B = A;
-    B.retry_list = s->d_retry2.p; B.retry_count = s->d_counters.p + 4; B.tile_cursor = s->d_counters.p + 5;
-    B.heaps = s->d_big_heaps.p; B.heap_bytes = gg_session::kBigHeap; B.nslots = gg_session::kBigSlots;
+    B.retry_list = s->dv->d_retry2.p; B.retry_count = s->dv->d_counters.p + 4; B.tile_cursor = s->dv->d_counters.p + 5;
+    B.heaps = s->dv->d_big_heaps.p; B.heap_bytes = gg_session::kBigHeap; B.nslots = gg_session::kBigSlots;
     B.wave_frames_bytes = gg_session::kBigFrames; B.wave_recs_bytes = gg_session::kBigRecs;
     B.retry2_list = nullptr; B.retry2_count = nullptr;
     hipLaunchKernelGGL(guard_eval_kernel, dim3(gg_session::kBigSlots), dim3(64), B.lds_prog_words * 4, st, B);
@@ -428,8 +481,8 @@ void session_launch(gg_session* s) {
   }
   HIPCHK(hipEventRecord(s->ev1, st));
   uint32_t cblocks = std::min<uint32_t>((ntiles + 255) / 256, g_dev.ncu * 4);
-  hipLaunchKernelGGL(rule_count_kernel, dim3(cblocks), dim3(256), s->ncounts * sizeof(uint32_t), st, s->d_tiles.p,
-                     s->d_rule_status.p, s->d_progs.p, A.nfiles, ntiles, s->max_top, counts);
+  hipLaunchKernelGGL(rule_count_kernel, dim3(cblocks), dim3(256), s->ncounts * sizeof(uint32_t), st, s->dv->d_tiles.p,
+                     s->dv->d_rule_status.p, s->dv->d_progs.p, A.nfiles, ntiles, s->max_top, counts);
   HIPCHK(hipGetLastError());
   s->launched = true;
 }
@@ -447,10 +500,10 @@ double session_wait(gg_session* s) {
 // kernel ms of every launch since the last drain (synchronises on the last one)
 size_t session_drain(gg_session* s, double* out, size_t cap) {
   size_t n = s->nq;
-  if (n) HIPCHK(hipEventSynchronize(s->evq[n - 1].second));
+  if (n) HIPCHK(hipEventSynchronize(s->dv->evq[n - 1].second));
   for (size_t i = 0; i < n; i++) {
     float ms = 0;
-    HIPCHK(hipEventElapsedTime(&ms, s->evq[i].first, s->evq[i].second));
+    HIPCHK(hipEventElapsedTime(&ms, s->dv->evq[i].first, s->dv->evq[i].second));
     if (i < cap && out) out[i] = ms;
   }
   s->nq = 0;
@@ -461,7 +514,7 @@ size_t session_drain(gg_session* s, double* out, size_t cap) {
 uint32_t session_records_wanted(gg_session* s) {
   uint32_t nrec = 0;
   HIPCHK(hipStreamSynchronize(session_stream(s)));
-  HIPCHK(hipMemcpy(&nrec, s->d_counters.p, 4, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(&nrec, s->dv->d_counters.p, 4, hipMemcpyDeviceToHost));
   return nrec;
 }
 
@@ -475,24 +528,35 @@ void session_fetch(gg_session* s) {
   if (nrec > s->rec_cap) nrec = (uint32_t)s->rec_cap;
   s->recs.resize(nrec);
   if (ntiles) {
-    HIPCHK(hipMemcpy(s->tiles.data(), s->d_tiles.p, ntiles * sizeof(TileOut), hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(s->rule_status.data(), s->d_rule_status.p, s->rule_status.size(), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(s->tiles.data(), s->dv->d_tiles.p, ntiles * sizeof(TileOut), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(s->rule_status.data(), s->dv->d_rule_status.p, s->rule_status.size(), hipMemcpyDeviceToHost));
   }
-  if (nrec) HIPCHK(hipMemcpy(s->recs.data(), s->d_recs.p, nrec * sizeof(Rec), hipMemcpyDeviceToHost));
+  if (nrec) HIPCHK(hipMemcpy(s->recs.data(), s->dv->d_recs.p, nrec * sizeof(Rec), hipMemcpyDeviceToHost));
   s->counts.resize(s->ncounts);
-  HIPCHK(hipMemcpy(s->counts.data(), s->ext_counts ? s->ext_counts : s->d_counts.p, s->ncounts * sizeof(unsigned long long),
+  HIPCHK(hipMemcpy(s->counts.data(), s->ext_counts ? s->ext_counts : s->dv->d_counts.p, s->ncounts * sizeof(unsigned long long),
                    hipMemcpyDeviceToHost));
   s->evaluated = true;
 }
 
-// one complete evaluation; grows the record arena and re-runs when the first pass overflowed it
+// one complete evaluation; re-runs when the first pass overflowed the record arena (grown) or left
+// tiles for the large-heap pass before its heaps existed (allocated)
 double session_run(gg_session* s, bool fetch) {
   session_launch(s);
   double ms = session_wait(s);
-  uint32_t want = session_records_wanted(s);
-  if (want > s->rec_cap) {
-    s->rec_cap = std::min<size_t>((size_t)want + want / 8 + 1024, (size_t)0xFFFFFFF0u);
-    s->d_recs.alloc(s->rec_cap);
+  uint32_t cnt[5] = {0, 0, 0, 0, 0};
+  HIPCHK(hipStreamSynchronize(session_stream(s)));
+  HIPCHK(hipMemcpy(cnt, s->dv->d_counters.p, sizeof(cnt), hipMemcpyDeviceToHost));
+  bool again = false;
+  if (cnt[0] > s->rec_cap) {
+    s->rec_cap = std::min<size_t>((size_t)cnt[0] + cnt[0] / 8 + 1024, (size_t)0xFFFFFFF0u);
+    s->dv->d_recs.alloc(s->rec_cap);
+    again = true;
+  }
+  if (cnt[4] && !s->dv->d_big_heaps.p) {
+    s->dv->d_big_heaps.alloc((size_t)gg_session::kBigSlots * gg_session::kBigHeap);
+    again = true;
+  }
+  if (again) {
     session_launch(s);
     ms = session_wait(s);
   }
@@ -995,7 +1059,7 @@ int64_t gg_session_report_bytes(gg_session* s, int32_t output_format, size_t max
 }
 
 size_t gg_session_ncounts(gg_session* s) { return s->ncounts; }
-void* gg_session_counts_device(gg_session* s) { return s->ext_counts ? (void*)s->ext_counts : (void*)s->d_counts.p; }
+void* gg_session_counts_device(gg_session* s) { return s->ext_counts ? (void*)s->ext_counts : s->dv ? (void*)s->dv->d_counts.p : nullptr; }
 void gg_session_bind_counts(gg_session* s, void* dev, size_t n) {
   s->ext_counts = (dev && n >= s->ncounts) ? (unsigned long long*)dev : nullptr;
 }
@@ -1341,7 +1405,7 @@ int64_t gg_session_stat(gg_session* s, int32_t what) {
     case 15: return (int64_t)s->heap_bytes;
     case 16: {   // tiles the lane kernel handed to wave mode in the last launch
       uint32_t v = 0;
-      if (s->d_counters.p) HIPCHK(hipMemcpy(&v, s->d_counters.p + 3, 4, hipMemcpyDeviceToHost));
+      if (s->dv && s->dv->d_counters.p) HIPCHK(hipMemcpy(&v, s->dv->d_counters.p + 3, 4, hipMemcpyDeviceToHost));
       return v;
     }
     case 17: return (int64_t)s->lane_slots;
@@ -1367,9 +1431,9 @@ double gg_session_last_kernel_ms(gg_session* s) { return s->last_kernel_ms; }
 // node reads, heap accesses, query_retrieval calls, clause evaluations, frames pushed, records,
 // map entries scanned by key lookups, fast-filter tests, tiles
 int32_t gg_session_kernel_stats(gg_session* s, uint64_t* out, size_t n) {
-  if (!s->d_stats.p) return -1;
+  if (!s->dv || !s->dv->d_stats.p) return -1;
   std::vector<unsigned long long> v(16);
-  HIPCHK(hipMemcpy(v.data(), s->d_stats.p, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(v.data(), s->dv->d_stats.p, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   for (size_t i = 0; i < n && i < 16; i++) out[i] = v[i];
   return 0;
 }
