@@ -329,7 +329,8 @@ def main():
                        "tiles_fail_pass_skip_err": [n_fail, n_pass, n_skip, n_err],
                        "loader": args.loader, "load_s": round(t_load, 2), "host_threads": threads,
                        "upload_s": round(t_upload, 2), "device_loader": load_stats,
-                       "rule_tallies_sum": tally_sum, "rule_tallies_fetched": int(sum(tally))},
+                       "rule_tallies_sum": tally_sum, "rule_tallies_fetched": int(sum(tally)),
+                       "lane_tiles_retried_in_wave_mode": sess.stat(16)},
         }
         line["cpu_baseline"] = cpu
         line["e2e"] = e2e
