@@ -505,7 +505,27 @@ struct Compiler {
     if (!v.empty()) memcpy(blob.data() + at, v.data(), v.size() * sizeof(T));
   }
 
+  // `%var` heads whose variable can only come from the root scope's resolved variables (a root
+  // query / function let or a key capture): no block let or rule parameter anywhere in the file
+  // has the name, and no root literal let shadows it.  The walker reads those straight from the
+  // root table (PPart.c = 1) instead of asking the scope chain.
+  void mark_root_vars() {
+    std::vector<uint8_t> scoped(P.var_names.size(), 0);
+    const PBlock& rb = blocks[P.hdr.root_block];
+    for (size_t b = 0; b < blocks.size(); b++) {
+      for (uint32_t i = 0; i < blocks[b].nlets; i++) {
+        const PLet& l = lets[blocks[b].first_let + i];
+        if (b != P.hdr.root_block || l.kind == L_LITERAL) scoped[l.var] = 1;
+      }
+    }
+    (void)rb;
+    for (uint32_t v : param_vars) scoped[v] = 1;
+    for (auto& pp : parts)
+      if (pp.kind == P_VAR_HEAD) pp.c = scoped[pp.a] ? 0u : 1u;
+  }
+
   void assemble() {
+    mark_root_vars();
     std::vector<uint32_t> blob(sizeof(ProgHeader) / 4 + 2, 0);
     ProgHeader& h = P.hdr;
     put(blob, h.off_strs, h.n_strs, P.strs);
