@@ -15,6 +15,27 @@ def shard_range(rank, world, docs_per_rank):
     return rank * docs_per_rank, docs_per_rank
 
 
+def shard_ranges_by_bytes(sizes, world):
+    """Contiguous document ranges [(first, count)] per rank, balanced by document bytes (the arena a
+    document becomes is proportional to its text).  Contiguity keeps rank order =
+    document order, so gathered reports stitch into the single-process output."""
+    total = sum(sizes)
+    out, start, acc = [], 0, 0
+    for r in range(world):
+        target = total * (r + 1) / world
+        end = start
+        while end < len(sizes) and (acc + sizes[end] <= target or end == start) and len(sizes) - end > world - r - 1:
+            acc += sizes[end]
+            end += 1
+        if r == world - 1:
+            while end < len(sizes):
+                acc += sizes[end]
+                end += 1
+        out.append((start, end - start))
+        start = end
+    return out
+
+
 def tally_index(file, rule, status, max_top):
     """Index into the tally vector: ((file * (max_top + 1) + rule) * 4) + status.
     rule == max_top is the file-level line (file status, errored tiles in status 3)."""
@@ -34,10 +55,11 @@ def all_reduce_tallies(tensor, dist):
 
 # ---------------------------------------------------------------- reports -----
 # The structured report of a sharded run: every rank reports its own documents;
-# the per-rank texts are gathered to rank 0 (all_gather of the byte counts, then one padded
-# all_gather of the bytes: RCCL on GPU ranks, gloo on CPU) and stitched in rank order.  Rank order
-# is document order, so the result is the single-process `validate --structured` output
-# (reporters/validate/structured.rs:99-133 writes one FileReport per data file, in input order).
+# the per-rank texts are gathered to rank 0 (all_gather of the byte counts, then point-to-point
+# send / recv of each rank's bytes to rank 0 only: RCCL on GPU ranks, gloo on CPU) and stitched in
+# rank order.  Rank order is document order, so the result is the single-process
+# `validate --structured` output (reporters/validate/structured.rs:99-133 writes one FileReport per
+# data file, in input order); SARIF and JUnit runs are re-totalled (sarif.rs, xml.rs).
 
 # exit-code precedence of a structured run (commands/validate.rs:391-403, structured.rs:111-113):
 # an evaluation error aborts the run (-1); otherwise any FAIL sets 19, which overrides the
@@ -59,24 +81,31 @@ def reduce_exit_code(code, dist, device="cpu"):
 
 
 def gather_bytes(payload, dist, device="cpu"):
-    """Every rank's `payload` (bytes) in rank order on rank 0; None on the other ranks."""
+    """Every rank's `payload` (bytes) in rank order on rank 0; None on the other ranks.  The byte
+    counts are all-gathered (8 B per rank); then each rank sends its bytes to rank 0 alone, so a
+    rank holds only its own report and rank 0 the job's (no world-sized padded buffers)."""
     import torch
     if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
         return [payload]
-    world = dist.get_world_size()
+    world, rank = dist.get_world_size(), dist.get_rank()
     n = torch.tensor([len(payload)], dtype=torch.int64, device=device)
     sizes = [torch.zeros(1, dtype=torch.int64, device=device) for _ in range(world)]
     dist.all_gather(sizes, n)
     sizes = [int(s.item()) for s in sizes]
-    cap = max(1, max(sizes))
-    buf = torch.zeros(cap, dtype=torch.uint8, device=device)
-    if payload:
-        buf[:len(payload)] = torch.frombuffer(bytearray(payload), dtype=torch.uint8).to(device)
-    parts = [torch.empty(cap, dtype=torch.uint8, device=device) for _ in range(world)]
-    dist.all_gather(parts, buf)
-    if dist.get_rank() != 0:
+    if rank != 0:
+        if sizes[rank]:
+            buf = torch.frombuffer(bytearray(payload), dtype=torch.uint8).to(device)
+            dist.send(buf, dst=0)
         return None
-    return [bytes(p[:s].cpu().numpy().tobytes()) for p, s in zip(parts, sizes)]
+    parts = [payload]
+    for r in range(1, world):
+        if not sizes[r]:
+            parts.append(b"")
+            continue
+        buf = torch.empty(sizes[r], dtype=torch.uint8, device=device)
+        dist.recv(buf, src=r)
+        parts.append(bytes(buf.cpu().numpy().tobytes()))
+    return parts
 
 
 def merge_reports(parts, output="json"):
@@ -100,7 +129,52 @@ def merge_reports(parts, output="json"):
             if not p.startswith("- "):
                 raise ValueError("not a YAML sequence of file reports")
         return "".join(bodies) if bodies else "[]\n"
-    raise ValueError("merge_reports supports json and yaml (SARIF / JUnit carry run-level totals)")
+    if output == "sarif":
+        return _merge_sarif(parts)
+    if output == "junit":
+        return _merge_junit(parts)
+    raise ValueError("unknown output format %r" % (output,))
+
+
+def _merge_sarif(parts):
+    """SarifReport (reporters/validate/sarif.rs): one run whose artifacts are the distinct failing
+    data files in order and whose results are every failure in order; serde_json pretty text."""
+    import json
+    from collections import OrderedDict
+    docs = [json.loads(p, object_pairs_hook=OrderedDict) for p in parts]
+    base = docs[0]
+    run = base["runs"][0]
+    seen = {json.dumps(a, sort_keys=True) for a in run["artifacts"]}
+    for d in docs[1:]:
+        r = d["runs"][0]
+        for a in r["artifacts"]:
+            k = json.dumps(a, sort_keys=True)
+            if k not in seen:
+                seen.add(k)
+                run["artifacts"].append(a)
+        run["results"].extend(r["results"])
+    return json.dumps(base, indent=2, ensure_ascii=False)
+
+
+def _merge_junit(parts):
+    """JunitReport (reporters/validate/xml.rs): the test suites in order under one <testsuites> whose
+    tests / failures / errors are the sums."""
+    import re
+    head = re.compile(r'^(<\?xml[^\n]*\n)<testsuites name="([^"]*)" tests="(\d+)" failures="(\d+)" errors="(\d+)" time="([^"]*)">\n')
+    tests = failures = errors = 0
+    bodies = []
+    decl = name = time = None
+    for p in parts:
+        m = head.match(p)
+        if not m or not p.endswith("</testsuites>\n"):
+            raise ValueError("not a JUnit report")
+        decl, name, time = m.group(1), m.group(2), m.group(6)
+        tests += int(m.group(3))
+        failures += int(m.group(4))
+        errors += int(m.group(5))
+        bodies.append(p[m.end():-len("</testsuites>\n")])
+    return '%s<testsuites name="%s" tests="%d" failures="%d" errors="%d" time="%s">\n%s</testsuites>\n' % (
+        decl, name, tests, failures, errors, time, "".join(bodies))
 
 
 def gather_report(local_text, local_code, dist, output="json", device="cpu"):

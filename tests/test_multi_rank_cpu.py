@@ -100,7 +100,7 @@ def _report_worker(rank, world, port, q, codes):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     out = {}
-    for fmt in ("json", "yaml"):
+    for fmt in ("json", "yaml", "sarif", "junit"):
         first, n = sharding.shard_range(rank, world, REPORT_DOCS)
         text, code = _shard_report(first, n, fmt)
         out[fmt] = sharding.gather_report(text, code, dist, output=fmt)
@@ -109,7 +109,7 @@ def _report_worker(rank, world, port, q, codes):
     if rank == 0:
         q.put(out)
     else:
-        assert out["json"][0] is None and out["yaml"][0] is None
+        assert all(out[f][0] is None for f in ("json", "yaml", "sarif", "junit"))
     dist.destroy_process_group()
 
 
@@ -125,9 +125,9 @@ def test_two_rank_report_gather_matches_single_process():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for fmt in ("json", "yaml"):
+    for fmt in ("json", "yaml", "sarif", "junit"):
         full, code = _shard_report(0, 2 * REPORT_DOCS, fmt)
-        assert got[fmt] == (full, code)
+        assert got[fmt] == (full, code), fmt
     assert got["codes"] == [19, 19, 19, 5, 0, -1, -1]
 
 
@@ -138,4 +138,15 @@ def test_merge_reports_edge_cases():
     with pytest.raises(ValueError):
         sharding.merge_reports(["{}"])
     with pytest.raises(ValueError):
-        sharding.merge_reports(["x"], "sarif")
+        sharding.merge_reports(["x"], "junit")
+
+
+def test_byte_balanced_shard_ranges():
+    sizes = [10, 10, 10, 70, 5, 5, 5, 5, 40, 40]
+    r = sharding.shard_ranges_by_bytes(sizes, 3)
+    assert [c for _, c in r] and sum(c for _, c in r) == len(sizes)
+    assert all(r[i][0] + r[i][1] == r[i + 1][0] for i in range(2))   # contiguous, in order
+    loads = [sum(sizes[a:a + n]) for a, n in r]
+    assert max(loads) <= 100 and min(c for _, c in r) >= 1
+    assert sharding.shard_ranges_by_bytes([1] * 8, 4) == [(0, 2), (2, 2), (4, 2), (6, 2)]
+    assert sharding.shard_ranges_by_bytes([5], 2) == [(0, 0), (0, 1)]   # fewer documents than ranks

@@ -28,7 +28,9 @@ def main(d):
     for name, ctrs in per.items():
         row = {c: sum(v) / len(v) for c, v in ctrs.items()}
         out[name] = {"fetch_kib_raw": row.get("FETCH_SIZE"), "write_kib_raw": row.get("WRITE_SIZE"),
-                     "dispatches": max(len(v) for v in ctrs.values())}
+                     "dispatches": max(len(v) for v in ctrs.values()),
+                     "counters_mean_per_dispatch": {c: v for c, v in sorted(row.items())
+                                                    if c not in ("FETCH_SIZE", "WRITE_SIZE")}}
     lanes = out.get("lanes", {})
     hbm = None
     if lanes.get("fetch_kib_raw") is not None and lanes.get("write_kib_raw") is not None:
