@@ -1,18 +1,32 @@
 // Guard DSL parser -- a PEG over the same grammar as the reference's nom 7 combinators
 // (guard/src/rules/parser.rs; each method names the combinator it restates).
-// `Err` = nom::Err::Error (recoverable), `Fail` = nom::Err::Failure (cut).
+// `Err` = nom::Err::Error (recoverable), `Fail` = nom::Err::Failure (cut).  Both carry nom 7's
+// ParserError payload -- the input position the failing combinator saw and its context string --
+// propagated the way nom 7.1.3 propagates them (alt: the last alternative's error; many1 /
+// separated_list: the element's error; fold_many1: a fresh error at its own input; context(): its
+// input position and "ctx/inner"; cut: Error -> Failure), so a rules file that does not parse
+// reports the reference's "Error parsing file F at line L at column C, when handling CTX, fragment
+// REST" (parser.rs:48-101).
 #include <cstring>
+#include <map>
 #include <stdexcept>
 
 #include "host_format.h"
+#include "regex_dfa.h"
 #include "rules_ast.h"
 
 namespace gg {
 
 namespace {
 
-struct Err {};
-struct Fail {};
+struct Err { size_t pos; std::string ctx; };
+struct Fail { size_t pos; std::string ctx; };
+[[noreturn]] void E(size_t p, const std::string& c = std::string()) { throw Err{p, c}; }
+[[noreturn]] void F(size_t p, const std::string& c = std::string()) { throw Fail{p, c}; }
+// nom's ContextError::add_context (parser.rs:48-62): the context's own input, "ctx" or "ctx/inner"
+std::string add_ctx(const char* ctx, const std::string& inner) { return inner.empty() ? ctx : std::string(ctx) + "/" + inner; }
+const char* const CTX_CMP = "expecting comparison binary operators like >, <= or unary operators KEYS, EXISTS, EMPTY or NOT";
+const char* const CTX_RHS = "expecting either a property access \"engine.core\" or value like \"string\" or [\"this\", \"that\"]";
 
 const std::vector<std::string> UNARY = {"Exists", "Empty", "IsString", "IsList", "IsMap", "IsBool", "IsInt", "IsFloat", "IsNull"};
 
@@ -47,14 +61,29 @@ struct P {
     return l;
   }
 
+  mutable std::map<std::string, bool> rx_ok;   // fancy-regex validity per pattern (parses backtrack)
+  bool regex_ok(const std::string& rx) const {
+    auto it = rx_ok.find(rx);
+    if (it != rx_ok.end()) return it->second;
+    const bool ok = compile_regex(rx).valid;
+    rx_ok[rx] = ok;
+    return ok;
+  }
+  // nom_locate position of offset p: 1-based line, 1-based column counted in UTF-8 characters
+  std::string error_text(size_t p, const std::string& ctx) const {
+    FileLoc l = loc(p);
+    return "Error parsing file " + file + " at line " + std::to_string(l.line) + " at column " + std::to_string(l.column) +
+           ", when handling " + ctx + ", fragment " + s.substr(p);
+  }
+
   bool starts(size_t p, const char* t) const { size_t m = strlen(t); return p + m <= n && s.compare(p, m, t) == 0; }
-  size_t tag(size_t p, const char* t) const { if (starts(p, t)) return p + strlen(t); throw Err(); }
-  size_t ch(size_t p, char c) const { if (p < n && s[p] == c) return p + 1; throw Err(); }
+  size_t tag(size_t p, const char* t) const { if (starts(p, t)) return p + strlen(t); E(p); }
+  size_t ch(size_t p, char c) const { if (p < n && s[p] == c) return p + 1; E(p); }
   static bool ms(char c) { return c == ' ' || c == '\t' || c == '\r' || c == '\n'; }
   size_t multispace0(size_t p) const { while (p < n && ms(s[p])) p++; return p; }
   size_t space0(size_t p) const { while (p < n && (s[p] == ' ' || s[p] == '\t')) p++; return p; }
-  size_t space1(size_t p) const { size_t q = space0(p); if (q == p) throw Err(); return q; }
-  size_t digit1(size_t p) const { size_t q = p; while (q < n && s[q] >= '0' && s[q] <= '9') q++; if (q == p) throw Err(); return q; }
+  size_t space1(size_t p) const { size_t q = space0(p); if (q == p) E(p); return q; }
+  size_t digit1(size_t p) const { size_t q = p; while (q < n && s[q] >= '0' && s[q] <= '9') q++; if (q == p) E(p); return q; }
   size_t comment2(size_t p) const { p = ch(p, '#'); while (p < n && s[p] != '\n') p++; return multispace0(p); }
   size_t ws_or_comment(size_t p) const { size_t q = multispace0(p); if (q > p) return q; return comment2(p); }
   size_t ws0(size_t p) const {
@@ -68,13 +97,13 @@ struct P {
     try {
       size_t q = digit1(p);
       std::string d = s.substr(p, q - p);
-      if (d.size() > 19 || (d.size() == 19 && d > "9223372036854775807")) throw Err();
+      if (d.size() > 19 || (d.size() == 19 && d > "9223372036854775807")) E(p);
       v = LitValue(); v.k = LitValue::Int; v.i = std::stoll(d); return q;
     } catch (Err&) {}
     size_t q = tag(p, "-");
     size_t r = digit1(q);
     std::string d = s.substr(q, r - q);
-    if (d.size() > 19 || (d.size() == 19 && d > "9223372036854775807")) throw Err();
+    if (d.size() > 19 || (d.size() == 19 && d > "9223372036854775807")) E(p);
     v = LitValue(); v.k = LitValue::Int; v.i = -std::stoll(d); return r;
   }
 
@@ -89,12 +118,12 @@ struct P {
       if (!frag.empty() && frag.back() == '\\') {
         out += frag.substr(0, frag.size() - 1);
         out.push_back(q);
-        if (e >= n) throw Err();
+        if (e >= n) E(p, "Could not parse string");
         span = e + 1;
         continue;
       }
       out += frag;
-      if (e >= n) throw Fail();
+      if (e >= n) F(e);   // cut(char(q))
       return e + 1;
     }
   }
@@ -105,7 +134,7 @@ struct P {
   size_t parse_bool(size_t p, LitValue& v) const {
     const char* t[] = {"true", "True", "false", "False"};
     for (int i = 0; i < 4; i++) if (starts(p, t[i])) { v = LitValue(); v.k = LitValue::Bool; v.b = i < 2; return p + strlen(t[i]); }
-    throw Err();
+    E(p);
   }
   size_t recognize_float(size_t p) const {
     size_t q = p;
@@ -115,11 +144,11 @@ struct P {
       if (q < n && s[q] == '.') { q++; while (q < n && isdigit((unsigned char)s[q])) q++; }
     } else if (q + 1 < n && s[q] == '.' && isdigit((unsigned char)s[q + 1])) {
       q = digit1(q + 1);
-    } else throw Err();
+    } else E(p);
     if (q < n && (s[q] == 'e' || s[q] == 'E')) {
       size_t r = q + 1;
       if (r < n && (s[r] == '+' || s[r] == '-')) r++;
-      try { r = digit1(r); } catch (Err&) { throw Fail(); }
+      try { r = digit1(r); } catch (Err& e) { F(e.pos, e.ctx); }   // nom recognize_float: cut(digit1)
       q = r;
     }
     return q;
@@ -136,7 +165,7 @@ struct P {
       v = LitValue(); v.k = LitValue::Float; v.f = strtod(s.substr(p, r - p).c_str(), nullptr);
       return r;
     }
-    throw Err();
+    E(p, "Could not parse floating number");
   }
   size_t parse_regex(size_t p, LitValue& v) const {
     p = ch(p, '/');
@@ -145,24 +174,27 @@ struct P {
     for (;;) {
       size_t e = span;
       while (e < n && s[e] != '/') e++;
-      if (e == span) throw Err();
+      if (e == span) E(span);   // is_not("/")
       std::string frag = s.substr(span, e - span);
       if (frag.back() == '\\') {
         rx += frag.substr(0, frag.size() - 1);
         rx.push_back('/');
-        if (e >= n) throw Err();
+        if (e >= n) E(p, "Could not parse regular expression");
         span = e + 1;
         continue;
       }
       rx += frag;
-      // fancy-regex validation happens at compile time of the program (regex.cpp)
+      // Regex::try_from (parser.rs:273-280): a pattern fancy-regex rejects fails the parse here.
+      // The reference's context then quotes fancy-regex's error text; that text is not restated
+      // (the alternatives around a regex literal always report a later alternative's error).
+      if (!regex_ok(rx)) E(p, "Could not parse regular expression");
       size_t q = ch(e, '/');
       v = LitValue(); v.k = LitValue::Regex; v.s = rx;
       return q;
     }
   }
   size_t parse_char(size_t p, LitValue& v) const {
-    if (p >= n) throw Err();
+    if (p >= n) E(p);
     size_t i = p;
     uint32_t cp = utf8_next((const unsigned char*)s.data(), n, i);
     v = LitValue(); v.k = LitValue::Char; v.ch = cp;
@@ -178,20 +210,20 @@ struct P {
   }
   size_t parse_range(size_t p, LitValue& v) const {
     p = ch(p, 'r');
-    if (!(p < n && (s[p] == '(' || s[p] == '['))) throw Err();
+    if (!(p < n && (s[p] == '(' || s[p] == '['))) E(p);
     char open = s[p++];
     LitValue a, b;
     p = range_value(p, a);
     p = ch(p, ',');
     p = range_value(p, b);
-    if (!(p < n && (s[p] == ')' || s[p] == ']'))) throw Err();
+    if (!(p < n && (s[p] == ')' || s[p] == ']'))) E(p);
     char close = s[p++];
     uint8_t incl = (open == '[' ? 1 : 0) | (close == ']' ? 2 : 0);
     v = LitValue(); v.incl = incl;
     if (a.k == LitValue::Int && b.k == LitValue::Int) { v.k = LitValue::RangeInt; v.ilo = a.i; v.ihi = b.i; }
     else if (a.k == LitValue::Float && b.k == LitValue::Float) { v.k = LitValue::RangeFloat; v.flo = a.f; v.fhi = b.f; }
     else if (a.k == LitValue::Char && b.k == LitValue::Char) { v.k = LitValue::RangeChar; v.clo = a.ch; v.chi = b.ch; }
-    else throw Fail();
+    else F(p, "Could not parse range");
     return p;
   }
   size_t parse_scalar_value(size_t p, LitValue& v) const {
@@ -253,7 +285,7 @@ struct P {
   }
   size_t parse_null(size_t p, LitValue& v) const {
     if (starts(p, "null") || starts(p, "NULL")) { v = LitValue(); v.k = LitValue::Null; return p + 4; }
-    throw Err();
+    E(p);
   }
   size_t parse_value(size_t p, LitValue& v) const {
     p = ws0(p);
@@ -268,7 +300,7 @@ struct P {
   size_t var_name(size_t p, std::string& out) const {
     size_t q = p;
     while (q < n && is_ascii_alpha((unsigned char)s[q])) q++;
-    if (q == p) throw Err();
+    if (q == p) E(p);
     while (q < n && (is_alnum_u((unsigned char)s[q]) || s[q] == '_')) q++;
     out = s.substr(p, q - p);
     return q;
@@ -282,7 +314,7 @@ struct P {
   }
   size_t in_keyword(size_t p) const {
     if (starts(p, "in") || starts(p, "IN")) return p + 2;
-    throw Err();
+    E(p);
   }
   size_t not_(size_t p) const {
     for (const char* t : {"not", "NOT"}) {
@@ -293,7 +325,7 @@ struct P {
   size_t eq(size_t p, std::string& op, bool& neg) const {
     if (starts(p, "==")) { op = "Eq"; neg = false; return p + 2; }
     if (starts(p, "!=")) { op = "Eq"; neg = true; return p + 2; }
-    throw Err();
+    E(p);
   }
   size_t other_operations(size_t p, std::string& op, bool& neg) const {
     neg = false;
@@ -306,10 +338,10 @@ struct P {
                                      {"IS_NULL", "IsNull"}, {"is_null", "IsNull"}, {"IS_FLOAT", "IsFloat"},
                                      {"is_float", "IsFloat"}};
     for (auto& w : words) if (starts(p, w[0])) { op = w[1]; return p + strlen(w[0]); }
-    throw Err();
+    E(p);
   }
   size_t value_cmp(size_t p, std::string& op, bool& neg) const {
-    if (starts(p, "<<")) throw Err();
+    if (starts(p, "<<")) E(p, "Custom message tag detected");
     try { return eq(p, op, neg); } catch (Err&) {}
     static const char* cmps[][2] = {{">=", "Ge"}, {"<=", "Le"}, {">", "Gt"}, {"<", "Lt"}};
     for (auto& c : cmps) if (starts(p, c[0])) { op = c[1]; neg = false; return p + strlen(c[0]); }
@@ -318,7 +350,7 @@ struct P {
   size_t custom_message(size_t p, std::string& msg) const {
     p = tag(p, "<<");
     size_t j = s.find(">>", p);
-    if (j == std::string::npos) throw Fail();
+    if (j == std::string::npos) F(p, "Unable to find a closing >> tag for message");
     msg = s.substr(p, j - p);
     return j + 2;
   }
@@ -337,7 +369,7 @@ struct P {
     try { p = variable_capture(p, var); has = true; } catch (Err&) {}
     auto conj = std::make_shared<Conj>();
     p = cnf_clauses(p, *conj, 0);
-    try { p = close_array(p); } catch (Err&) { throw Fail(); }
+    try { p = close_array(p); } catch (Err& e) { F(e.pos, e.ctx); }
     part = QueryPart(); part.k = QueryPart::Filter; part.filter = conj; part.has_name = has; part.key = var;
     return p;
   }
@@ -362,7 +394,7 @@ struct P {
   size_t array_index(size_t p, QueryPart& part) const {
     p = open_array(p);
     LitValue v; p = parse_int_value(p, v);
-    try { p = close_array(p); } catch (Err&) { throw Fail(); }
+    try { p = close_array(p); } catch (Err& e) { F(e.pos, e.ctx); }
     part = QueryPart(); part.k = QueryPart::Index; part.index = (int32_t)v.i;
     return p;
   }
@@ -383,7 +415,7 @@ struct P {
     std::string var; bool has = false;
     try { p = variable_capture(p, var); has = true; } catch (Err&) {}
     p = ws0(p);
-    if (starts(p, "KEYS") || starts(p, "keys")) p += 4; else throw Err();
+    if (starts(p, "KEYS") || starts(p, "keys")) p += 4; else E(p);
     std::string op; bool neg = false;
     try {
       size_t q = ws0(p);
@@ -392,13 +424,13 @@ struct P {
         try { p = in_keyword(q); op = "In"; neg = false; }
         catch (Err&) { q = not_(q); p = in_keyword(q); op = "In"; neg = true; }
       }
-    } catch (Err&) { throw Fail(); }
+    } catch (Err& e) { F(e.pos, e.ctx); }
     auto with = std::make_shared<LetValue>();
     try {
       size_t q = ws0(p);
       try { LitValue v; p = parse_value(q, v); with->k = LetValue::Value; with->value = v; }
       catch (Err&) { q = ws0(q); p = access(q, with->access); with->k = LetValue::Access; }
-    } catch (Err&) { throw Fail(); }
+    } catch (Err& e) { F(e.pos, e.ctx); }
     p = close_array(p);
     part = QueryPart(); part.k = QueryPart::MapKeyFilter; part.has_name = has; part.key = var;
     part.mk_op = op; part.mk_not = neg; part.mk_with = with;
@@ -417,7 +449,7 @@ struct P {
   }
   size_t dotted_access(size_t p, std::vector<QueryPart>& out) const {
     QueryPart part;
-    p = one_dotted(p, part);
+    try { p = one_dotted(p, part); } catch (Err&) { E(p); }   // fold_many1: from_error_kind(input, Many1)
     out.push_back(part);
     for (;;) {
       QueryPart q2; size_t q;
@@ -432,12 +464,12 @@ struct P {
   size_t some_keyword(size_t p) const {
     p = ws0(p);
     if (starts(p, "SOME") || starts(p, "some")) return ws1(p + 4);
-    throw Err();
+    E(p);
   }
   size_t this_keyword(size_t p) const {
     p = ws0(p);
     if (starts(p, "this") || starts(p, "THIS")) return p + 4;
-    throw Err();
+    E(p);
   }
   size_t access(size_t p, AccessQuery& q) const {
     bool some = false;
@@ -474,8 +506,11 @@ struct P {
     p = call_expr(p, name, params);
     int arity = -1;
     for (auto& fn : FUNCS) if (name == fn[0]) arity = atoi(fn[1]);
-    if (arity < 0) throw Err();
-    if ((int)params.size() != arity) throw Err();
+    // parser.rs:1082-1100 (errors at the input after the call; FunctionName Display = its name)
+    if (arity < 0) E(p, "Parser Error when parsing `No function with the name '" + name + "' exists.`");
+    if ((int)params.size() != arity)
+      E(p, "function: " + name + " requires: " + std::to_string(arity) + " parameters to be passed, but received: " +
+               std::to_string(params.size()));
     f.name = name; f.params = params;
     return p;
   }
@@ -513,29 +548,38 @@ struct P {
     try { p = not_(p); c.negation = true; } catch (Err&) {}
     p = access(p, c.query);
     p = ws0(p);
-    p = value_cmp(p, c.op, c.op_not);
+    try { p = value_cmp(p, c.op, c.op_not); }
+    catch (Err& e) { E(p, add_ctx(CTX_CMP, e.ctx)); }   // context(.., value_cmp), parser.rs:974
     if (is_unary(c.op)) {
       size_t q = ws0(p);
       try { p = custom_message(q, c.msg); c.has_msg = true; } catch (Err&) { p = q; }
       return p;
     }
-    // cut(alt((value, function, access)))
+    // context(.., cut(alt((value msg?, function msg?, access msg?)))), parser.rs:1000-1023
+    const size_t at = p;
     try {
+      auto msg = [&](size_t r) {
+        size_t q = ws0(r);
+        try { r = custom_message(q, c.msg); c.has_msg = true; } catch (Err&) { r = q; }
+        return r;
+      };
       bool done = false;
-      try { LitValue v; size_t q = parse_value(p, v); c.rhs.k = LetValue::Value; c.rhs.value = v; p = q; done = true; } catch (Err&) {}
+      try {
+        LitValue v; size_t q = parse_value(p, v);
+        c.rhs = LetValue(); c.rhs.k = LetValue::Value; c.rhs.value = v; p = msg(q); done = true;
+      } catch (Err&) {}
       if (!done) {
         try {
           size_t q = ws0(p); auto f = std::make_shared<FuncExpr>(); q = function_expr(q, *f);
-          c.rhs = LetValue(); c.rhs.k = LetValue::Func; c.rhs.func = f; p = q; done = true;
+          c.rhs = LetValue(); c.rhs.k = LetValue::Func; c.rhs.func = f; p = msg(q); done = true;
         } catch (Err&) {}
       }
       if (!done) {
-        size_t q = ws0(p); c.rhs = LetValue(); c.rhs.k = LetValue::Access; p = access(q, c.rhs.access);
+        size_t q = ws0(p); c.rhs = LetValue(); c.rhs.k = LetValue::Access; q = access(q, c.rhs.access); p = msg(q);
       }
-    } catch (Err&) { throw Fail(); }
+    } catch (Err& e) { F(at, add_ctx(CTX_RHS, e.ctx)); }
+    catch (Fail& e) { F(at, add_ctx(CTX_RHS, e.ctx)); }
     c.has_rhs = true;
-    size_t q = ws0(p);
-    try { p = custom_message(q, c.msg); c.has_msg = true; } catch (Err&) { p = q; }
     return p;
   }
   size_t block_clause(size_t p, Clause& c) const {
@@ -561,7 +605,7 @@ struct P {
     try { return parameterized_rule_call_clause(p, c); } catch (Err&) {}
     return clause_with_map(p, c);
   }
-  size_t newline(size_t p) const { if (starts(p, "\n")) return p + 1; if (starts(p, "\r\n")) return p + 2; throw Err(); }
+  size_t newline(size_t p) const { if (starts(p, "\n")) return p + 1; if (starts(p, "\r\n")) return p + 2; E(p); }
   size_t rule_clause(size_t p, Clause& c) const {
     c = Clause(); c.k = Clause::NamedRule; c.loc = loc(p);
     try { p = not_(p); c.negation = true; } catch (Err&) {}
@@ -574,7 +618,7 @@ struct P {
       if (!ret) try { or_join(p); ret = true; } catch (Err&) {}
     }
     if (ret) return p;
-    try { p = custom_message(space0(p), c.msg); c.has_msg = true; } catch (Err&) { throw Fail(); }
+    try { p = custom_message(space0(p), c.msg); c.has_msg = true; } catch (Err& e) { F(e.pos, e.ctx); }
     return p;
   }
   // parser kinds for cnf: 0 = clause, 1 = single_clauses element, 2 = clause | rule_clause, 3 = type_block
@@ -609,10 +653,17 @@ struct P {
   }
   size_t cnf_clauses(size_t p, Conj& out, int kind) const {
     out.clear();
+    const size_t p0 = p;
     for (;;) {
       Disj d; size_t q;
       try { q = disjunction_clauses(p, d, kind); }
-      catch (Err&) { if (out.empty()) throw Fail(); return p; }
+      catch (Err&) {
+        if (out.empty()) {   // parser.rs:1300-1312: a Failure at the conjunction's own input
+          FileLoc l = loc(p0);
+          F(p0, "There were no clauses present " + file + "#" + std::to_string(l.line) + "@" + std::to_string(l.column));
+        }
+        return p;
+      }
       out.push_back(d); p = q;
     }
   }
@@ -620,12 +671,10 @@ struct P {
     p = tag(p, "let");
     p = ws1(p);
     p = var_name(p, name);
-    try {
-      size_t q = ws0(p);
-      if (starts(q, "=")) return q + 1;
-      if (starts(q, ":=")) return q + 2;
-      throw Err();
-    } catch (Err&) { throw Fail(); }
+    size_t q = ws0(p);
+    if (starts(q, "=")) return q + 1;
+    if (starts(q, ":=")) return q + 2;
+    F(q);   // cut(preceded(ws, alt((tag("="), tag(":=")))))
   }
   size_t assignment(size_t p, LetExpr& le) const {
     p = let_assignment_expr(p, le.var);
@@ -636,12 +685,12 @@ struct P {
     } catch (Err&) {} catch (Fail&) {}
     try {
       size_t q = ws0(p); le.value = LetValue(); le.value.k = LetValue::Access; return access(q, le.value.access);
-    } catch (Err&) { throw Fail(); }
+    } catch (Err& e) { F(e.pos, e.ctx); }
   }
   size_t when_conditions(size_t p, Conj& conds) const {
     p = ws0(p);
-    if (starts(p, "when") || starts(p, "WHEN")) p += 4; else throw Err();
-    try { p = ws1(p); return cnf_clauses(p, conds, 1); } catch (Err&) { throw Fail(); }
+    if (starts(p, "when") || starts(p, "WHEN")) p += 4; else E(p);
+    try { p = ws1(p); return cnf_clauses(p, conds, 1); } catch (Err& e) { F(e.pos, e.ctx); }
   }
   // block(clause_parser) with items: assignment | disjunction_clauses(kind)
   size_t block(size_t p, Block& b, int kind) const {
@@ -651,9 +700,9 @@ struct P {
       try { size_t r = ws0(q); LetExpr le; r = assignment(r, le); b.assignments.push_back(le); return r; } catch (Err&) {}
       Disj d; size_t r = disjunction_clauses(q, d, kind); b.conjunctions.push_back(d); return r;
     };
-    p = item(p);
+    try { p = item(p); } catch (Err&) { E(p); }   // fold_many1
     for (;;) { size_t q; try { q = item(p); } catch (Err&) { break; } p = q; }
-    try { return white_space(p, '}'); } catch (Err&) { throw Fail(); }
+    try { return white_space(p, '}'); } catch (Err& e) { F(e.pos, e.ctx); }
   }
   size_t rule_block_items(size_t p, Block& b) const {
     // block(rule_block_clause)
@@ -666,9 +715,9 @@ struct P {
       b.conjunctions.push_back(d);
       return r;
     };
-    p = item(p);
+    try { p = item(p); } catch (Err&) { E(p); }   // fold_many1
     for (;;) { size_t q; try { q = item(p); } catch (Err&) { break; } p = q; }
-    try { return white_space(p, '}'); } catch (Err&) { throw Fail(); }
+    try { return white_space(p, '}'); } catch (Err& e) { F(e.pos, e.ctx); }
   }
   size_t rule_disjunction(size_t p, Disj& out) const {
     out.clear();
@@ -698,11 +747,11 @@ struct P {
   size_t type_block(size_t p, TypeBlock& tb) const {
     FileLoc l = loc(p);
     p = type_name(p, tb.type_name);
-    try { p = ws1(p); } catch (Err&) { throw Fail(); }
+    try { p = ws1(p); } catch (Err& e) { F(e.pos, e.ctx); }
     tb.has_conditions = false;
     try { p = when_conditions(p, tb.conditions); tb.has_conditions = true; } catch (Err&) {}
     if (tb.has_conditions) {
-      try { p = block(p, tb.block, 0); } catch (Err&) { throw Fail(); }
+      try { p = block(p, tb.block, 0); } catch (Err& e) { F(e.pos, e.ctx); }
     } else {
       try { p = block(p, tb.block, 0); }
       catch (Err&) {
@@ -712,7 +761,7 @@ struct P {
           p = clause(q, *c);
           tb.block = Block();
           tb.block.conjunctions.push_back(Disj{c});
-        } catch (Err&) { throw Fail(); }
+        } catch (Err& e) { F(e.pos, e.ctx); }
       }
     }
     // desugaring: Resources.*[ Type == "<type>" ]   (parser.rs:1631-1655)
@@ -763,15 +812,15 @@ struct P {
     p = ws0(p);
     p = tag(p, "rule");
     p = ws1(p);
-    try { p = var_name(p, r.name); } catch (Err&) { throw Fail(); }
+    try { p = var_name(p, r.name); } catch (Err& e) { F(e.pos, e.ctx); }
     r.has_conditions = false;
     try { p = when_conditions(p, r.conditions); r.has_conditions = true; } catch (Err&) {}
-    try { return rule_block_items(p, r.block); } catch (Err&) { throw Fail(); }
+    try { return rule_block_items(p, r.block); } catch (Err& e) { F(e.pos, e.ctx); }
   }
   size_t parameter_names(size_t p, std::vector<std::string>& names) const {
     p = ch(p, '(');
     auto elem2 = [&](size_t q, std::string& nm) -> size_t {
-      try { q = multispace0(q); q = var_name(q, nm); return multispace0(q); } catch (Err&) { throw Fail(); }
+      try { q = multispace0(q); q = var_name(q, nm); return multispace0(q); } catch (Err& e) { F(e.pos, e.ctx); }
     };
     std::string nm; p = elem2(p, nm);
     names.clear(); names.push_back(nm);
@@ -785,22 +834,22 @@ struct P {
       if (!dup) names.push_back(nm2);
       p = q;
     }
-    try { return ch(p, ')'); } catch (Err&) { throw Fail(); }
+    try { return ch(p, ')'); } catch (Err& e) { F(e.pos, e.ctx); }
   }
   size_t parameterized_rule_block(size_t p, ParamRule& pr) const {
     p = ws0(p);
     p = tag(p, "rule");
     p = ws1(p);
-    try { p = var_name(p, pr.rule.name); } catch (Err&) { throw Fail(); }
+    try { p = var_name(p, pr.rule.name); } catch (Err& e) { F(e.pos, e.ctx); }
     p = parameter_names(p, pr.params);
     pr.rule.has_conditions = false;
-    try { return rule_block_items(p, pr.rule.block); } catch (Err&) { throw Fail(); }
+    try { return rule_block_items(p, pr.rule.block); } catch (Err& e) { F(e.pos, e.ctx); }
   }
   size_t or_join(size_t p) const {
     p = ws0(p);
     if (starts(p, "|OR|")) p += 4;
     else if (starts(p, "or") || starts(p, "OR")) p += 2;
-    else throw Err();
+    else E(p);
     return ws1(p);
   }
 
@@ -810,6 +859,7 @@ struct P {
     if (p >= n) { empty = true; return true; }
     Conj defaults;
     bool any = false;
+    const size_t p0 = p;
     for (;;) {
       size_t q = ws0(p);
       bool matched = false;
@@ -822,11 +872,11 @@ struct P {
         defaults.push_back(Disj{c}); p = ws0(r); matched = true;
       } catch (Err&) {}
       if (!matched) try { Disj d; size_t r = disjunction_clauses(q, d, 0); defaults.push_back(d); p = ws0(r); matched = true; } catch (Err&) {}
-      if (!matched) { if (!any) throw Err(); break; }
+      if (!matched) { if (!any) E(p0); break; }   // fold_many1: from_error_kind(input, Many1)
       any = true;
       if (p >= n) break;
     }
-    if (p != n) throw Err();
+    if (p != n) E(p);   // all_consuming: Eof at the first unparsed item
     if (!defaults.empty()) {
       Rule d;
       std::string trimmed = file;
@@ -844,12 +894,13 @@ struct P {
 
 bool parse_rules_file(const std::string& text, const std::string& file_name, RulesFile& out, bool& empty, std::string& msg) {
   P p(text, file_name);
+  // nom::Err<ParserError> -> Error::ParseError("Parsing Error {ParserError}") (errors.rs:107-115)
   try {
     return p.rules_file(out, empty);
-  } catch (Err&) {
-    msg = "Error parsing file " + file_name;
-  } catch (Fail&) {
-    msg = "Error parsing file " + file_name;
+  } catch (Err& e) {
+    msg = "Parsing Error " + p.error_text(e.pos, e.ctx);
+  } catch (Fail& e) {
+    msg = "Parsing Error " + p.error_text(e.pos, e.ctx);
   }
   return false;
 }

@@ -3,8 +3,13 @@
 A PEG restatement of the nom 7.1.3 grammar in ``guard/src/rules/parser.rs`` (function names
 below follow the reference's combinators 1:1, with their file:line).  ``Err`` models
 ``nom::Err::Error`` (recoverable, ``alt`` tries the next branch) and ``Fail`` models
-``nom::Err::Failure`` (raised by ``cut``).  Parse-error *messages* are not restated
-byte-for-byte (only success paths are pinned); a failure raises ``GuardError('ParseError')``.
+``nom::Err::Failure`` (raised by ``cut``).  Both carry nom's ParserError payload (the input
+position the failing combinator saw, and its context), propagated as nom 7.1.3 does: ``alt``
+reports its last alternative's error, ``many1`` / ``separated_list`` their element's,
+``fold_many1`` a fresh error at its own input, ``context`` its input position and "ctx/inner",
+``cut`` turns Error into Failure.  A failed parse raises ``GuardError('ParseError', "Parsing Error
+Error parsing file F at line L at column C, when handling CTX, fragment REST")`` as
+``errors.rs:107-115`` / ``parser.rs:88-101`` display it.
 
 AST nodes are plain dicts/tuples mirroring ``guard/src/rules/exprs.rs``.
 """
@@ -14,11 +19,24 @@ from . import rxcompat
 
 
 class Err(Exception):
-    pass
+    def __init__(self, pos=0, ctx=""):
+        super().__init__(pos, ctx)
+        self.pos, self.ctx = pos, ctx
 
 
 class Fail(Exception):
-    pass
+    def __init__(self, pos=0, ctx=""):
+        super().__init__(pos, ctx)
+        self.pos, self.ctx = pos, ctx
+
+
+def _add_ctx(ctx, inner):
+    """nom ContextError::add_context (parser.rs:48-62)"""
+    return ctx if not inner else "%s/%s" % (ctx, inner)
+
+
+CTX_CMP = "expecting comparison binary operators like >, <= or unary operators KEYS, EXISTS, EMPTY or NOT"
+CTX_RHS = 'expecting either a property access "engine.core" or value like "string" or ["this", "that"]'
 
 
 FUNCTION_ARITY = {
@@ -51,16 +69,22 @@ class Parser:
             col = len(self.s[start:p].encode("utf-8")) + 1
         return {"line": li + 1, "column": col, "file": self.file}
 
+    def error_text(self, p, ctx):
+        """ParserError Display (parser.rs:88-101)"""
+        lc = self.loc(p)
+        return "Error parsing file %s at line %d at column %d, when handling %s, fragment %s" % (
+            self.file, lc["line"], lc["column"], ctx, self.s[p:])
+
     # -- primitives -----------------------------------------------------------
     def tag(self, p, t):
         if self.s.startswith(t, p):
             return p + len(t)
-        raise Err()
+        raise Err(p)
 
     def char(self, p, c):
         if p < self.n and self.s[p] == c:
             return p + 1
-        raise Err()
+        raise Err(p)
 
     def multispace0(self, p):
         while p < self.n and self.s[p] in MULTISPACE:
@@ -75,7 +99,7 @@ class Parser:
     def space1(self, p):
         q = self.space0(p)
         if q == p:
-            raise Err()
+            raise Err(p)
         return q
 
     def digit1(self, p):
@@ -83,7 +107,7 @@ class Parser:
         while q < self.n and "0" <= self.s[q] <= "9":
             q += 1
         if q == p:
-            raise Err()
+            raise Err(p)
         return q
 
     def alpha1(self, p):
@@ -91,7 +115,7 @@ class Parser:
         while q < self.n and (("a" <= self.s[q] <= "z") or ("A" <= self.s[q] <= "Z")):
             q += 1
         if q == p:
-            raise Err()
+            raise Err(p)
         return q
 
     # comment2  parser.rs:111-113
@@ -130,7 +154,7 @@ class Parser:
             q = self.digit1(p)
             v = int(self.s[p:q])
             if v > (1 << 63) - 1:
-                raise Err()
+                raise Err(p)   # map_res: the error is at map_res's input
             return q, ("Int", v)
         except Err:
             pass
@@ -138,7 +162,7 @@ class Parser:
         r = self.digit1(q)
         v = int(self.s[q:r])
         if v > (1 << 63) - 1:
-            raise Err()
+            raise Err(p)
         return r, ("Int", -v)
 
     def parse_string_inner(self, p, ch):
@@ -155,12 +179,12 @@ class Parser:
                 completed.append(frag[:-1])
                 completed.append(ch)
                 if q >= self.n:
-                    raise Err()
+                    raise Err(start_input, "Could not parse string")
                 span = q + 1
                 continue
             completed.append(frag)
             if q >= self.n or self.s[q] != ch:
-                raise Fail()
+                raise Fail(q)   # cut(char(ch))
             return q + 1, ("String", "".join(completed))
 
     def parse_string(self, p):
@@ -173,7 +197,7 @@ class Parser:
         for t, v in (("true", True), ("True", True), ("false", False), ("False", False)):
             if self.s.startswith(t, p):
                 return p + len(t), ("Bool", v)
-        raise Err()
+        raise Err(p)
 
     def _recognize_float(self, p):
         # nom::number::complete::recognize_float (+ nan/inf exceptions)
@@ -189,15 +213,15 @@ class Parser:
         elif q < self.n and self.s[q] == "." and q + 1 < self.n and "0" <= self.s[q + 1] <= "9":
             q = self.digit1(q + 1)
         else:
-            raise Err()
+            raise Err(p)
         if q < self.n and self.s[q] in "eE":
             r = q + 1
             if r < self.n and self.s[r] in "+-":
                 r += 1
             try:
                 r = self.digit1(r)
-            except Err:
-                raise Fail()
+            except Err as e:
+                raise Fail(e.pos, e.ctx)   # cut(digit1)
             q = r
         return q
 
@@ -221,7 +245,7 @@ class Parser:
         if frac or expo:
             r = self._recognize_float(p)
             return r, ("Float", float(self.s[p:r]))
-        raise Err()
+        raise Err(p, "Could not parse floating number")
 
     def parse_regex_inner(self, p):
         regex = []
@@ -231,19 +255,21 @@ class Parser:
             while q < self.n and self.s[q] != "/":
                 q += 1
             if q == span:
-                raise Err()
+                raise Err(span)   # is_not("/")
             frag = self.s[span:q]
             if frag.endswith("\\"):
                 regex.append(frag[:-1])
                 regex.append("/")
                 if q >= self.n:
-                    raise Err()
+                    raise Err(p, "Could not parse regular expression")
                 span = q + 1
                 continue
             regex.append(frag)
             rx = "".join(regex)
             if not rxcompat.is_valid(rx):
-                raise Err()
+                # the reference appends fancy-regex's error text; the alternatives around a regex
+                # literal always report a later alternative's error, so it never reaches a message
+                raise Err(p, "Could not parse regular expression")
             return q, ("Regex", rx)
 
     def parse_regex(self, p):
@@ -255,17 +281,18 @@ class Parser:
     def parse_char(self, p):
         if p < self.n:
             return p + 1, ("Char", self.s[p])
-        raise Err()
+        raise Err(p)
 
     def range_value(self, p):
         p = self.space0(p)
-        for f in (self.parse_float, self.parse_int_value, self.parse_char):
+        for f in (self.parse_float, self.parse_int_value):
             try:
                 q, v = f(p)
                 return self.space0(q), v
             except Err:
                 continue
-        raise Err()
+        q, v = self.parse_char(p)
+        return self.space0(q), v
 
     def parse_range(self, p):
         p = self.char(p, "r")
@@ -273,7 +300,7 @@ class Parser:
             open_ = self.s[p]
             p += 1
         else:
-            raise Err()
+            raise Err(p)
         p, a = self.range_value(p)
         p = self.char(p, ",")
         p, b = self.range_value(p)
@@ -281,7 +308,7 @@ class Parser:
             close = self.s[p]
             p += 1
         else:
-            raise Err()
+            raise Err(p)
         inc = (P.LOWER_INCLUSIVE if open_ == "[" else 0) | (P.UPPER_INCLUSIVE if close == "]" else 0)
         if a[0] == "Int" and b[0] == "Int":
             return p, ("RangeInt", (a[1], b[1], inc))
@@ -289,15 +316,15 @@ class Parser:
             return p, ("RangeFloat", (a[1], b[1], inc))
         if a[0] == "Char" and b[0] == "Char":
             return p, ("RangeChar", (a[1], b[1], inc))
-        raise Fail()
+        raise Fail(p, "Could not parse range")
 
     def parse_scalar_value(self, p):
-        for f in (self.parse_string, self.parse_float, self.parse_int_value, self.parse_bool, self.parse_regex):
+        for f in (self.parse_string, self.parse_float, self.parse_int_value, self.parse_bool):
             try:
                 return f(p)
             except Err:
                 continue
-        raise Err()
+        return self.parse_regex(p)   # alt: the last alternative's error
 
     def separated_list0(self, p, sep, elem):
         out = []
@@ -373,16 +400,16 @@ class Parser:
         for t in ("null", "NULL"):
             if self.s.startswith(t, p):
                 return p + len(t), ("Null", None)
-        raise Err()
+        raise Err(p)
 
     def parse_value(self, p):
         p = self.zero_or_more_ws_or_comment(p)
-        for f in (self.parse_null, self.parse_scalar_value, self.parse_range, self.parse_list, self.parse_map):
+        for f in (self.parse_null, self.parse_scalar_value, self.parse_range, self.parse_list):
             try:
                 return f(p)
             except Err:
                 continue
-        raise Err()
+        return self.parse_map(p)
 
     # -- expressions ----------------------------------------------------------
     def var_name(self, p):
@@ -400,7 +427,7 @@ class Parser:
         for t in ("in", "IN"):
             if self.s.startswith(t, p):
                 return p + len(t), "In"
-        raise Err()
+        raise Err(p)
 
     def not_(self, p):
         for t in ("not", "NOT"):
@@ -416,7 +443,7 @@ class Parser:
             return p + 2, ("Eq", False)
         if self.s.startswith("!=", p):
             return p + 2, ("Eq", True)
-        raise Err()
+        raise Err(p)
 
     _UNARY_WORDS = [
         (("EXISTS", "exists"), "Exists"), (("EMPTY", "empty"), "Empty"),
@@ -444,11 +471,11 @@ class Parser:
             for w in words:
                 if self.s.startswith(w, p):
                     return p + len(w), (op, neg)
-        raise Err()
+        raise Err(p)
 
     def value_cmp(self, p):
         if self.s.startswith("<<", p):
-            raise Err()
+            raise Err(p, "Custom message tag detected")
         try:
             return self.eq(p)
         except Err:
@@ -462,7 +489,7 @@ class Parser:
         p = self.tag(p, "<<")
         j = self.s.find(">>", p)
         if j < 0:
-            raise Fail()
+            raise Fail(p, "Unable to find a closing >> tag for message")
         return j + 2, self.s[p:j]
 
     def variable_capture_in_map_or_index(self, p):
@@ -481,8 +508,8 @@ class Parser:
     def cut(self, f, *a):
         try:
             return f(*a)
-        except Err:
-            raise Fail()
+        except Err as e:
+            raise Fail(e.pos, e.ctx)
 
     def opt(self, f, p):
         try:
@@ -563,7 +590,7 @@ class Parser:
                 p += len(t)
                 break
         else:
-            raise Err()
+            raise Err(p)
 
         def cmp_(q):
             q = self.zero_or_more_ws_or_comment(q)
@@ -598,13 +625,12 @@ class Parser:
         return p, ("MapKeyFilter", var, {"comparator": cmp, "compare_with": with_v})
 
     def predicate_or_index(self, p):
-        for f in (self.all_indices, self.array_index, self.map_key_lookup, self.map_keys_match,
-                  self.predicate_filter_clauses):
+        for f in (self.all_indices, self.array_index, self.map_key_lookup, self.map_keys_match):
             try:
                 return f(p)
             except Err:
                 continue
-        raise Err()
+        return self.predicate_filter_clauses(p)
 
     def dotted_access(self, p):
         def one(q):
@@ -612,7 +638,10 @@ class Parser:
                 return self.dotted_property(q)
             except Err:
                 return self.predicate_or_index(q)
-        p, v = one(p)
+        try:
+            p, v = one(p)
+        except Err:
+            raise Err(p)   # fold_many1: from_error_kind(input, Many1)
         out = [v]
         while True:
             try:
@@ -634,14 +663,14 @@ class Parser:
         for t in ("SOME", "some"):
             if self.s.startswith(t, p):
                 return self.one_or_more_ws_or_comment(p + len(t))
-        raise Err()
+        raise Err(p)
 
     def this_keyword(self, p):
         p = self.zero_or_more_ws_or_comment(p)
         for t in ("this", "THIS"):
             if self.s.startswith(t, p):
                 return p + len(t), ("This",)
-        raise Err()
+        raise Err(p)
 
     def access(self, p):
         r = self.opt(self.some_keyword, p)
@@ -679,7 +708,10 @@ class Parser:
             pass
         p, query = self.access(p)
         p = self.zero_or_more_ws_or_comment(p)
-        p, cmp = self.value_cmp(p)
+        try:
+            p, cmp = self.value_cmp(p)
+        except Err as e:   # context(.., value_cmp)  parser.rs:974
+            raise Err(p, _add_ctx(CTX_CMP, e.ctx))
         if cmp[0] in UNARY_OPS:
             q = self.zero_or_more_ws_or_comment(p)
             msg = None
@@ -690,29 +722,38 @@ class Parser:
             return p, {"kind": kind, "query": query, "comparator": cmp, "compare_with": None,
                        "custom_message": msg, "location": location, "negation": negation}
 
+        def with_msg(r):
+            q = self.zero_or_more_ws_or_comment(r)
+            try:
+                return self.custom_message(q)
+            except Err:
+                return q, None
+
         def rhs(q):
             try:
                 r, v = self.parse_value(q)
-                return r, ("Value", P.from_value(_lit(v)))
+                v = ("Value", P.from_value(_lit(v)))
+                r, m = with_msg(r)
+                return r, (v, m)
             except Err:
                 pass
             try:
                 r = self.zero_or_more_ws_or_comment(q)
                 r, f = self.function_expr(r)
-                return r, ("Func", f)
+                r, m = with_msg(r)
+                return r, (("Func", f), m)
             except Err:
                 pass
             r = self.zero_or_more_ws_or_comment(q)
             r, acc = self.access(r)
-            return r, ("Access", acc)
+            r, m = with_msg(r)
+            return r, (("Access", acc), m)
 
-        p, with_v = self.cut(rhs, p)
-        q = self.zero_or_more_ws_or_comment(p)
-        msg = None
+        # context(.., cut(alt(...)))  parser.rs:1000-1023
         try:
-            p, msg = self.custom_message(q)
-        except Err:
-            p = q
+            p, (with_v, msg) = self.cut(rhs, p)
+        except Fail as e:
+            raise Fail(p, _add_ctx(CTX_RHS, e.ctx))
         return p, {"kind": kind, "query": query, "comparator": cmp, "compare_with": with_v,
                    "custom_message": msg, "location": location, "negation": negation}
 
@@ -735,15 +776,17 @@ class Parser:
         for t in tags:
             if self.s.startswith(t, p):
                 return p + len(t)
-        raise Err()
+        raise Err(p)
 
     def function_expr(self, p):
         location = self.loc(p, utf8=False)
         p, (name, params) = self.call_expr(p)
+        # parser.rs:1082-1100, errors at the input after the call
         if name not in FUNCTION_ARITY:
-            raise Err()
+            raise Err(p, "Parser Error when parsing `No function with the name '%s' exists.`" % name)
         if len(params) != FUNCTION_ARITY[name]:
-            raise Err()
+            raise Err(p, "function: %s requires: %d parameters to be passed, but received: %d"
+                      % (name, FUNCTION_ARITY[name], len(params)))
         return p, {"name": name, "parameters": params, "location": location}
 
     def let_value(self, p):
@@ -815,7 +858,7 @@ class Parser:
         for t in ("\n", "\r\n"):
             if self.s.startswith(t, p):
                 return p + len(t)
-        raise Err()
+        raise Err(p)
 
     def rule_clause(self, p):
         location = self.loc(p)
@@ -847,12 +890,14 @@ class Parser:
 
     def cnf_clauses(self, p, f):
         conj = []
+        p0 = p
         while True:
             try:
                 p2, disj = self.disjunction_clauses(p, f)
             except Err:
-                if not conj:
-                    raise Fail()
+                if not conj:   # parser.rs:1300-1312
+                    lc = self.loc(p0)
+                    raise Fail(p0, "There were no clauses present %s#%d@%d" % (self.file, lc["line"], lc["column"]))
                 return p, conj
             p = p2
             conj.append(disj)
@@ -941,7 +986,10 @@ class Parser:
             r, d = self.disjunction_clauses(q, clause_parser)
             return r, ("conj", d)
 
-        p, v = item(p)
+        try:
+            p, v = item(p)
+        except Err:
+            raise Err(p)   # fold_many1
         items = [v]
         while True:
             try:
@@ -1093,11 +1141,16 @@ class Parser:
                     r, v = f(q)
                     return self.zero_or_more_ws_or_comment(r), (kind, v)
                 except Err:
+                    if kind == "DefaultClause":
+                        raise
                     continue
-            raise Err()
 
         try:
-            p, e = one(p)
+            p0 = p
+            try:
+                p, e = one(p)
+            except Err:
+                raise Err(p0)   # fold_many1: from_error_kind(input, Many1)
             exprs.append(e)
             while True:
                 try:
@@ -1106,10 +1159,10 @@ class Parser:
                     break
                 exprs.append(e)
                 p = q
-        except (Err, Fail):
-            raise GuardError("ParseError", "Error parsing file %s at offset %d" % (self.file, p))
-        if p != self.n:
-            raise GuardError("ParseError", "Error parsing file %s at offset %d" % (self.file, p))
+            if p != self.n:
+                raise Err(p)    # all_consuming: Eof
+        except (Err, Fail) as e:
+            raise GuardError("ParseError", "Parsing Error " + self.error_text(e.pos, e.ctx))
 
         assignments, named, param, default = [], [], [], []
         for kind, v in exprs:
@@ -1158,10 +1211,7 @@ def _lit(v):
 
 def parse_rules(text: str, file_name: str):
     """``rules_file`` parser.rs:1840-1932.  Returns None for an empty/comment-only file."""
-    try:
-        return Parser(text, file_name).rules_file()
-    except Fail:
-        raise GuardError("ParseError", "Error parsing file %s" % file_name)
+    return Parser(text, file_name).rules_file()
 
 
 # ---------------------------------------------------------------------------

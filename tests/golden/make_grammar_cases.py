@@ -4,6 +4,10 @@ lifted to whole rules files so both of our parsers (csrc/rules_parser.cpp throug
 oracle/guard_oracle/parser.py) can be checked against them.  Run once in the build container:
     python tests/golden/make_grammar_cases.py /root/reference
 
+Also builds tests/golden/parse_error_cases.json: the parse-error messages the reference pins (spans
+and contexts its parser tests assert for Failures that reach rules_file unchanged, and the
+`cfn-guard test` golden for invalid_rule.guard).
+
 Each case is {"id", "src" (parser_tests.rs line), "how", "text", "accept"}.  `how` says how the
 sub-parser input became a rules file:
   file    the text is a whole rules file / rule / type block / assignment already
@@ -188,6 +192,49 @@ def main():
     out = os.path.join(os.path.dirname(os.path.abspath(__file__)), "grammar_cases.json")
     json.dump(cases, open(out, "w"), indent=1, ensure_ascii=False)
     print(len(cases), "cases ->", out)
+    errors_fixture(lines)
+
+
+CTX_RHS = 'expecting either a property access "engine.core" or value like "string" or ["this", "that"]'
+
+
+def display(file, text, off, ctx):
+    """Error::ParseError(format!("Parsing Error {ParserError}")) as errors.rs:20,107-115 and
+    parser.rs:88-101 display it, for a single-line text (line 1, column = chars before + 1)"""
+    return "Parser Error when parsing `Parsing Error Error parsing file %s at line 1 at column %d, when handling %s, " \
+           "fragment %s`" % (file, len(text[:off]) + 1, ctx, text[off:])
+
+
+def errors_fixture(lines):
+    """parse-error messages the reference pins: spans + contexts its parser unit tests assert for
+    errors that reach the top of rules_file unchanged (Failures: no alt / context() above them),
+    and the test command's golden (guard/tests/test_command.rs:183-200)"""
+    out = []
+    for lhs in ("configuration.containers.*.image", "engine"):   # test_clause_failures 1934-1953
+        for op in (">", "<", "==", "!="):
+            t = "%s %s << message >>" % (lhs, op)
+            out.append({"src": "parser_tests.rs:1936", "file": "g.guard", "text": t,
+                        "expected": display("g.guard", t, len(lhs) + len(op) + 1, CTX_RHS)})
+    # test_predicate_clause_success #4 / #5 (1865-1878): a Failure out of access()
+    t = "resources.*[] exists"
+    out.append({"src": "parser_tests.rs:1866", "file": "g.guard", "text": t,
+                "expected": display("g.guard", t, len("resources.*["), "There were no clauses present g.guard#1@13")})
+    t = "resources.*[type == /AWS::RDS/"
+    out.append({"src": "parser_tests.rs:1872", "file": "g.guard", "text": t, "expected": display("g.guard", t, len(t), "")})
+    # test_command.rs:183-200: `cfn-guard test` on resources/test-command/rule-dir/invalid_rule.guard
+    tc = open(os.path.join(ROOT, "guard", "tests", "test_command.rs"), encoding="utf-8").read()
+    i = tc.index("fn test_parse_error_when_guard_rule_has_syntax_error")
+    j = tc.index('r#"Parse Error on ruleset file ', i) + len('r#"Parse Error on ruleset file ')
+    k = tc.index('"#', j)
+    golden = tc[j:k]
+    assert golden.endswith("`\n")
+    rule = open(os.path.join(ROOT, "guard", "resources", "test-command", "rule-dir", "invalid_rule.guard"),
+                encoding="utf-8").read()
+    out.append({"src": "test_command.rs:193", "file": "resources/test-command/rule-dir/invalid_rule.guard",
+                "text": rule, "expected": golden[:-1]})
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "parse_error_cases.json")
+    json.dump(out, open(path, "w"), indent=1, ensure_ascii=False)
+    print(len(out), "pinned parse errors ->", path)
 
 
 if __name__ == "__main__":

@@ -35,3 +35,44 @@ def _oracle(text):
 def test_grammar_case(case):
     assert _native(case["text"]) == case["accept"], ("native", case["src"], case["text"])
     assert _oracle(case["text"]) == case["accept"], ("oracle", case["src"], case["text"])
+
+
+# ---- parse-error text (FFI code 5 message, `cfn-guard test` "Parse Error on ruleset file ...") ----
+ERRORS = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "parse_error_cases.json"), encoding="utf-8"))
+
+
+def _native_msg(text, name):
+    with pytest.raises(guard_amd.GuardError) as ei:
+        guard_amd.parse_rules(text, name)
+    assert ei.value.code == 5
+    return ei.value.message
+
+
+def _oracle_msg(text, name):
+    with pytest.raises(OracleGuardError) as ei:
+        oracle_parse_rules(text, name)
+    return ei.value.display()
+
+
+@pytest.mark.parametrize("case", ERRORS, ids=["%s_%d" % (c["src"].replace(":", "_"), i) for i, c in enumerate(ERRORS)])
+def test_pinned_parse_error_text(case):
+    """messages the reference pins: nom's position + context of the Failure, the fragment after it"""
+    assert _native_msg(case["text"], case["file"]) == case["expected"]
+    assert _oracle_msg(case["text"], case["file"]) == case["expected"]
+
+
+UNPINNED_BAD = [
+    "rule r { }", "rule r {\n  Resources exists\n", "x ==", "let x", "x exists\n}\n", "rule 5 {}", "x == 'abc",
+    "x exists <<msg", "x == 5 <<msg", "rule r when { x exists }", "AWS::S3::Bucket", "AWS::S3::Bucket{ x exists }",
+    "rule r(a { }", "let a = count(", "x in [1,2", "x == {a: 1", "x.y[ z == 1 exists", "x.y[KEYS == ] exists",
+    "%a.b exists << ok >> trailing", "rule p(a, ) { %a exists }", "when x exists { }", "x == r(1, 'a')", "x == 1.5e",
+    "x == /abc", "x == foo(1)", "let c = count(a, b)\nrule r { %c > 1 }", "régle r { x exists }", "x == 'café' y",
+    "rule r {\n  AWS::S3::Bucket {\n    Properties.x == [1,\n  }\n}\n", "let x = Resources.*[ Type == ]\n",
+]
+
+
+@pytest.mark.parametrize("text", UNPINNED_BAD + [c["text"] for c in CASES if c["accept"] is False])
+def test_parse_error_text_native_equals_oracle(text):
+    """every rejected grammar case and a set of malformed files: the product's parser reports the
+    same nom error (position, context, fragment) as the oracle's independent restatement"""
+    assert _native_msg(text, "g.guard") == _oracle_msg(text, "g.guard")
