@@ -411,8 +411,8 @@ void session_upload(gg_session* s) {
   s->rec_cap = std::min<size_t>(std::max<size_t>(ntiles * 48, 4096), (size_t)96 * 1024 * 1024);
   s->dv->d_recs.alloc(s->rec_cap);
   s->dv->d_counters.alloc(32);   // [0..6] cursors / counts, [16..23] per-XCD lane-mode queues
-  s->dv->d_stats.alloc(16);
-  HIPCHK(hipMemsetAsync(s->dv->d_stats.p, 0, 16 * sizeof(unsigned long long), st));
+  s->dv->d_stats.alloc(32);
+  HIPCHK(hipMemsetAsync(s->dv->d_stats.p, 0, 32 * sizeof(unsigned long long), st));
   s->ncounts = s->progs.size() * (s->max_top + 1) * 4;
   if (s->ncounts * sizeof(uint32_t) > 60 * 1024)
     throw std::runtime_error("too many (rules file x rule) tallies for one LDS block; split the rules files across sessions");
@@ -1432,9 +1432,9 @@ double gg_session_last_kernel_ms(gg_session* s) { return s->last_kernel_ms; }
 // map entries scanned by key lookups, fast-filter tests, tiles
 int32_t gg_session_kernel_stats(gg_session* s, uint64_t* out, size_t n) {
   if (!s->dv || !s->dv->d_stats.p) return -1;
-  std::vector<unsigned long long> v(16);
-  HIPCHK(hipMemcpy(v.data(), s->dv->d_stats.p, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-  for (size_t i = 0; i < n && i < 16; i++) out[i] = v[i];
+  std::vector<unsigned long long> v(32);
+  HIPCHK(hipMemcpy(v.data(), s->dv->d_stats.p, 32 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  for (size_t i = 0; i < n && i < 32; i++) out[i] = v[i];
   return 0;
 }
 

@@ -301,6 +301,16 @@ struct Compiler {
       }
       local.push_back(pp);
     }
+    // PPart.b of a `%var` head or a `*` / `[*]` step: 1 when a later step reads the scope a value
+    // frame would give each fanned-out value (a filter, a map-key filter or a `%var` key); the walker
+    // pushes value frames only then (eval_core.inc walk_run)
+    for (size_t i = 0; i < local.size(); i++) {
+      PPart& pp = local[i];
+      if (pp.kind != P_VAR_HEAD && pp.kind != P_ALL_VALUES && pp.kind != P_ALL_INDICES) continue;
+      pp.b = 0;
+      for (size_t j = i + 1; j < local.size(); j++)
+        if (local[j].kind == P_FILTER || local[j].kind == P_MAP_KEY_FILTER || local[j].kind == P_KEY_VAR) pp.b = 1;
+    }
     queries[qid].first = (uint32_t)parts.size();
     queries[qid].n = (uint32_t)local.size();
     for (auto& pp : local) parts.push_back(pp);

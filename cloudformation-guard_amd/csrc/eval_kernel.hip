@@ -86,7 +86,9 @@ __device__ __attribute__((always_inline)) inline void tile_begin(CtxT& c, const 
   c.tix = c.resmap != NONE ? A.docs.tix + A.docs.tix_off[doc] : nullptr;
   c.type_key = A.docs.type_key; c.ffok = NONE; c.naux = 0;
 #ifdef GG_STATS
-  for (int i = 0; i < 8; i++) c.st[i] = 0;
+  for (int i = 0; i < 8; i++) { c.st[i] = 0; c.tdep[i] = 0; }
+  for (int i = 0; i < 9; i++) c.tst[i] = 0;
+  c.tst[8] = __builtin_amdgcn_s_memtime();
 #endif
 }
 template <typename CtxT>
@@ -94,6 +96,8 @@ __device__ __attribute__((always_inline)) inline void tile_stats(CtxT& c, const 
 #ifdef GG_STATS
   for (int i = 0; i < 8; i++) atomicAdd(&A.stats[i], (unsigned long long)c.st[i]);
   atomicAdd(&A.stats[8], 1ull);
+  c.tst[8] = __builtin_amdgcn_s_memtime() - c.tst[8];
+  for (int i = 0; i < 9; i++) atomicAdd(&A.stats[9 + i], c.tst[i]);
 #endif
 }
 

@@ -386,8 +386,8 @@ class Session:
         return list(buf)[:min(n, cap)]
 
     def kernel_stats(self):
-        out = (ctypes.c_uint64 * 16)()
-        lib().gg_session_kernel_stats(self.s, out, 16)
+        out = (ctypes.c_uint64 * 32)()
+        lib().gg_session_kernel_stats(self.s, out, 32)
         return list(out)
 
     def counts(self):

@@ -11,9 +11,19 @@ import rulepack  # noqa: E402
 
 NAMES = ["node_reads", "heap_accesses", "query_calls", "clause_evals", "frames", "records", "map_entries_scanned",
          "fast_filter_tests"]
+# inclusive shader-clock cycles per tile (outermost entry of each category; lanes of a wave share time)
+TIMES = ["eval_rule", "query_retrieval", "binary_operation", "unary_operation", "rec_push", "filter_test",
+         "resolve_variable", "push_frame", "tile_total"]
 ndocs = int(sys.argv[1]) if len(sys.argv) > 1 else 20000
 out = {}
-for name, text in rulepack.rule_pack():
+PACK = os.environ.get("PACK", "cfg2")
+if PACK == "micro":
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from micro_cases import CASES  # noqa: E402
+    FILES = [(k + ".guard", v) for k, v in CASES.items()]
+else:
+    FILES = rulepack.rule_pack(PACK)
+for name, text in FILES:
     s = guard_amd.Session()
     s.add_rules(text, name)
     s.add_synthetic(0, ndocs, threads=16)
@@ -23,5 +33,6 @@ for name, text in rulepack.rule_pack():
     tiles = max(1, st[8])
     out[name] = {"kernel_ms": round(min(ms), 3), "tiles": st[8]}
     out[name].update({k: round(st[i] / tiles, 1) for i, k in enumerate(NAMES)})
+    out[name]["cycles_per_tile"] = {k: round(st[9 + i] / tiles) for i, k in enumerate(TIMES)}
     s.close()
 print(json.dumps(out, indent=1))

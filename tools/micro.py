@@ -7,17 +7,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "cloudformation-guard_amd"), os.path.join(ROOT, "tests")]
 import guard_amd  # noqa: E402
 
-CASES = {
-    "exists_root": "rule r { Resources exists }",
-    "let_typefilter": "let b = Resources.*[ Type == 'AWS::S3::Bucket' ]\nrule r when %b !empty { %b exists }",
-    "all_props_exists": "rule r { Resources.*.Properties exists }",
-    "all_tags_empty": "rule r { Resources.*.Properties.Tags !empty }",
-    "typeblock_1": "rule r { AWS::S3::Bucket { Properties.BucketName exists } }",
-    "typeblock_3": "rule r { AWS::S3::Bucket { Properties.BucketName exists\n Properties.VersioningConfiguration exists\n Properties.LoggingConfiguration exists } }",
-    "var_eq_5": "let b = Resources.*[ Type == 'AWS::S3::Bucket' ]\nrule r when %b !empty {\n" + "\n".join(
-        "  %%b.Properties.PublicAccessBlockConfiguration.%s == true" % k for k in
-        ["BlockPublicAcls", "BlockPublicPolicy", "IgnorePublicAcls", "RestrictPublicBuckets", "BlockPublicAcls"]) + "\n}",
-}
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from micro_cases import CASES  # noqa: E402
 ndocs = int(sys.argv[1]) if len(sys.argv) > 1 else 100000
 s = guard_amd.Session()
 for k, v in CASES.items():
