@@ -26,8 +26,10 @@ YAML_LIB = "/opt/conda/lib"
 HOST_SRCS = ["doc_loader.cpp", "rules_parser.cpp", "regex_dfa.cpp", "cruet.cpp", "compiler.cpp", "reporter.cpp",
              "synth_corpus.cpp"]
 HIP_SRCS = ["eval_kernel.hip", "json_gpu.hip", "capi.cpp"]
-# occupancy target of the lane-mode kernel (waves per SIMD); it caps VGPRs at 512 / N
-LANE_WAVES_PER_EU = os.environ.get("GG_LANE_WAVES_PER_EU", "2")
+# occupancy target of the lane-mode kernel (waves per SIMD); it caps VGPRs at 512 / N.  4 (126 VGPRs,
+# 8 spilled) beats 2 (178) and 3 (168): the kernel waits on dependent loads, so resident waves are
+# worth more than registers (profiles/r02_ab_occupancy.log; capi.cpp sizes the grid to 16 waves/CU)
+LANE_WAVES_PER_EU = os.environ.get("GG_LANE_WAVES_PER_EU", "4")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-I" + YAML_INC, "-Wno-unused-result",
          "-DGG_LANE_WAVES_PER_EU=" + LANE_WAVES_PER_EU]
 
@@ -61,7 +63,7 @@ def build(verbose=False, variant=""):
     flags = list(FLAGS)
     if variant == "stats":
         flags.append("-DGG_STATS")
-    elif variant == "ab":
+    elif variant.startswith("ab"):
         flags += shlex.split(os.environ.get("GG_AB_FLAGS", ""))
     elif variant:
         raise ValueError("unknown build variant %r" % variant)

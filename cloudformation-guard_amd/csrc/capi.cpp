@@ -325,6 +325,8 @@ void session_upload(gg_session* s) {
   {
     // host arena (32 B nodes) -> device arena (16 B packed nodes + key-length column)
     const size_t n = s->docs.nodes.size();
+    // lane-mode tiles address their document by a 32-bit global node index (eval_core.inc Ctx)
+    if (n >= 0xFFFFFFFFull) throw std::runtime_error("batch too large for one session: split it (>= 2^32 arena nodes)");
     DBuf<DNode> tmp;
     tmp.upload(s->docs.nodes.data(), n, st);
     s->dv->d_nodes.alloc(std::max<size_t>(n, 1));
@@ -398,7 +400,7 @@ void session_upload(gg_session* s) {
   s->nslots = slots;
   s->dv->d_heaps.alloc((size_t)slots * s->heap_bytes);
   // lane-mode grid: waves per CU (default 8 = the kernel's occupancy at 2 waves/SIMD)
-  size_t lane_waves_per_cu = 8;
+  size_t lane_waves_per_cu = 16;   // 4 waves per SIMD (build.py GG_LANE_WAVES_PER_EU); LDS holds 16 at cfg-2 program sizes
   if (const char* e = getenv("GG_LANE_WAVES_PER_CU")) lane_waves_per_cu = std::max(1, atoi(e));
   s->lane_slots = s->mode == 1 ? 0 : (uint32_t)std::min<size_t>(std::max<size_t>(nbatches, 1), (size_t)g_dev.ncu * lane_waves_per_cu);
   // every one of the 8 per-XCD queues needs waves (block b serves queue b % 8)

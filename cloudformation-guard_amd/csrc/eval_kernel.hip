@@ -74,17 +74,34 @@ __device__ __attribute__((always_inline)) inline const DevProg* stage_program(co
   return sp;
 }
 
-// Shared per-tile prologue: scratch heap layout, root frame, memo table.
+// Shared per-tile prologue: scratch heap layout, root frame, memo table.  Lane mode: the wave's
+// shared values (heap, arena bases, heap layout) are in ln::g_wave (set once per wave); wave mode
+// keeps them in the Ctx.
 template <typename CtxT>
+__device__ __attribute__((always_inline)) inline void tile_ptrs_lane(CtxT& c, const LaunchArgs& A, uint32_t doc) {
+  c.dbase = (uint32_t)A.docs.base[doc];
+  c.resmap = A.docs.res_map ? A.docs.res_map[doc] : NONE;
+  c.tix_off = c.resmap != NONE ? A.docs.tix_off[doc] : NONE;
+}
+template <typename CtxT>
+__device__ __attribute__((always_inline)) inline void tile_ptrs_wave(CtxT& c, const LaunchArgs& A, const DevProg* P,
+                                                                     uint32_t doc, uint8_t* heap, uint32_t frames_bytes,
+                                                                     uint32_t recs_bytes) {
+  c.P = (decltype(c.P))P; c.dn = A.docs.nodes + A.docs.base[doc]; c.kl = A.docs.klen + A.docs.base[doc]; c.db = A.docs.bytes; c.heap = heap;
+  c.fcap = frames_bytes; c.rcap = recs_bytes;
+  c.resmap = A.docs.res_map ? A.docs.res_map[doc] : NONE;
+  c.tix = c.resmap != NONE ? A.docs.tix + A.docs.tix_off[doc] : nullptr;
+  c.type_key = A.docs.type_key;
+}
+template <bool LANE, typename CtxT>
 __device__ __attribute__((always_inline)) inline void tile_begin(CtxT& c, const LaunchArgs& A, const DevProg* P,
                                                                  uint32_t doc, uint8_t* heap, uint32_t heap_bytes,
                                                                  uint32_t frames_bytes, uint32_t recs_bytes) {
-  c.P = (decltype(c.P))P; c.dn = A.docs.nodes + A.docs.base[doc]; c.kl = A.docs.klen + A.docs.base[doc]; c.db = A.docs.bytes; c.heap = heap; c.cap = heap_bytes;
-  c.tmp = frames_bytes + recs_bytes; c.pers = heap_bytes; c.fcap = frames_bytes; c.rcap = recs_bytes; c.nframes = 0; c.nrec = 0;
+  if constexpr (LANE) tile_ptrs_lane(c, A, doc);
+  else tile_ptrs_wave(c, A, P, doc, heap, frames_bytes, recs_bytes);
+  c.tmp = frames_bytes + recs_bytes; c.pers = heap_bytes; c.nframes = 0; c.nrec = 0;
   c.err = 0; c.err_a = 0; c.err_b = 0; c.suppress = 0; c.rec_created = 0; c.depth = 0; c.nsyn = 0;
-  c.resmap = A.docs.res_map ? A.docs.res_map[doc] : NONE;
-  c.tix = c.resmap != NONE ? A.docs.tix + A.docs.tix_off[doc] : nullptr;
-  c.type_key = A.docs.type_key; c.ffok = NONE; c.naux = 0;
+  c.ffok = NONE; c.naux = 0;
 #ifdef GG_STATS
   for (int i = 0; i < 8; i++) { c.st[i] = 0; c.tdep[i] = 0; }
   for (int i = 0; i < 9; i++) c.tst[i] = 0;
@@ -123,6 +140,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
   __shared__ Ctx s_ctx[64];
   extern __shared__ uint4 s_blob[];
   LCtx& c = *(LCtx*)&s_ctx[lane];
+  if (lane == 0) {
+    g_wave.heap = heap; g_wave.nodes = A.docs.nodes; g_wave.klen = A.docs.klen; g_wave.db = A.docs.bytes;
+    g_wave.tix = A.docs.tix; g_wave.fcap = FRAMES_BYTES; g_wave.rcap = RECS_BYTES; g_wave.type_key = A.docs.type_key;
+  }
+  __syncthreads();
   uint32_t staged = NONE;
   const DevProg* P = nullptr;
   for (;;) {
@@ -143,8 +165,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
       continue;
     }
     if (active) {
-      tile_begin(c, A, P, doc, heap, A.lane_heap_bytes, FRAMES_BYTES, RECS_BYTES);
-      c.lane16 = lane * 16u;
+      tile_begin<true>(c, A, P, doc, heap, A.lane_heap_bytes, FRAMES_BYTES, RECS_BYTES);
       c.syn_off = alloc_pers(c, 256 * 16);
       c.wbase = alloc_pers(c, WLEVELS * (uint32_t)sizeof(WLevel)); c.wdepth = 0;
       c.memo = alloc_pers(c, (P->n_slots ? P->n_slots : 1) * 4);
@@ -213,8 +234,7 @@ __global__ void __launch_bounds__(64) guard_eval_kernel(LaunchArgs A) {
     uint32_t tile = A.retry_list ? A.retry_list[t] : A.tile_base + t;
     uint32_t doc = tile / A.nfiles, file = tile % A.nfiles;
     if (file != staged) { P = stage_program(&A.progs[file], &s_prog, s_blob, A.lds_prog_words); staged = file; }
-    tile_begin(c, A, P, doc, heap, A.heap_bytes, A.wave_frames_bytes, A.wave_recs_bytes);
-    c.lane16 = 0;
+    tile_begin<false>(c, A, P, doc, heap, A.heap_bytes, A.wave_frames_bytes, A.wave_recs_bytes);
     c.syn_off = alloc_pers(c, 256 * 16);
       c.wbase = alloc_pers(c, WLEVELS * (uint32_t)sizeof(WLevel)); c.wdepth = 0;
     c.memo = alloc_pers(c, (P->n_slots ? P->n_slots : 1) * 4);

@@ -287,3 +287,20 @@ def test_parallel_report_matches_serial():
         os.environ.pop("GG_REPORT_THREADS", None)
         os.environ.pop("GG_REPORT_BLOCK", None)
     s.close()
+
+
+def test_duplicate_yaml_keys_vs_oracle():
+    """a repeated mapping key keeps its first position and takes the last value
+    (MapValue.values is an IndexMap, path_value.rs:453-470); value queries over such documents,
+    in every output format, against the oracle (PyYAML keeps the same first-position / last-value
+    mapping).  `keys` filters over a duplicate key are the documented exception."""
+    data = [("dup.yaml", "Resources:\n  b:\n    Type: AWS::S3::Bucket\n    Properties:\n      Port: 1\n      Name: x\n"
+                         "      Port: 2\n  c:\n    Type: AWS::S3::Bucket\n    Type: AWS::EC2::Volume\n    Properties:\n"
+                         "      Size: 300\n")]
+    rules = [("dup.guard", "rule ports { Resources.*[ Type == 'AWS::S3::Bucket' ].Properties.Port == 1 }\n"
+                           "rule vols { AWS::EC2::Volume { Properties.Size <= 256 } }\n"
+                           "rule order { Resources.b.Properties.* exists }\n")]
+    for fmt in ("json", "yaml", "sarif", "junit"):
+        exp, ecode, _ = oracle_validate(rules, data, output=fmt)
+        out, code = guard_amd.validate_structured(rules, data, output=fmt)
+        assert (code, out) == (ecode, exp), fmt
