@@ -31,6 +31,7 @@
 
 namespace gg {
 __global__ void guard_eval_kernel(LaunchArgs A);
+__global__ void guard_eval_verbose_kernel(LaunchArgs A);
 __global__ void guard_eval_lanes_kernel(LaunchArgs A);
 __global__ void resource_type_kernel(DevBatch D);
 __global__ void pack_nodes_kernel(const DNode* in, DNodeP* out, uint32_t* klen, uint64_t n, uint32_t* bad);
@@ -298,6 +299,7 @@ struct gg_session {
   uint32_t lds_prog_words = 2048;              // per-launch program staging window (words)
   static constexpr uint32_t kMaxLdsProgWords = 4096;   // 16 KB
   int32_t mode = 0;               // 0: lane mode + wave-mode retry; 1: wave mode only
+  bool verbose = false;           // wave mode recording the EventRecord tree (guard_eval_verbose_kernel)
   size_t rec_cap = 0;
   // results
   std::vector<TileOut> tiles;
@@ -467,7 +469,8 @@ void session_launch(gg_session* s) {
     hipLaunchKernelGGL(guard_eval_lanes_kernel, dim3(s->lane_slots), dim3(64), A.lds_prog_words * 4, st, A);
     HIPCHK(hipGetLastError());
   }
-  hipLaunchKernelGGL(guard_eval_kernel, dim3(s->nslots), dim3(64), A.lds_prog_words * 4, st, A);
+  auto wave_kernel = s->verbose ? guard_eval_verbose_kernel : guard_eval_kernel;
+  hipLaunchKernelGGL(wave_kernel, dim3(s->nslots), dim3(64), A.lds_prog_words * 4, st, A);
   HIPCHK(hipGetLastError());
   if (s->dv->d_big_heaps.p) {
     // large-heap pass over the wave pass's overflow list (counters[4]; its cursor is counters[6]);
@@ -478,7 +481,7 @@ void session_launch(gg_session* s) {
     B.heaps = s->dv->d_big_heaps.p; B.heap_bytes = gg_session::kBigHeap; B.nslots = gg_session::kBigSlots;
     B.wave_frames_bytes = gg_session::kBigFrames; B.wave_recs_bytes = gg_session::kBigRecs;
     B.retry2_list = nullptr; B.retry2_count = nullptr;
-    hipLaunchKernelGGL(guard_eval_kernel, dim3(gg_session::kBigSlots), dim3(64), B.lds_prog_words * 4, st, B);
+    hipLaunchKernelGGL(wave_kernel, dim3(gg_session::kBigSlots), dim3(64), B.lds_prog_words * 4, st, B);
     HIPCHK(hipGetLastError());
   }
   HIPCHK(hipEventRecord(s->ev1, st));
@@ -694,10 +697,6 @@ void cfn_guard_free_string(char* s) { free(s); }
 
 char* cfn_guard_run_checks(validate_input_t data, validate_input_t rules, bool verbose, extern_err_t* err) {
   set_err(err, 0, "");
-  if (verbose) {
-    set_err(err, -1, "unsupported on MI355X path: verbose EventRecord tree output (SURVEY.md 8f row 4)");
-    return nullptr;
-  }
   try {
     std::string why;
     if (!ensure_device(why)) { set_err(err, -1, why); return nullptr; }
@@ -720,6 +719,7 @@ char* cfn_guard_run_checks(validate_input_t data, validate_input_t rules, bool v
     auto gp = std::make_unique<GpuProgram>();
     if (!compile_program(rf, rname, gp->prog, perr)) { set_err(err, 5, error_display("ParseError", perr)); return nullptr; }
     s.progs.push_back(std::move(gp));
+    if (verbose) { s.mode = 1; s.verbose = true; }   // one tile, evaluated by the verbose wave kernel
     session_upload(&s);
     session_run(&s, true);
     if (s.tiles[0].err) {
@@ -731,6 +731,13 @@ char* cfn_guard_run_checks(validate_input_t data, validate_input_t rules, bool v
     TileResult tr = tile_view(s.tiles.data(), s.rule_status.data(), s.max_top, s.recs.data(), 0);
     std::string out;
     ReportError re;
+    if (verbose) {
+      if (!verbose_tree(s.docs, 0, s.progs[0]->prog, tr, dname, out, re)) {
+        set_err(err, ffi_code(re.kind), error_display(re.kind, re.msg));
+        return nullptr;
+      }
+      return dup_str(out);
+    }
     std::vector<const Program*> progs{&s.progs[0]->prog};
     std::vector<const TileResult*> tp{&tr};
     if (!report_document(s.docs, 0, progs, tp, 0, out, re)) {

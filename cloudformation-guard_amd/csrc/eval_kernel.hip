@@ -34,6 +34,13 @@ namespace ln {
 #include "eval_core.inc"
 #undef GG_LANE
 }  // namespace ln
+namespace vb {
+#define GG_LANE 0
+#define GG_VERBOSE 1
+#include "eval_core.inc"
+#undef GG_VERBOSE
+#undef GG_LANE
+}  // namespace vb
 
 // ------------------------------------------------------------------ kernels ---
 // Rules program staging: every section of the file's program blob before the regex DFA tables
@@ -217,62 +224,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
 // when A.retry_list is null.
 __global__ void __launch_bounds__(64) guard_eval_kernel(LaunchArgs A) {
   using namespace wv;
-  const uint32_t lane = __lane_id();
-  uint8_t* heap = A.heaps + (size_t)blockIdx.x * A.heap_bytes;
-  const uint32_t ntiles = A.retry_list ? *A.retry_count : A.ntiles;
-  __shared__ Ctx s_ctx[64];
-  __shared__ DevProg s_prog;
-  extern __shared__ uint4 s_blob[];
-  LCtx& c = *(LCtx*)&s_ctx[lane];
-  uint32_t staged = NONE;
-  const DevProg* P = nullptr;
-  for (;;) {
-    uint32_t t = 0;
-    if (lane == 0) t = atomicAdd(A.tile_cursor + 1, 1u);
-    t = __shfl(t, 0);
-    if (t >= ntiles) break;
-    uint32_t tile = A.retry_list ? A.retry_list[t] : A.tile_base + t;
-    uint32_t doc = tile / A.nfiles, file = tile % A.nfiles;
-    if (file != staged) { P = stage_program(&A.progs[file], &s_prog, s_blob, A.lds_prog_words); staged = file; }
-    tile_begin<false>(c, A, P, doc, heap, A.heap_bytes, A.wave_frames_bytes, A.wave_recs_bytes);
-    c.syn_off = alloc_pers(c, 256 * 16);
-      c.wbase = alloc_pers(c, WLEVELS * (uint32_t)sizeof(WLevel)); c.wdepth = 0;
-    c.memo = alloc_pers(c, (P->n_slots ? P->n_slots : 1) * 4);
-    if (!c.err) for (uint32_t i = 0; i < P->n_slots; i++) u32a(c, c.memo)[i] = 3u;
-    c.vtab = alloc_pers(c, (P->n_vars ? P->n_vars : 1) * 16);
-    if (!c.err) for (uint32_t i = 0; i < P->n_vars; i++) u32a(c, c.vtab)[i * 4] = 0u;
-    push_frame(c, F_ROOT, NONE, A.docs.roots[doc], P->root_block);
-    uint32_t fails = 0, passes = 0;
-    uint8_t* rs = A.rule_status + (size_t)tile * A.max_top;
-    for (uint32_t r = 0; r < P->n_top && !c.err; r++) {
-      uint32_t st = eval_rule(c, P->top_first + r, 0, NONE);
-      if (c.err) break;
-      if (lane == 0) rs[r] = (uint8_t)st;
-      if (st == ST_PASS) passes++; else if (st == ST_FAIL) fails++;
-    }
-    uint32_t status = fails ? ST_FAIL : (passes ? ST_PASS : ST_SKIP);
-    // a tile that outgrows this pass's heap, record staging or frame limits goes to the next pass
-    // (a larger heap per wave), when there is one
-    if (A.retry2_list && lane == 0 && (c.err == E_HEAP || c.err == E_RECORDS || c.err == E_DEPTH))
-      A.retry2_list[atomicAdd(A.retry2_count, 1u)] = tile;
-    // publish records
-    uint32_t off = 0;
-    uint32_t n = c.err ? 0 : c.nrec + c.naux;
-    if (lane == 0 && n) off = atomicAdd(A.rec_cursor, n);
-    off = __shfl(off, 0);
-    if (n && off + n > A.rec_cap) { c.err = E_RECORDS; n = 0; }
-    const uint32_t naux = n ? c.naux : 0, nrec = n - naux;
-    const Rec* src = (const Rec*)(heap + c.fcap);
-    for (uint32_t i = lane; i < nrec; i += 64) A.recs[off + i] = src[i];
-    const Rec* atop = (const Rec*)(heap + c.fcap + c.rcap);
-    for (uint32_t i = lane; i < naux; i += 64) A.recs[off + nrec + i] = atop[-(int32_t)(i + 1)];
-    if (lane == 0) {
-      TileOut o;
-      o.status = status; o.err = c.err; o.err_a = c.err_a; o.err_b = c.err_b;
-      o.rec_off = off; o.rec_n = nrec; o.pad0 = naux; o.pad1 = 0;
-      A.tiles[tile] = o;
-    }
-  }
+#include "wave_tile_loop.inc"
+}
+
+// guard-ffi run_checks(verbose = true): the same wave-mode evaluation recording every event of the
+// reference's EventRecord tree (eval_core.inc, GG_VERBOSE); the host renders it (reporter.cpp
+// verbose_tree).  Launched only for verbose requests, so the two kernels above keep no trace of it.
+__global__ void __launch_bounds__(64) guard_eval_verbose_kernel(LaunchArgs A) {
+  using namespace vb;
+#include "wave_tile_loop.inc"
 }
 
 }  // namespace gg

@@ -173,6 +173,17 @@ enum RecKind : uint32_t {
   REC_BLOCK_EMPTY = 5, REC_MISSING_BLOCK_VALUE = 6, REC_UNARY = 7, REC_NOVALUE_EMPTY = 8,
   REC_DEPENDENT_RULE = 9, REC_CMP = 10, REC_IN = 11, REC_LIST = 12,
   REC_AUX = 13,   // side record (TileOut.pad0 of them after the tile's records): join-key lists of R4 / R5
+  // verbose kernel only (the EventRecord tree, rules/mod.rs:278-355): every event is recorded, in
+  // evaluation order -- container opens / closes and one leaf per value check (failure records
+  // above, REC_SUCCESS for ClauseCheck::Success)
+  REC_EV_OPEN = 14,    // clause: rule / clause id (NONE for file, disjunction, filter); x: EvType; y: TypeBlock value index | filter #conjunctions
+  REC_EV_CLOSE = 15,   // clause, x as the open; y: status | at_least_one_matches << 8; from.uref: RuleCheck custom message id
+  REC_SUCCESS = 16,    // clause id (NONE: a map-key-filter comparison, context "")
+};
+
+enum EvType : uint32_t {
+  EV_FILE = 0, EV_RULE = 1, EV_RULE_COND = 2, EV_DISJ = 3, EV_GAC = 4, EV_NAMED = 5, EV_BLOCK = 6, EV_WHEN = 7,
+  EV_WHEN_COND = 8, EV_TYPE = 9, EV_TYPE_COND = 10, EV_TYPE_VAL = 11, EV_FILTER_MAP = 12, EV_FILTER_LIST = 13,
 };
 
 // NotComparable reasons carried in Rec.x for REC_CMP

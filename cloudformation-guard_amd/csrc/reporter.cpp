@@ -363,6 +363,22 @@ struct R {
     J a = J::arr(); a.push(J::str(names[op])); a.push(J::boolean(neg)); return a;
   }
   std::string custom(const PClause& pc) const { return pc.e == NONE ? "" : prog.msgs[pc.e]; }
+  // NotComparable reason of a REC_CMP (rc.x != NC_NONE; operators.rs / path_value.rs compare_*)
+  std::string nc_reason(const Rec& rc) const {
+    if (rc.x == NC_TYPES) return std::string("PathAwareValues are not comparable ") + type_info(rc.y >> 8) + ", " + type_info(rc.y & 0xFF);
+    if (rc.x == NC_FLOAT) return "Float values are not comparable";
+    if (rc.x == NC_STRING_IN) return "Type not comparable, " + pav_display(rc.from) + ", " + pav_display(rc.to);
+    return "Can not compare type " + pav_display(rc.from) + ", " + pav_display(rc.to);
+  }
+  // serde of a QueryResult (rules/mod.rs:172-177): externally tagged {"Resolved" | "Literal": PathAwareValue}
+  // or {"UnResolved": {traversed_to, remaining_query, reason}}
+  J qr_json(const QR& q, bool keep_literal) const {
+    const uint32_t k = q.meta & 3u;
+    J o = J::obj();
+    if (k == QR_UNRESOLVED) o.add("UnResolved", unresolved_json(q));
+    else o.add(keep_literal && k == QR_LITERAL ? "Literal" : "Resolved", pav_json(q));
+    return o;
+  }
   J custom_opt(const PClause& pc) const { return pc.e == NONE ? J::null() : J::str(prog.msgs[pc.e]); }
 };
 
@@ -511,14 +527,7 @@ struct Walker {
           std::string ctx = mk ? std::string() : r.prog.ctx[pcp->d];
           std::string cust = mk ? std::string() : r.custom(*pcp);
           std::string errm;
-          if (rc.x) {
-            std::string reason;
-            if (rc.x == NC_TYPES) reason = std::string("PathAwareValues are not comparable ") + type_info(rc.y >> 8) + ", " + type_info(rc.y & 0xFF);
-            else if (rc.x == NC_FLOAT) reason = "Float values are not comparable";
-            else if (rc.x == NC_STRING_IN) reason = "Type not comparable, " + r.pav_display(rc.from) + ", " + r.pav_display(rc.to);
-            else reason = "Can not compare type " + r.pav_display(rc.from) + ", " + r.pav_display(rc.to);
-            errm = " Error = [" + reason + "]";
-          }
+          if (rc.x) errm = " Error = [" + r.nc_reason(rc) + "]";
           J bin = J::obj();
           bin.add("context", J::str(ctx));
           if ((rc.from.meta & 3u) == QR_UNRESOLVED) {
@@ -1211,6 +1220,213 @@ std::string test_report(int32_t fmt, const std::string& rules_name, const std::v
   std::string out;
   pretty(res, 0, out);
   return out;
+}
+
+namespace {
+
+J status_json(uint32_t s) { return J::str(status_str(s)); }
+J block_check(bool alo, uint32_t st) {
+  J b = J::obj();
+  b.add("at_least_one_matches", J::boolean(alo));
+  b.add("status", status_json(st));
+  b.add("message", J::null());
+  return b;
+}
+J tagged(const char* k, J v) { J o = J::obj(); o.add(k, std::move(v)); return o; }
+
+// one open event of the verbose tree
+struct VNode {
+  uint32_t type = 0, id = NONE;
+  std::string ctx;
+  J children = J::arr();
+};
+
+struct VerboseBuilder {
+  const R& r;
+  const std::string& data_name;
+  std::vector<VNode> stack;
+  J root;
+  bool have_root = false;
+
+  const PClause& pc(uint32_t cid) const { return r.prog.clauses[cid]; }
+  const std::string& ctx_d(uint32_t cid) const { return r.prog.ctx[pc(cid).d]; }
+  std::string when_ctx(uint32_t cid) const { return (pc(cid).flags & 1u) ? "RuleClause" : "GuardConditionClause"; }
+
+  void attach(std::string ctx, J container, J children) {
+    J e = J::obj();
+    e.add("context", J::str(ctx));
+    e.add("container", std::move(container));
+    e.add("children", std::move(children));
+    if (stack.empty()) { root = std::move(e); have_root = true; }
+    else stack.back().children.push(std::move(e));
+  }
+  void leaf(std::string ctx, J check) { attach(std::move(ctx), tagged("ClauseValueCheck", std::move(check)), J::arr()); }
+
+  // eval_conjunction_clauses' context: format!("{}#disjunction", type_name::<T>()) (eval.rs:1980), T
+  // the clause type the enclosing container evaluates
+  std::string disj_ctx() const {
+    const uint32_t pt = stack.empty() ? EV_FILE : stack.back().type;
+    const char* t = pt == EV_RULE ? "RuleClause"
+                  : (pt == EV_RULE_COND || pt == EV_TYPE_COND || pt == EV_WHEN_COND) ? "WhenGuardClause"
+                  : "GuardClause";
+    return std::string("cfn_guard::rules::exprs::") + t + "#disjunction";
+  }
+
+  std::string open_ctx(const Rec& rc) const {
+    switch (rc.x) {
+      case EV_FILE: return "File(rules=" + std::to_string(r.prog.n_rules) + ")";
+      case EV_RULE: return r.prog.rule_names[rc.clause];
+      case EV_RULE_COND: return "Rule#" + r.prog.rule_names[rc.clause] + "/When";
+      case EV_DISJ: return disj_ctx();
+      case EV_GAC: return "GuardAccessClause#block" + ctx_d(rc.clause);
+      case EV_NAMED: case EV_BLOCK: case EV_TYPE: return ctx_d(rc.clause);
+      case EV_WHEN: return when_ctx(rc.clause);
+      case EV_WHEN_COND: return when_ctx(rc.clause) + "/When";
+      case EV_TYPE_COND: return ctx_d(rc.clause) + "/When";
+      case EV_TYPE_VAL: return ctx_d(rc.clause) + "/" + std::to_string(rc.y);
+      case EV_FILTER_MAP: return "Filter/Map#" + std::to_string(rc.y);
+      default: return "Filter/List#" + std::to_string(rc.y);
+    }
+  }
+
+  J close_container(const Rec& rc) const {
+    const uint32_t st = rc.y & 0xFFu;
+    const bool alo = (rc.y >> 8) & 1u;
+    switch (rc.x) {
+      case EV_FILE: {
+        J n = J::obj(); n.add("name", J::str(data_name)); n.add("status", status_json(st)); n.add("message", J::null());
+        return tagged("FileCheck", std::move(n));
+      }
+      case EV_RULE: {
+        const uint32_t m = rc.from.uref;
+        J n = J::obj(); n.add("name", J::str(r.prog.rule_names[rc.clause])); n.add("status", status_json(st));
+        n.add("message", m == NONE ? J::null() : J::str(r.prog.msgs[m]));
+        return tagged("RuleCheck", std::move(n));
+      }
+      case EV_RULE_COND: return tagged("RuleCondition", status_json(st));
+      case EV_DISJ: return tagged("Disjunction", block_check(true, st));
+      case EV_GAC: return tagged("GuardClauseBlockCheck", block_check(alo, st));
+      case EV_NAMED: {
+        if (st == ST_PASS) return tagged("ClauseValueCheck", J::str("Success"));
+        J m = J::obj();
+        m.add("rule", J::str(r.prog.ctx[pc(rc.clause).f]));
+        m.add("message", J::null());
+        m.add("custom_message", r.custom_opt(pc(rc.clause)));
+        m.add("status", status_json(ST_FAIL));
+        return tagged("ClauseValueCheck", tagged("DependentRule", std::move(m)));
+      }
+      case EV_BLOCK: return tagged("BlockGuardCheck", block_check(alo, st));
+      case EV_WHEN: return tagged("WhenCheck", block_check(false, st));
+      case EV_WHEN_COND: return tagged("WhenCondition", status_json(st));
+      case EV_TYPE: {
+        J t = J::obj(); t.add("type_name", J::str(r.prog.ctx[pc(rc.clause).f])); t.add("block", block_check(false, st));
+        return tagged("TypeCheck", std::move(t));
+      }
+      case EV_TYPE_COND: return tagged("TypeCondition", status_json(st));
+      case EV_TYPE_VAL: return tagged("TypeBlock", status_json(st));
+      default: return tagged("Filter", status_json(st));
+    }
+  }
+
+  void run(const RecSpan& recs) {
+    for (size_t i = 0; i < recs.size(); i++) {
+      const Rec& rc = recs[i];
+      const bool mk = rc.clause == NONE;   // a map-key-filter comparison: context "", no custom message
+      switch (rc.kind) {
+        case REC_EV_OPEN: {
+          VNode n; n.type = rc.x; n.id = rc.clause; n.ctx = open_ctx(rc);
+          stack.push_back(std::move(n));
+          break;
+        }
+        case REC_EV_CLOSE: {
+          if (stack.empty() || stack.back().type != rc.x) throw Fatal{"IncompatibleError", "MI355X path: unbalanced verbose event records"};
+          VNode n = std::move(stack.back());
+          stack.pop_back();
+          attach(std::move(n.ctx), close_container(rc), std::move(n.children));
+          break;
+        }
+        case REC_SUCCESS: leaf(mk ? std::string() : ctx_d(rc.clause), J::str("Success")); break;
+        case REC_CMP: {
+          const uint32_t op = mk ? (rc.y & 15u) : (pc(rc.clause).flags & 15u);
+          const bool neg = mk ? ((rc.y >> 4) & 1u) : ((pc(rc.clause).flags >> 4) & 1u);
+          J m = J::obj();
+          m.add("comparison", r.comparison(op, neg));
+          m.add("from", r.qr_json(rc.from, false));
+          m.add("to", rc.to.meta == 0xFFFFFFFFu ? J::null() : r.qr_json(rc.to, false));
+          m.add("message", rc.x ? J::str(r.nc_reason(rc)) : J::null());
+          m.add("custom_message", mk ? J::null() : r.custom_opt(pc(rc.clause)));
+          m.add("status", status_json(ST_FAIL));
+          leaf(mk ? std::string() : ctx_d(rc.clause), tagged("Comparison", std::move(m)));
+          break;
+        }
+        case REC_IN: {
+          const uint32_t op = mk ? (rc.y & 15u) : (pc(rc.clause).flags & 15u);
+          const bool neg = mk ? ((rc.y >> 4) & 1u) : ((pc(rc.clause).flags >> 4) & 1u);
+          J to = J::arr();
+          uint32_t got = 0;
+          while (got < rc.x && i + 1 < recs.size() && recs[i + 1].kind == REC_LIST) {
+            const Rec& l = recs[++i];
+            to.push(r.qr_json(l.from, false)); got++;
+            if (got < rc.x) { to.push(r.qr_json(l.to, false)); got++; }
+          }
+          J m = J::obj();
+          m.add("comparison", r.comparison(op, neg));
+          m.add("from", r.qr_json(rc.from, false));
+          m.add("to", std::move(to));
+          m.add("message", J::null());
+          m.add("custom_message", mk ? J::null() : r.custom_opt(pc(rc.clause)));
+          m.add("status", status_json(ST_FAIL));
+          leaf(mk ? std::string() : ctx_d(rc.clause), tagged("InComparison", std::move(m)));
+          break;
+        }
+        case REC_UNARY: {
+          const PClause& p = pc(rc.clause);
+          J v = J::obj();
+          v.add("from", r.qr_json(rc.from, true));
+          v.add("message", J::null());
+          v.add("custom_message", r.custom_opt(p));
+          v.add("status", status_json(ST_FAIL));
+          J u = J::obj();
+          u.add("value", std::move(v));
+          u.add("comparison", r.comparison(p.flags & 15u, (p.flags >> 4) & 1u));
+          leaf(ctx_d(rc.clause), tagged("Unary", std::move(u)));
+          break;
+        }
+        case REC_NOVALUE_EMPTY: leaf(ctx_d(rc.clause), tagged("NoValueForEmptyCheck", r.custom_opt(pc(rc.clause)))); break;
+        case REC_MISSING_BLOCK_VALUE: {
+          // eval.rs:1343-1358: message "Query <query> did not resolve to correct value, reason <reason>"
+          const PClause& p = pc(rc.clause);
+          J v = J::obj();
+          v.add("from", r.qr_json(rc.from, false));
+          v.add("message", J::str("Query " + slice_display(r.prog.queries[p.a], 0) + " did not resolve to correct value, reason " +
+                                  r.reason(rc.from)));
+          v.add("custom_message", J::null());
+          v.add("status", status_json(ST_FAIL));
+          leaf(r.prog.ctx[p.f], tagged("MissingBlockValue", std::move(v)));
+          break;
+        }
+        default: break;   // report-only records (rule / disjunction brackets) and REC_LIST (consumed above)
+      }
+    }
+    if (!stack.empty() || !have_root) throw Fatal{"IncompatibleError", "MI355X path: incomplete verbose event records"};
+  }
+};
+
+}  // namespace
+
+bool verbose_tree(const DocBatch& docs, uint32_t doc, const Program& prog, const TileResult& tile, const std::string& data_name,
+                  std::string& out, ReportError& err) {
+  try {
+    if (tile.out.err) { tile_error(docs, doc, prog, tile.out, err); return false; }
+    R r{docs, prog, docs.serde, docs.base[doc], &tile.aux};
+    VerboseBuilder b{r, data_name, {}, J(), false};
+    b.run(tile.recs);
+    pretty(b.root, 0, out);
+    return true;
+  } catch (Fatal& f) {
+    err.set = true; err.kind = f.kind; err.msg = f.msg;
+    return false;
+  }
 }
 
 bool report_document(const DocBatch& docs, uint32_t doc, const std::vector<const Program*>& progs,

@@ -43,6 +43,11 @@ struct ReportError { bool set = false; std::string kind, msg; };
 bool report_document(const DocBatch& docs, uint32_t doc, const std::vector<const Program*>& progs,
                      const std::vector<const TileResult*>& tiles, int indent, std::string& out, ReportError& err);
 
+// guard-ffi run_checks(verbose = true) (commands/helper.rs:62-64): the serde pretty EventRecord tree
+// (rules/mod.rs:165-355, eval_context.rs:990-997) from the verbose kernel's event records of one tile.
+bool verbose_tree(const DocBatch& docs, uint32_t doc, const Program& prog, const TileResult& tile, const std::string& data_name,
+                  std::string& out, ReportError& err);
+
 // error text for a tile error (Error Display, guard/src/rules/errors.rs:11-54)
 void tile_error(const DocBatch& docs, uint32_t doc, const Program& prog, const TileOut& t, ReportError& err);
 

@@ -201,7 +201,8 @@ def _b(s):
 
 
 def run_checks(data, data_name, rules, rules_name, verbose=False):
-    """guard-ffi run_checks: one document x one rules file -> pretty FileReport JSON."""
+    """guard-ffi run_checks: one document x one rules file -> pretty FileReport JSON (verbose: the
+    pretty EventRecord tree of the evaluation, commands/helper.rs:62-64)."""
     err = ExternError()
     p = lib().cfn_guard_run_checks(ValidateInput(_b(data), _b(data_name)), ValidateInput(_b(rules), _b(rules_name)),
                                    verbose, ctypes.byref(err))

@@ -2,7 +2,7 @@
  *
  * Drop-in for guard-ffi (reference: guard-ffi/src/lib.rs:32-47, guard-ffi/src/types.rs:4-8,
  * guard-ffi/example/cfn_guard.h): same struct layouts, same error codes
- * (guard-ffi/src/errors.rs:12-38), same JSON bytes for non-verbose calls.
+ * (guard-ffi/src/errors.rs:12-38), same JSON bytes.
  * All entry points evaluate on the GPU; without a HIP device they fail with code -1.
  * One device per process: the HIP device current on the thread of the first call (a multi-GPU
  * job sets it per rank, e.g. torch.cuda.set_device(LOCAL_RANK)), or GG_DEVICE=<ordinal>.
@@ -32,8 +32,8 @@ typedef struct {
 } validate_input_t;
 
 /* Replaces guard-ffi `cfn_guard_run_checks` (guard-ffi/src/lib.rs:32-45 -> run_checks,
- * guard/src/commands/helper.rs:25-87): one document x one rules file, pretty FileReport JSON.
- * verbose == true (EventRecord tree) is reported as unsupported (code -1). */
+ * guard/src/commands/helper.rs:25-87): one document x one rules file, pretty FileReport JSON;
+ * verbose == true: the pretty serde EventRecord tree of the evaluation (helper.rs:62-64). */
 char *cfn_guard_run_checks(validate_input_t data, validate_input_t rules, bool verbose, extern_err_t *err);
 
 /* Replaces guard-ffi `cfn_guard_free_string` (guard-ffi/src/lib.rs:47). NULL is a no-op. */

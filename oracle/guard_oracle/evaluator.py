@@ -1118,10 +1118,10 @@ def eval_guard_access_clause(gac, ctx):
             # operators in the reference (eval.rs:1146-1153)
             res = binary_operation(gac["query"]["query"], rhs, cmp, gac_display(gac), gac["custom_message"], ctx)
     except GuardError:
-        ctx.end_record(blk_context, ("GuardClauseBlockCheck", FAIL))
+        ctx.end_record(blk_context, ("GuardClauseBlockCheck", FAIL, not all_))
         raise
     if res[0] == "empty":
-        ctx.end_record(blk_context, ("GuardClauseBlockCheck", res[1]))
+        ctx.end_record(blk_context, ("GuardClauseBlockCheck", res[1], all_))
         return res[1]
     fails = sum(1 for _, s in res[1] if s == FAIL)
     passes = sum(1 for _, s in res[1] if s == PASS)
@@ -1129,7 +1129,7 @@ def eval_guard_access_clause(gac, ctx):
         outcome = FAIL if fails > 0 else PASS
     else:
         outcome = PASS if passes > 0 else FAIL
-    ctx.end_record(blk_context, ("GuardClauseBlockCheck", outcome))
+    ctx.end_record(blk_context, ("GuardClauseBlockCheck", outcome, not all_))
     return outcome
 
 
@@ -1166,11 +1166,11 @@ def eval_guard_block_clause(bc, ctx):
     try:
         values = ctx.query(bc["query"]["query"])
     except GuardError:
-        ctx.end_record(context, ("BlockGuardCheck", FAIL))
+        ctx.end_record(context, ("BlockGuardCheck", FAIL, not match_all))
         raise
     if not values:
         status = FAIL if bc["not_empty"] else SKIP
-        ctx.end_record(context, ("BlockGuardCheck", status))
+        ctx.end_record(context, ("BlockGuardCheck", status, not match_all))
         return status
     fails = passes = 0
     for each in values:
@@ -1179,13 +1179,16 @@ def eval_guard_block_clause(bc, ctx):
             ur = each[1]
             gctx = "GuardBlockAccessClause#%s" % file_location_display(bc["location"])
             ctx.start_record(gctx)
-            ctx.end_record(gctx, ("ClauseValueCheck", ("MissingBlockValue", {"from": each, "custom_message": None})))
+            ctx.end_record(gctx, ("ClauseValueCheck", ("MissingBlockValue", {
+                "from": each, "custom_message": None,
+                "message": "Query %s did not resolve to correct value, reason %s" % (
+                    slice_display(bc["query"]["query"]), ur.reason or "")})))
         else:
             vr = ValueScope(each[1], ctx)
             try:
                 st = eval_general_block_clause(bc["block"], vr, eval_guard_clause)
             except GuardError:
-                ctx.end_record(context, ("BlockGuardCheck", FAIL))
+                ctx.end_record(context, ("BlockGuardCheck", FAIL, not match_all))
                 raise
             if st == PASS:
                 passes += 1
@@ -1195,7 +1198,7 @@ def eval_guard_block_clause(bc, ctx):
         status = FAIL if fails > 0 else (PASS if passes > 0 else SKIP)
     else:
         status = PASS if passes > 0 else (FAIL if fails > 0 else SKIP)
-    ctx.end_record(context, ("BlockGuardCheck", status))
+    ctx.end_record(context, ("BlockGuardCheck", status, not match_all))
     return status
 
 
@@ -1275,25 +1278,25 @@ def eval_type_block_clause(tb, ctx):
             st = eval_conjunction_clauses(tb["conditions"], ctx, eval_when_clause)
         except GuardError:
             ctx.end_record(when_context, ("TypeCondition", FAIL))
-            ctx.end_record(context, ("TypeCheck", FAIL))
+            ctx.end_record(context, ("TypeCheck", FAIL, tb["type_name"]))
             raise
         if st != PASS:
             ctx.end_record(when_context, ("TypeCondition", st))
-            ctx.end_record(context, ("TypeCheck", SKIP))
+            ctx.end_record(context, ("TypeCheck", SKIP, tb["type_name"]))
             return SKIP
         ctx.end_record(when_context, ("TypeCondition", PASS))
     try:
         values = ctx.query(tb["query"])
     except GuardError:
-        ctx.end_record(context, ("TypeCheck", FAIL))
+        ctx.end_record(context, ("TypeCheck", FAIL, tb["type_name"]))
         raise
     if not values:
-        ctx.end_record(context, ("TypeCheck", SKIP))
+        ctx.end_record(context, ("TypeCheck", SKIP, tb["type_name"]))
         return SKIP
     fails = passes = 0
     for idx, each in enumerate(values):
         if each[0] == "U":
-            ctx.end_record(context, ("TypeCheck", FAIL))
+            ctx.end_record(context, ("TypeCheck", FAIL, tb["type_name"]))
             raise GuardError("MissingValue", "Unable to resolve type block query: %s" % tb["type_name"])
         block_context = "%s/%d" % (context, idx)
         ctx.start_record(block_context)
@@ -1302,7 +1305,7 @@ def eval_type_block_clause(tb, ctx):
             st = eval_general_block_clause(tb["block"], vr, eval_guard_clause)
         except GuardError:
             ctx.end_record(block_context, ("TypeBlock", FAIL))
-            ctx.end_record(context, ("TypeCheck", FAIL))
+            ctx.end_record(context, ("TypeCheck", FAIL, tb["type_name"]))
             raise
         if st == PASS:
             passes += 1
@@ -1310,7 +1313,7 @@ def eval_type_block_clause(tb, ctx):
             fails += 1
         ctx.end_record(block_context, ("TypeBlock", st))
     status = FAIL if fails > 0 else (PASS if passes > 0 else SKIP)
-    ctx.end_record(context, ("TypeCheck", status))
+    ctx.end_record(context, ("TypeCheck", status, tb["type_name"]))
     return status
 
 
@@ -1368,9 +1371,17 @@ def eval_rules_file(rf, ctx, data_file_name):
     return overall
 
 
+_DISJ_CONTEXT = {
+    "eval_guard_clause": "cfn_guard::rules::exprs::GuardClause#disjunction",
+    "eval_when_clause": "cfn_guard::rules::exprs::WhenGuardClause#disjunction",
+    "eval_rule_clause": "cfn_guard::rules::exprs::RuleClause#disjunction",
+}
+
+
 def eval_conjunction_clauses(conjunctions, ctx, eval_fn):
     num_passes = num_fails = 0
-    context = "disjunction"  # type_name-based context; never reported
+    # format!("{}#disjunction", std::any::type_name::<T>()) (eval.rs:1980): T from the clause evaluator
+    context = _DISJ_CONTEXT[eval_fn.__name__]
     for conjunction in conjunctions:
         disj_fails = 0
         multiple = len(conjunction) > 1

@@ -381,9 +381,78 @@ def validate_structured(rules, data, parsed_docs=None, output="json", raise_erro
     return out, exit_code, "".join(stderr)
 
 
-def run_checks(data_text, data_name, rules_text, rules_name):
-    """guard-ffi ``run_checks`` (commands/helper.rs:25-87), verbose = false.
-    Returns the pretty FileReport JSON or raises GuardError."""
+# ---------------------------------------------------------------------------
+# verbose EventRecord tree: serde's derived Serialize of EventRecord / RecordType
+# (rules/mod.rs:165-355; externally tagged enums, struct fields in declaration order)
+# ---------------------------------------------------------------------------
+_QR_TAG = {"R": "Resolved", "L": "Literal", "U": "UnResolved"}
+
+
+def _qr_json(q):
+    if q is None:
+        return None
+    k, v = q
+    return OMap([(_QR_TAG[k], _ur_json(v) if k == "U" else _pav_json(v))])
+
+
+def _block_check(alo, status):
+    return OMap([("at_least_one_matches", alo), ("status", status), ("message", None)])
+
+
+def _clause_check_json(cc):
+    k = cc[0]
+    if k == "Success":
+        return "Success"
+    m = cc[1]
+    if k == "Comparison":
+        return OMap([(k, OMap([("comparison", list(m["comparison"])), ("from", _qr_json(m["from"])),
+                               ("to", _qr_json(m["to"])), ("message", m["message"]),
+                               ("custom_message", m["custom_message"]), ("status", m["status"])]))])
+    if k == "InComparison":
+        return OMap([(k, OMap([("comparison", list(m["comparison"])), ("from", _qr_json(m["from"])),
+                               ("to", [_qr_json(t) for t in m["to"]]), ("message", m["message"]),
+                               ("custom_message", m["custom_message"]), ("status", m["status"])]))])
+    if k == "Unary":
+        return OMap([(k, OMap([("value", OMap([("from", _qr_json(m["from"])), ("message", m["message"]),
+                                                ("custom_message", m["custom_message"]), ("status", E.FAIL)])),
+                               ("comparison", list(m["comparison"]))]))])
+    if k == "NoValueForEmptyCheck":
+        return OMap([(k, m)])
+    if k == "DependentRule":
+        return OMap([(k, OMap([("rule", m["rule"]), ("message", None), ("custom_message", m["custom_message"]),
+                               ("status", E.FAIL)]))])
+    # MissingBlockValue(ValueCheck)
+    return OMap([(k, OMap([("from", _qr_json(m["from"])), ("message", m["message"]),
+                           ("custom_message", m["custom_message"]), ("status", E.FAIL)]))])
+
+
+def _container_json(c):
+    k = c[0]
+    if k in ("FileCheck", "RuleCheck"):
+        return OMap([(k, OMap([("name", c[1]), ("status", c[2]), ("message", c[3] if len(c) > 3 else None)]))])
+    if k in ("RuleCondition", "TypeCondition", "TypeBlock", "Filter", "WhenCondition"):
+        return OMap([(k, c[1])])
+    if k == "TypeCheck":
+        return OMap([(k, OMap([("type_name", c[2]), ("block", _block_check(False, c[1]))]))])
+    if k == "WhenCheck":
+        return OMap([(k, _block_check(False, c[1]))])
+    if k == "Disjunction":
+        return OMap([(k, _block_check(True, c[1]))])
+    if k in ("BlockGuardCheck", "GuardClauseBlockCheck"):
+        return OMap([(k, _block_check(c[2], c[1]))])
+    return OMap([(k, _clause_check_json(c[1]))])
+
+
+def event_json(ev):
+    """EventRecord {context, container, children} (eval_context.rs:990-997)"""
+    return OMap([("context", ev.context), ("container", _container_json(ev.container)),
+                 ("children", [event_json(ch) for ch in ev.children])])
+
+
+def run_checks(data_text, data_name, rules_text, rules_name, verbose=False):
+    """guard-ffi ``run_checks`` (commands/helper.rs:25-87).
+    Returns the pretty FileReport JSON (verbose: the pretty EventRecord tree of the evaluation,
+    helper.rs:62-64) or raises GuardError."""
     from .loader import load_serde_json
     try:
         doc = load_serde_json(data_text)
@@ -394,6 +463,10 @@ def run_checks(data_text, data_name, rules_text, rules_name):
     rf = parse_rules(rules_text, rules_name)
     if rf is None:
         return ""
+    if verbose:
+        root = E.RootScope(rf, doc)
+        E.eval_rules_file(rf, root, data_name)
+        return to_json_pretty(event_json(root.recorder.final_event))
     st, rep = eval_file_report(rf, doc, data_name)
     return to_json_pretty(OMap([
         ("name", rep["name"]), ("metadata", OMap([])), ("status", rep["status"]),
