@@ -681,7 +681,7 @@ void tile_error(const DocBatch& docs, uint32_t doc, const Program& prog, const T
                                   "join index out of bounds report", "unresolved join keys report", "map key filters (KEYS)",
                                   "functions other than count()", "clause kind"};
       err.kind = "Unsupported";
-      err.msg = std::string("unsupported on MI355X path: ") + (t.err_a < 9 ? why[t.err_a] : "construct");
+      err.msg = std::string("unsupported on MI355X path: ") + (t.err_a < 9 ? std::string(why[t.err_a]) : "construct #" + std::to_string(t.err_a) + "/" + std::to_string(t.err_b));
     }
   }
 }
