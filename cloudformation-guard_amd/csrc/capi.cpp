@@ -578,7 +578,9 @@ unsigned report_threads() {
 }
 
 // structured report over (docs x programs) in format `fmt` (OutFormat); false + err for an aborting error
-bool session_report(gg_session* s, std::string& out, int32_t& exit_code, ReportError& err, int32_t fmt = OUT_JSON) {
+// (cstr != null and JSON: the report goes to *cstr, a malloc'd buffer, without an intermediate string)
+bool session_report(gg_session* s, std::string& out, int32_t& exit_code, ReportError& err, int32_t fmt = OUT_JSON,
+                    char** cstr = nullptr) {
   exit_code = s->parse_errors.empty() ? 0 : 5;
   std::vector<const Program*> progs;
   for (auto& p : s->progs) progs.push_back(&p->prog);
@@ -596,7 +598,14 @@ bool session_report(gg_session* s, std::string& out, int32_t& exit_code, ReportE
   auto tile = [&](size_t d, size_t f) {
     return tile_view(s->tiles.data(), s->rule_status.data(), s->max_top, s->recs.data(), d * nf + f);
   };
-  if (!report_batch(s->docs, progs, 0, nd, tile, fmt, report_threads(), out, err)) { exit_code = -1; return false; }
+  if (fmt == OUT_JSON && cstr) {
+    std::vector<std::string> parts;
+    if (!report_batch_json_parts(s->docs, progs, 0, nd, tile, report_threads(), parts, err)) { exit_code = -1; return false; }
+    *cstr = json_parts_join(parts);
+  } else if (!report_batch(s->docs, progs, 0, nd, tile, fmt, report_threads(), out, err)) {
+    exit_code = -1;
+    return false;
+  }
   // exit code 19 when any rules file FAILed; a rules-file parse error set 5 beforehand
   // (structured.rs:40-43).  CommonStructuredReporter overwrites it with 19 (structured.rs:110-112);
   // JunitReporter::update_exit_code keeps 5 (reporters/mod.rs:97-103, validate/xml.rs:62-66).
@@ -787,15 +796,16 @@ char* cfn_guard_validate_batch_format(const validate_input_t* docs, size_t n_doc
     session_upload(&s);
     session_run(&s, true);
     std::string out;
+    char* cs = nullptr;
     int32_t code = 0;
     ReportError re;
-    if (!session_report(&s, out, code, re, output_format)) {
+    if (!session_report(&s, out, code, re, output_format, &cs)) {
       set_err(err, ffi_code(re.kind), error_display(re.kind, re.msg));
       if (exit_code) *exit_code = -1;
       return nullptr;
     }
     if (exit_code) *exit_code = code;
-    return dup_str(out);
+    return cs ? cs : dup_str(out);
   } catch (std::exception& e) {
     set_err(err, -1, e.what());
     if (exit_code) *exit_code = -1;
@@ -1047,19 +1057,28 @@ int64_t gg_session_report_bytes(gg_session* s, int32_t output_format, size_t max
     const size_t kBlock = getenv("GG_REPORT_BLOCK") ? (size_t)std::max(1, atoi(getenv("GG_REPORT_BLOCK"))) : 65536;
     int64_t bytes = 0;
     std::string out;
+    size_t json_parts = 0;   // JSON: the whole report is "[\n" + every block's parts joined by ",\n" + "\n]"
     for (size_t d0 = 0; d0 < nd; d0 += kBlock) {
       const size_t n = std::min(kBlock, nd - d0);
       ReportError re;
-      if (!report_batch(s->docs, progs, d0, n, tile, output_format, report_threads(), out, re)) {
+      bool ok;
+      if (output_format == OUT_JSON) {
+        std::vector<std::string> parts;
+        ok = report_batch_json_parts(s->docs, progs, d0, n, tile, report_threads(), parts, re);
+        for (auto& p : parts) bytes += (int64_t)p.size();
+        json_parts += parts.size();
+      } else {
+        ok = report_batch(s->docs, progs, d0, n, tile, output_format, report_threads(), out, re);
+        bytes += (int64_t)out.size();
+      }
+      if (!ok) {
         set_err(err, ffi_code(re.kind), error_display(re.kind, re.msg));
         if (exit_code) *exit_code = -1;
         return -1;
       }
-      // blocks join as the whole report would: JSON drops each block's brackets for ",\n"
-      bytes += (int64_t)out.size() - (output_format == OUT_JSON && nd > n ? 2 : 0);
       if (getenv("GG_PROGRESS")) fprintf(stderr, "[report] %zu / %zu documents, %lld bytes\n", d0 + n, nd, (long long)bytes);
     }
-    if (output_format == OUT_JSON && nd > kBlock) bytes += 2;
+    if (output_format == OUT_JSON) bytes += json_parts ? (int64_t)(4 + 2 * (json_parts - 1)) : 2;
     bool anyfail = false;
     for (auto& t : s->tiles) if (t.status == ST_FAIL) anyfail = true;
     if (exit_code) *exit_code = anyfail ? 19 : (s->parse_errors.empty() ? 0 : 5);
@@ -1377,20 +1396,57 @@ char* gg_session_report_format(gg_session* s, int32_t output_format, int32_t* ex
   if (!s->evaluated) { set_err(err, -1, "session not evaluated"); return nullptr; }
   if (output_format < OUT_JSON || output_format > OUT_JUNIT) { set_err(err, 18, "IllegalArguments: unknown output format"); return nullptr; }
   std::string out;
+  char* cs = nullptr;
   int32_t code = 0;
   ReportError re;
-  if (!session_report(s, out, code, re, output_format)) {
+  if (!session_report(s, out, code, re, output_format, &cs)) {
     if (exit_code) *exit_code = -1;
     set_err(err, ffi_code(re.kind), error_display(re.kind, re.msg));
     return nullptr;
   }
   if (exit_code) *exit_code = code;
-  return dup_str(out);
+  return cs ? cs : dup_str(out);
 }
 
 // statistics: 0 ndocs, 1 nfiles, 2 nodes, 3 string bytes, 4 tiles FAIL, 5 tiles PASS, 6 tiles SKIP,
 // 7 tiles with error, 8 records, 9 device arena bytes (nodes + strings + roots), 10 first error code,
 // 11 record bytes of the last fetch, 12 record capacity, 13 max top rules per file, 14 wave slots, 15 heap bytes/slot
+// Diagnostic: an evaluation's results (tile headers, rule statuses, records) to / from a file, so the
+// host report writer can be profiled and A/B'd on a CPU against results the GPU produced.  The
+// loading session must hold the same rules files and documents, added in the same order.
+int32_t gg_session_save_results(gg_session* s, const char* path, extern_err_t* err) {
+  set_err(err, 0, "");
+  if (!s->evaluated) { set_err(err, -1, "session not evaluated"); return -1; }
+  FILE* f = fopen(path, "wb");
+  if (!f) { set_err(err, -1, std::string("cannot write ") + path); return -1; }
+  const uint64_t h[4] = {0x47475245ull, s->tiles.size(), s->max_top, s->recs.size()};
+  bool ok = fwrite(h, sizeof(h), 1, f) == 1;
+  ok = ok && (s->tiles.empty() || fwrite(s->tiles.data(), sizeof(TileOut), s->tiles.size(), f) == s->tiles.size());
+  ok = ok && (s->rule_status.empty() || fwrite(s->rule_status.data(), 1, s->rule_status.size(), f) == s->rule_status.size());
+  ok = ok && (s->recs.empty() || fwrite(s->recs.data(), sizeof(Rec), s->recs.size(), f) == s->recs.size());
+  fclose(f);
+  if (!ok) { set_err(err, -1, "short write"); return -1; }
+  return 0;
+}
+
+int32_t gg_session_load_results(gg_session* s, const char* path, extern_err_t* err) {
+  set_err(err, 0, "");
+  FILE* f = fopen(path, "rb");
+  if (!f) { set_err(err, -1, std::string("cannot read ") + path); return -1; }
+  uint64_t h[4];
+  bool ok = fread(h, sizeof(h), 1, f) == 1 && h[0] == 0x47475245ull && h[1] == s->docs.ndocs() * s->progs.size();
+  if (ok) {
+    s->tiles.resize(h[1]); s->max_top = (uint32_t)h[2]; s->rule_status.resize(h[1] * h[2]); s->recs.resize(h[3]);
+    ok = (h[1] == 0 || fread(s->tiles.data(), sizeof(TileOut), h[1], f) == h[1]) &&
+         (s->rule_status.empty() || fread(s->rule_status.data(), 1, s->rule_status.size(), f) == s->rule_status.size()) &&
+         (h[3] == 0 || fread(s->recs.data(), sizeof(Rec), h[3], f) == h[3]);
+  }
+  fclose(f);
+  if (!ok) { set_err(err, -1, "results file does not match this session"); return -1; }
+  s->evaluated = true;
+  return 0;
+}
+
 int64_t gg_session_stat(gg_session* s, int32_t what) {
   switch (what) {
     case 0: return (int64_t)s->docs.ndocs();

@@ -1,6 +1,8 @@
 // Document loader (see doc_loader.h for the reference mapping).
 #include "doc_loader.h"
 
+#include <charconv>
+
 #include <yaml.h>
 
 #include <algorithm>
@@ -686,17 +688,24 @@ void DocBatch::adopt(uint32_t off, uint32_t n) {
 }
 
 std::string DocBatch::path(uint64_t base, uint32_t node) const {
-  std::vector<std::string> parts;
+  // JSON-pointer-like path (path_value.rs Path): the node's ancestors' keys / indices, root first
   const DNode* N = nodes.data() + base;
-  uint32_t cur = node;
-  while (N[cur].parent != NONE) {
-    uint32_t p = N[cur].parent;
-    if (N[p].kind == K_MAP) parts.push_back(bytes.substr(N[cur].key_off, N[cur].key_len));
-    else parts.push_back(std::to_string(cur - N[p].a));
-    cur = p;
+  uint32_t chain[64];
+  std::vector<uint32_t> deep;
+  size_t n = 0;
+  for (uint32_t cur = node; N[cur].parent != NONE; cur = N[cur].parent) {
+    if (n < 64) chain[n] = cur; else deep.push_back(cur);
+    n++;
   }
   std::string out;
-  for (size_t i = parts.size(); i-- > 0;) { out.push_back('/'); out += parts[i]; }
+  char num[16];
+  for (size_t i = n; i-- > 0;) {
+    const uint32_t cur = i < 64 ? chain[i] : deep[i - 64];
+    const DNode& p = N[N[cur].parent];
+    out.push_back('/');
+    if (p.kind == K_MAP) out.append(bytes.data() + N[cur].key_off, N[cur].key_len);
+    else { auto r = std::to_chars(num, num + sizeof num, cur - p.a); out.append(num, r.ptr - num); }
+  }
   return out;
 }
 

@@ -4,6 +4,9 @@
 //   * serde_json / ryu float output (ryu::Buffer::format_finite)
 //   * serde_json string escaping, Rust `{:?}` string escaping
 #pragma once
+#if defined(__SSE2__)
+#include <emmintrin.h>
+#endif
 #include <charconv>
 #include <cmath>
 #include <cstdint>
@@ -81,9 +84,25 @@ inline std::string ryu_f64(double x) {
 }
 
 inline void json_escape_into(std::string& out, const char* p, size_t n) {
+  // serde_json's escaping; plain runs are appended whole (found 16 bytes at a time)
   out.push_back('"');
-  for (size_t i = 0; i < n; i++) {
-    unsigned char c = (unsigned char)p[i];
+  size_t run = 0;
+  size_t i = 0;
+#if defined(__SSE2__)
+  const __m128i q = _mm_set1_epi8('"'), bs = _mm_set1_epi8('\\'), lim = _mm_set1_epi8(0x1F);
+  while (i + 16 <= n) {
+    const __m128i x = _mm_loadu_si128((const __m128i*)(p + i));
+    const __m128i ctl = _mm_cmpeq_epi8(_mm_max_epu8(x, lim), lim);   // bytes <= 0x1F
+    const __m128i m = _mm_or_si128(ctl, _mm_or_si128(_mm_cmpeq_epi8(x, q), _mm_cmpeq_epi8(x, bs)));
+    if (_mm_movemask_epi8(m)) break;   // the byte loop below takes this chunk
+    i += 16;
+  }
+#endif
+  for (; i < n; i++) {
+    const unsigned char c = (unsigned char)p[i];
+    if (c >= 0x20 && c != '"' && c != '\\') continue;
+    out.append(p + run, i - run);
+    run = i + 1;
     switch (c) {
       case '"': out += "\\\""; break;
       case '\\': out += "\\\\"; break;
@@ -92,11 +111,10 @@ inline void json_escape_into(std::string& out, const char* p, size_t n) {
       case '\t': out += "\\t"; break;
       case '\b': out += "\\b"; break;
       case '\f': out += "\\f"; break;
-      default:
-        if (c < 0x20) { char b[8]; snprintf(b, sizeof b, "\\u%04x", c); out += b; }
-        else out.push_back((char)c);
+      default: { char b[8]; snprintf(b, sizeof b, "\\u%04x", c); out += b; }
     }
   }
+  out.append(p + run, n - run);
   out.push_back('"');
 }
 

@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <set>
+#include <stdexcept>
 
 #include "host_format.h"
 
@@ -19,8 +20,14 @@ namespace gg {
 
 namespace {
 
+const char* const CMP_NAMES[] = {"Eq", "In", "Gt", "Lt", "Le", "Ge", "Exists", "Empty", "IsString", "IsList", "IsMap",
+                                 "IsBool", "IsInt", "IsFloat", "IsNull"};
+
 struct J {
-  enum T { Null, Bool, Raw, Str, Arr, Obj } t = Null;
+  // Cmp: the `comparison` pair [CmpOperator, not] (op in `op`, not in `b`), kept unboxed because
+  // every clause record carries one
+  enum T { Null, Bool, Raw, Str, Arr, Obj, Cmp } t = Null;
+  uint32_t op = 0;
   std::string s;
   bool b = false;
   std::vector<J> a;
@@ -32,6 +39,7 @@ struct J {
   static J boolean(bool v) { J j; j.t = Bool; j.b = v; return j; }
   static J arr() { J j; j.t = Arr; return j; }
   static J obj() { J j; j.t = Obj; return j; }
+  static J cmp(uint32_t op, bool neg) { J j; j.t = Cmp; j.op = op; j.b = neg; return j; }
   J& add(const std::string& k, J v) { o.push_back({k, std::move(v)}); return *this; }
   J& push(J v) { a.push_back(std::move(v)); return *this; }
 };
@@ -42,6 +50,15 @@ void pretty(const J& j, int indent, std::string& out) {
     case J::Bool: out += j.b ? "true" : "false"; return;
     case J::Raw: out += j.s; return;
     case J::Str: json_escape_into(out, j.s.data(), j.s.size()); return;
+    case J::Cmp:
+      out += "[\n";
+      out.append((indent + 1) * 2, ' ');
+      out += '"'; out += CMP_NAMES[j.op]; out += "\",\n";
+      out.append((indent + 1) * 2, ' ');
+      out += j.b ? "true\n" : "false\n";
+      out.append(indent * 2, ' ');
+      out += "]";
+      return;
     case J::Arr: {
       if (j.a.empty()) { out += "[]"; return; }
       out += "[\n";
@@ -169,29 +186,37 @@ struct R {
     }
   }
 
-  std::string value_only(uint32_t ref) const {
+  // ValueOnlyDisplay (display.rs:33-107), appended to `s`
+  void value_only_into(std::string& s, uint32_t ref) const {
     const DNode& n = N(ref);
     switch (n.kind) {
-      case K_NULL: return "\"NULL\"";
-      case K_STRING: return "\"" + str(ref) + "\"";
-      case K_REGEX: return "\"/" + str(ref) + "/\"";
-      case K_BOOL: return n.a ? "true" : "false";
-      case K_INT: return std::to_string(ival(n));
-      case K_FLOAT: return rust_display_f64(fval(n));
-      case K_CHAR: { std::string s = "'"; utf8_append(s, n.a); return s + "'"; }
-      case K_LIST: {
-        std::string s = "[";
-        for (uint32_t j = 0; j < n.count; j++) { if (j) s += ","; s += value_only(child(ref, j)); }
-        return s + "]";
-      }
-      case K_MAP: {
-        std::string s = "{";
-        for (uint32_t j = 0; j < n.count; j++) { if (j) s += ","; uint32_t c = child(ref, j); s += "\"" + key(c) + "\":" + value_only(c); }
-        return s + "}";
-      }
-      default: return range_str(n);
+      case K_NULL: s += "\"NULL\""; return;
+      case K_STRING: { const DocBatch& b = B(ref); s += '"'; s.append(b.bytes.data() + n.a, n.count); s += '"'; return; }
+      case K_REGEX: { const DocBatch& b = B(ref); s += "\"/"; s.append(b.bytes.data() + n.a, n.count); s += "/\""; return; }
+      case K_BOOL: s += n.a ? "true" : "false"; return;
+      case K_INT: s += std::to_string(ival(n)); return;
+      case K_FLOAT: s += rust_display_f64(fval(n)); return;
+      case K_CHAR: s += '\''; utf8_append(s, n.a); s += '\''; return;
+      case K_LIST:
+        s += '[';
+        for (uint32_t j = 0; j < n.count; j++) { if (j) s += ','; value_only_into(s, child(ref, j)); }
+        s += ']';
+        return;
+      case K_MAP:
+        s += '{';
+        for (uint32_t j = 0; j < n.count; j++) {
+          if (j) s += ',';
+          const uint32_t c = child(ref, j);
+          const DNode& cn = N(c);
+          s += '"'; s.append(B(c).bytes.data() + cn.key_off, cn.key_len); s += "\":";
+          value_only_into(s, c);
+        }
+        s += '}';
+        return;
+      default: s += range_str(n); return;
     }
   }
+  std::string value_only(uint32_t ref) const { std::string s; value_only_into(s, ref); return s; }
 
   std::string dbg_path(const std::string& p, uint32_t l, uint32_t c) const {
     return "Path(" + rust_debug_str(p) + ", Location { line: " + std::to_string(l) + ", col: " + std::to_string(c) + " })";
@@ -357,11 +382,7 @@ struct R {
     if (q.node == NONE) return {0, 0};
     return {(int64_t)line(q.node), (int64_t)col(q.node)};
   }
-  J comparison(uint32_t op, bool neg) const {
-    static const char* names[] = {"Eq", "In", "Gt", "Lt", "Le", "Ge", "Exists", "Empty", "IsString", "IsList", "IsMap",
-                                  "IsBool", "IsInt", "IsFloat", "IsNull"};
-    J a = J::arr(); a.push(J::str(names[op])); a.push(J::boolean(neg)); return a;
-  }
+  J comparison(uint32_t op, bool neg) const { return J::cmp(op, neg); }
   std::string custom(const PClause& pc) const { return pc.e == NONE ? "" : prog.msgs[pc.e]; }
   // NotComparable reason of a REC_CMP (rc.x != NC_NONE; operators.rs / path_value.rs compare_*)
   std::string nc_reason(const Rec& rc) const {
@@ -601,6 +622,293 @@ struct Walker {
   }
 };
 
+// ---- streaming JSON ------------------------------------------------------------------------------
+// The FileReport JSON written straight into the output, byte-identical to building the J tree and
+// pretty() printing it (serde_json's PrettyFormatter: 2-space indent, "[]" / "{}" when empty), without
+// the tree: no per-value allocations, one pass.  Used for the JSON format (validate batches and the
+// FFI's non-verbose run_checks); YAML / SARIF / JUnit still read the tree.
+struct JW {
+  std::string& out;
+  struct Level { int indent; bool first; };
+  std::vector<Level> st;
+  int base;
+  JW(std::string& o, int indent) : out(o), base(indent) {}
+  int cur() const { return st.empty() ? base : st.back().indent + 1; }
+  void open(char c) { out += c; st.push_back(Level{cur(), true}); }
+  void close(char c) {
+    const Level L = st.back();
+    st.pop_back();
+    if (!L.first) { out += '\n'; out.append(L.indent * 2, ' '); }
+    out += c;
+  }
+  void item() {   // element / member prefix inside the innermost container
+    Level& L = st.back();
+    out += L.first ? "\n" : ",\n";
+    L.first = false;
+    out.append((L.indent + 1) * 2, ' ');
+  }
+  void key(const char* k) { item(); out += '"'; out += k; out += "\": "; }
+  void key(const std::string& k) { item(); json_escape_into(out, k.data(), k.size()); out += ": "; }
+  void str(const std::string& v) { json_escape_into(out, v.data(), v.size()); }
+  void str(const char* v) { json_escape_into(out, v, strlen(v)); }
+  void raw(const std::string& v) { out += v; }
+  void null() { out += "null"; }
+  void boolean(bool b) { out += b ? "true" : "false"; }
+  void obj() { open('{'); }
+  void end_obj() { close('}'); }
+  void arr() { open('['); }
+  void end_arr() { close(']'); }
+  void cmp(uint32_t op, bool neg) {
+    arr();
+    item(); out += '"'; out += CMP_NAMES[op]; out += '"';
+    item(); boolean(neg);
+    end_arr();
+  }
+};
+
+// R::value_json / pav_json / unresolved_json, streamed
+void write_value(const R& r, JW& w, uint32_t ref) {
+  const DNode& n = r.N(ref);
+  switch (n.kind) {
+    case K_NULL: w.null(); return;
+    case K_STRING: { const DocBatch& B = r.B(ref); json_escape_into(w.out, B.bytes.data() + n.a, n.count); return; }
+    case K_REGEX: w.str("/" + r.str(ref) + "/"); return;
+    case K_BOOL: w.boolean(n.a != 0); return;
+    case K_INT: w.raw(std::to_string(r.ival(n))); return;
+    case K_FLOAT: {
+      double d = r.fval(n);
+      if (std::isnan(d) || std::isinf(d))
+        throw Fatal{"IncompatibleError", "Could not convert float " + rust_display_f64(d) + " to serde::Value::Number"};
+      w.raw(ryu_f64(d));
+      return;
+    }
+    case K_CHAR: { std::string s; utf8_append(s, n.a); w.str(s); return; }
+    case K_LIST:
+      w.arr();
+      for (uint32_t j = 0; j < n.count; j++) { w.item(); write_value(r, w, r.child(ref, j)); }
+      w.end_arr();
+      return;
+    case K_MAP:
+      w.obj();
+      for (uint32_t j = 0; j < n.count; j++) {
+        const uint32_t c = r.child(ref, j);
+        const DNode& cn = r.N(c);
+        const DocBatch& B = r.B(c);
+        w.item(); json_escape_into(w.out, B.bytes.data() + cn.key_off, cn.key_len); w.out += ": ";
+        write_value(r, w, c);
+      }
+      w.end_obj();
+      return;
+    default: w.str(r.range_str(n)); return;
+  }
+}
+void write_pav(const R& r, JW& w, const QR& q) {
+  w.obj();
+  w.key("path"); w.str(r.q_path(q));
+  w.key("value");
+  if (r.is_synth(q)) w.raw(std::to_string(r.synth_val(q)));
+  else write_value(r, w, q.node);
+  w.end_obj();
+}
+void write_unresolved(const R& r, JW& w, const QR& q) {
+  w.obj();
+  w.key("traversed_to");
+  w.obj();
+  w.key("path"); w.str(r.path(q.node));
+  w.key("value"); write_value(r, w, q.node);
+  w.end_obj();
+  w.key("remaining_query"); w.str(r.remaining(q));
+  w.key("reason"); w.str(r.reason(q));
+  w.end_obj();
+}
+void write_messages(JW& w, const std::string* custom, const std::string* error) {
+  w.obj();
+  w.key("custom_message"); if (custom) w.str(*custom); else w.null();
+  w.key("error_message"); if (error) w.str(*error); else w.null();
+  w.end_obj();
+}
+
+// Walker::items, streamed: writes the ClauseReports of records [i, close) into the open array
+struct StreamWalker {
+  const R& r;
+  const RecSpan& recs;
+  JW& w;
+  size_t i = 0;
+
+  void items(uint32_t close_kind) {
+    while (i < recs.size()) {
+      const Rec& rc = recs[i];
+      if (rc.kind == close_kind) { i++; return; }
+      i++;
+      switch (rc.kind) {
+        case REC_RULE_OPEN: {
+          w.item(); w.obj(); w.key("Rule"); w.obj();
+          w.key("name"); w.str(r.prog.rule_names[rc.clause]);
+          w.key("metadata"); w.obj(); w.end_obj();
+          w.key("messages"); write_messages(w, rc.x == NONE ? nullptr : &r.prog.msgs[rc.x], nullptr);
+          w.key("checks"); w.arr();
+          items(REC_RULE_CLOSE);
+          w.end_arr();
+          w.end_obj(); w.end_obj();
+          break;
+        }
+        case REC_DISJ_OPEN: {
+          w.item(); w.obj(); w.key("Disjunctions"); w.obj();
+          w.key("checks"); w.arr();
+          items(REC_DISJ_CLOSE);
+          w.end_arr();
+          w.end_obj(); w.end_obj();
+          break;
+        }
+        case REC_BLOCK_EMPTY: {
+          const PClause& pc = r.prog.clauses[rc.clause];
+          static const std::string msg = "query for block clause did not retrieve any value";
+          w.item(); w.obj(); w.key("Block"); w.obj();
+          w.key("context"); w.str(r.prog.ctx[pc.d]);
+          w.key("messages"); write_messages(w, nullptr, &msg);
+          w.key("unresolved"); w.null();
+          w.end_obj(); w.end_obj();
+          break;
+        }
+        case REC_MISSING_BLOCK_VALUE: {
+          const PClause& pc = r.prog.clauses[rc.clause];
+          const std::string err = "Check was not compliant as property [" + r.remaining(rc.from) + "] is missing. Value traversed to [" +
+                                  r.unresolved_display(rc.from) + "]";
+          static const std::string empty;
+          w.item(); w.obj(); w.key("Block"); w.obj();
+          w.key("context"); w.str(r.prog.ctx[pc.f]);
+          w.key("messages"); write_messages(w, &empty, &err);
+          w.key("unresolved"); write_unresolved(r, w, rc.from);
+          w.end_obj(); w.end_obj();
+          break;
+        }
+        case REC_UNARY: {
+          const PClause& pc = r.prog.clauses[rc.clause];
+          const uint32_t op = pc.flags & 15u;
+          const bool neg = (pc.flags >> 4) & 1u;
+          const bool unres = (rc.from.meta & 3u) == QR_UNRESOLVED;
+          const std::string msg = unres ? "Check was not compliant as property [" + r.remaining(rc.from) + "] is missing. Value traversed to [" +
+                                              r.unresolved_display(rc.from) + "]."
+                                        : "Check was not compliant as property [" + r.q_path_display(rc.from) + "] " + unary_msg(op, neg) + ".";
+          const std::string cm = r.custom(pc);
+          w.item(); w.obj(); w.key("Clause"); w.obj(); w.key("Unary"); w.obj();
+          w.key("check"); w.obj(); w.key(unres ? "UnResolved" : "Resolved"); w.obj();
+          w.key("value"); if (unres) write_unresolved(r, w, rc.from); else write_pav(r, w, rc.from);
+          w.key("comparison"); w.cmp(op, neg);
+          w.end_obj(); w.end_obj();
+          w.key("context"); w.str(r.prog.ctx[pc.d]);
+          w.key("messages"); write_messages(w, &cm, &msg);
+          w.end_obj(); w.end_obj(); w.end_obj();
+          break;
+        }
+        case REC_NOVALUE_EMPTY: {
+          const PClause& pc = r.prog.clauses[rc.clause];
+          const std::string& ctx = r.prog.ctx[pc.d];
+          std::string cm = r.custom(pc);
+          for (auto& ch : cm) if (ch == '\n') ch = ';';
+          const std::string msg = "Check was not compliant as variable in context [" + ctx + "] was not empty";
+          w.item(); w.obj(); w.key("Clause"); w.obj(); w.key("Unary"); w.obj();
+          w.key("check"); w.obj(); w.key("UnResolvedContext"); w.str(ctx); w.end_obj();
+          w.key("context"); w.str(ctx);
+          w.key("messages"); write_messages(w, &cm, &msg);
+          w.end_obj(); w.end_obj(); w.end_obj();
+          break;
+        }
+        case REC_DEPENDENT_RULE: {
+          const PClause& pc = r.prog.clauses[rc.clause];
+          const std::string& ctx = r.prog.ctx[pc.d];
+          const std::string& rule = r.prog.ctx[pc.f];
+          const std::string cm = r.custom(pc);
+          const std::string msg = "Check was not compliant as dependent rule [" + rule + "] did not PASS. Context [" + ctx + "]";
+          w.item(); w.obj(); w.key("Clause"); w.obj(); w.key("Unary"); w.obj();
+          w.key("check"); w.obj(); w.key("UnResolvedContext"); w.str(rule); w.end_obj();
+          w.key("context"); w.str(ctx);
+          w.key("messages"); write_messages(w, &cm, &msg);
+          w.end_obj(); w.end_obj(); w.end_obj();
+          break;
+        }
+        case REC_CMP: {
+          const bool mk = rc.clause == NONE;
+          const PClause* pcp = mk ? nullptr : &r.prog.clauses[rc.clause];
+          const uint32_t op = mk ? (rc.y & 15u) : (pcp->flags & 15u);
+          const bool neg = mk ? ((rc.y >> 4) & 1u) : ((pcp->flags >> 4) & 1u);
+          const bool from_unres = (rc.from.meta & 3u) == QR_UNRESOLVED;
+          if (!from_unres && rc.to.meta == 0xFFFFFFFFu) break;   // `to` absent: nothing reported (eval_context.rs:2283)
+          const std::string cust = mk ? std::string() : r.custom(*pcp);
+          const std::string errm = rc.x ? " Error = [" + r.nc_reason(rc) + "]" : std::string();
+          w.item(); w.obj(); w.key("Clause"); w.obj(); w.key("Binary"); w.obj();
+          w.key("context"); w.str(mk ? std::string() : r.prog.ctx[pcp->d]);
+          if (from_unres) {
+            const std::string msg = "Check was not compliant as property [" + r.remaining(rc.from) +
+                                    "] to compare from is missing. Value traversed to [" + r.unresolved_display(rc.from) + "]." + errm;
+            w.key("messages"); write_messages(w, &cust, &msg);
+            w.key("check"); w.obj(); w.key("UnResolved"); w.obj();
+            w.key("value"); write_unresolved(r, w, rc.from);
+            w.key("comparison"); w.cmp(op, neg);
+            w.end_obj(); w.end_obj();
+          } else if ((rc.to.meta & 3u) == QR_UNRESOLVED) {
+            const std::string msg = "Check was not compliant as property [" + r.remaining(rc.to) +
+                                    "] to compare to is missing. Value traversed to [" + r.unresolved_display(rc.to) + "]." + errm;
+            w.key("messages"); write_messages(w, &cust, &msg);
+            w.key("check"); w.obj(); w.key("UnResolved"); w.obj();
+            w.key("value"); write_unresolved(r, w, rc.to);
+            w.key("comparison"); w.cmp(op, neg);
+            w.end_obj(); w.end_obj();
+          } else {
+            const std::string msg = "Check was not compliant as property value [" + r.pav_display(rc.from) + "] " + op_msg(op, neg) +
+                                    " value [" + r.pav_display(rc.to) + "]." + errm;
+            w.key("messages"); write_messages(w, &cust, &msg);
+            w.key("check"); w.obj(); w.key("Resolved"); w.obj();
+            w.key("from"); write_pav(r, w, rc.from);
+            w.key("to"); write_pav(r, w, rc.to);
+            w.key("comparison"); w.cmp(op, neg);
+            w.end_obj(); w.end_obj();
+          }
+          w.end_obj(); w.end_obj(); w.end_obj();
+          break;
+        }
+        case REC_IN: {
+          const bool mk = rc.clause == NONE;
+          const PClause* pcp = mk ? nullptr : &r.prog.clauses[rc.clause];
+          const uint32_t op = mk ? (rc.y & 15u) : (pcp->flags & 15u);
+          const bool neg = mk ? ((rc.y >> 4) & 1u) : ((pcp->flags >> 4) & 1u);
+          std::vector<QR> to;
+          const uint32_t n = rc.x;
+          while (to.size() < n && i < recs.size() && recs[i].kind == REC_LIST) {
+            to.push_back(recs[i].from);
+            if (to.size() < n) to.push_back(recs[i].to);
+            i++;
+          }
+          std::string sd;
+          for (size_t k = 0; k < to.size(); k++) {
+            std::string item = (to[k].meta & 3u) == QR_UNRESOLVED ? "(unresolved, " + r.unresolved_display(to[k]) + ")"
+                                                                  : "(resolved, " + r.pav_display(to[k]) + ")";
+            sd = k ? sd + "." + item : item;
+          }
+          std::string fixed;
+          for (size_t k = 0; k < sd.size(); k++) { if (sd[k] == '.' && k + 1 < sd.size() && sd[k + 1] == '[') continue; fixed.push_back(sd[k]); }
+          const std::string err = "Check was not compliant as property [" + r.q_path_display(rc.from) + "] was not present in [" + fixed + "]";
+          const std::string* cm = (mk || pcp->e == NONE) ? nullptr : &r.prog.msgs[pcp->e];
+          w.item(); w.obj(); w.key("Clause"); w.obj(); w.key("Binary"); w.obj();
+          w.key("context"); w.str(mk ? std::string() : r.prog.ctx[pcp->d]);
+          w.key("messages"); write_messages(w, cm, &err);
+          w.key("check"); w.obj(); w.key("InResolved"); w.obj();
+          w.key("from"); write_pav(r, w, rc.from);
+          w.key("to"); w.arr();
+          for (auto& t : to) if ((t.meta & 3u) != QR_UNRESOLVED) { w.item(); write_pav(r, w, t); }
+          w.end_arr();
+          w.key("comparison"); w.cmp(op, neg);
+          w.end_obj(); w.end_obj();
+          w.end_obj(); w.end_obj(); w.end_obj();
+          break;
+        }
+        default:
+          break;
+      }
+    }
+  }
+};
+
 std::string status_str(uint32_t s) { return s == ST_PASS ? "PASS" : s == ST_FAIL ? "FAIL" : "SKIP"; }
 uint32_t status_and(uint32_t a, uint32_t b) {
   if (a == ST_FAIL) return ST_FAIL;
@@ -728,6 +1036,55 @@ bool build_file_report(const DocBatch& docs, uint32_t doc, const std::vector<con
   }
 }
 
+// build_file_report, streamed (JSON): the same object, written as it is walked
+bool write_file_report(const DocBatch& docs, uint32_t doc, const std::vector<const Program*>& progs,
+                       const std::vector<const TileResult*>& tiles, int indent, std::string& out, ReportError& err) {
+  const size_t mark = out.size();
+  try {
+    uint32_t status = ST_SKIP;
+    std::set<std::string> pass, skip;
+    for (size_t f = 0; f < progs.size(); f++) {
+      const Program& P = *progs[f];
+      const TileResult& T = *tiles[f];
+      if (T.out.err) continue;   // reported in file order below
+      status = status_and(status, T.out.status);
+      for (uint32_t k = 0; k < P.n_rules; k++) {
+        const std::string& nm = P.rule_names[P.rule_names.size() - P.n_rules + k];
+        if (T.rule_status[k] == ST_PASS) pass.insert(nm);
+        else if (T.rule_status[k] == ST_SKIP) skip.insert(nm);
+      }
+    }
+    JW w(out, indent);
+    w.obj();
+    w.key("name"); w.str(docs.names[doc]);
+    w.key("metadata"); w.obj(); w.end_obj();
+    w.key("status"); w.str(status_str(status));
+    w.key("not_compliant"); w.arr();
+    for (size_t f = 0; f < progs.size(); f++) {
+      const TileResult& T = *tiles[f];
+      // an earlier file's abort (a value serde cannot write) wins over this tile's error, as in
+      // build_file_report's file-order walk
+      if (T.out.err) { out.resize(mark); tile_error(docs, doc, *progs[f], T.out, err); return false; }
+      R r{docs, *progs[f], docs.serde, docs.base[doc], &T.aux};
+      StreamWalker sw{r, T.recs, w};
+      sw.items(0xFFFFFFFFu);
+    }
+    w.end_arr();
+    w.key("not_applicable"); w.arr();
+    for (auto& x : skip) { w.item(); w.str(x); }
+    w.end_arr();
+    w.key("compliant"); w.arr();
+    for (auto& x : pass) { w.item(); w.str(x); }
+    w.end_arr();
+    w.end_obj();
+    return true;
+  } catch (Fatal& f) {
+    out.resize(mark);
+    err.set = true; err.kind = f.kind; err.msg = f.msg;
+    return false;
+  }
+}
+
 const J* field(const J& o, const char* k) {
   for (auto& kv : o.o) if (kv.first == k) return &kv.second;
   return nullptr;
@@ -832,6 +1189,14 @@ struct YamlOut {
       case J::Bool: scalar(j.b ? "true" : "false", YAML_ANY_SCALAR_STYLE); return;
       case J::Raw: scalar(j.s, YAML_ANY_SCALAR_STYLE); return;
       case J::Str: str(j.s); return;
+      case J::Cmp:
+        yaml_sequence_start_event_initialize(&ev, nullptr, nullptr, 1, YAML_BLOCK_SEQUENCE_STYLE);
+        emit(ev);
+        str(CMP_NAMES[j.op]);
+        scalar(j.b ? "true" : "false", YAML_ANY_SCALAR_STYLE);
+        yaml_sequence_end_event_initialize(&ev);
+        emit(ev);
+        return;
       case J::Arr:
         yaml_sequence_start_event_initialize(&ev, nullptr, nullptr, 1, YAML_BLOCK_SEQUENCE_STYLE);
         emit(ev);
@@ -908,6 +1273,15 @@ ReportWriter::~ReportWriter() {
 
 bool ReportWriter::add(const DocBatch& docs, uint32_t doc, const std::vector<const Program*>& progs,
                        const std::vector<const TileResult*>& tiles, ReportError& err) {
+  if (p_->fmt == OUT_JSON) {
+    Impl& I = *p_;
+    const size_t mark = I.json.size();
+    I.json += I.ndocs == 0 ? "[\n" : ",\n";
+    I.json.append(2, ' ');
+    if (!write_file_report(docs, doc, progs, tiles, 1, I.json, err)) { I.json.resize(mark); return false; }
+    I.ndocs++;
+    return true;
+  }
   J fr;
   std::vector<J> per_file;
   if (!build_file_report(docs, doc, progs, tiles, fr, p_->fmt == OUT_JUNIT ? &per_file : nullptr, err)) return false;
@@ -1077,6 +1451,69 @@ bool report_batch(const DocBatch& docs, const std::vector<const Program*>& progs
   return true;
 }
 
+bool report_batch_json_parts(const DocBatch& docs, const std::vector<const Program*>& progs, size_t first, size_t ndocs,
+                             const std::function<TileResult(size_t doc, size_t file)>& tile, unsigned nthreads,
+                             std::vector<std::string>& parts, ReportError& err) {
+  const size_t nf = progs.size();
+  const size_t T = std::max<size_t>(1, std::min<size_t>(nthreads, (ndocs + 255) / 256));
+  parts.assign(T, std::string());
+  std::vector<ReportError> errs(T);
+  std::vector<size_t> err_doc(T, SIZE_MAX);
+  auto work = [&](size_t t) {
+    const size_t d0 = first + ndocs * t / T, d1 = first + ndocs * (t + 1) / T;
+    std::vector<TileResult> trs(nf);
+    std::vector<const TileResult*> tp(nf);
+    std::string& o = parts[t];
+    for (size_t d = d0; d < d1; d++) {
+      for (size_t f = 0; f < nf; f++) { trs[f] = tile(d, f); tp[f] = &trs[f]; }
+      if (d > d0) o += ",\n";
+      o.append(2, ' ');
+      if (!write_file_report(docs, (uint32_t)d, progs, tp, 1, o, errs[t])) { err_doc[t] = d; return; }
+      // size the part once from its first documents: growing it by doubling copies it again and
+      // again and faults its pages in twice
+      if (d == d0 + 7 && d1 - d0 > 16) o.reserve(o.size() / 8 * (d1 - d0) / 8 * 9);
+    }
+  };
+  std::vector<std::thread> th;
+  for (size_t t = 1; t < T; t++) th.emplace_back(work, t);
+  work(0);
+  for (auto& x : th) x.join();
+  for (size_t t = 0; t < T; t++) if (err_doc[t] != SIZE_MAX) { err = errs[t]; return false; }
+  std::vector<std::string> kept;
+  for (auto& p : parts) if (!p.empty()) kept.push_back(std::move(p));
+  parts.swap(kept);
+  return true;
+}
+
+size_t json_parts_size(const std::vector<std::string>& parts) {
+  if (parts.empty()) return 2;   // "[]"
+  size_t n = 4 + 2 * (parts.size() - 1);   // "[\n" ... "\n]", ",\n" between parts
+  for (auto& p : parts) n += p.size();
+  return n;
+}
+
+char* json_parts_join(const std::vector<std::string>& parts) {
+  const size_t n = json_parts_size(parts);
+  char* buf = (char*)malloc(n + 1);
+  if (!buf) throw std::bad_alloc();
+  if (parts.empty()) { memcpy(buf, "[]", 3); return buf; }
+  std::vector<size_t> off(parts.size());
+  size_t o = 2;
+  for (size_t k = 0; k < parts.size(); k++) { off[k] = o; o += parts[k].size() + 2; }
+  memcpy(buf, "[\n", 2);
+  // each part (and the separator after it) copied by its own thread: one pass over the output
+  auto copy = [&](size_t k) {
+    memcpy(buf + off[k], parts[k].data(), parts[k].size());
+    memcpy(buf + off[k] + parts[k].size(), k + 1 < parts.size() ? ",\n" : "\n]", 2);
+  };
+  std::vector<std::thread> th;
+  for (size_t k = 1; k < parts.size(); k++) th.emplace_back(copy, k);
+  copy(0);
+  for (auto& x : th) x.join();
+  buf[n] = 0;
+  return buf;
+}
+
 std::string ReportWriter::finish() {
   Impl& I = *p_;
   switch (I.fmt) {
@@ -1121,7 +1558,9 @@ std::string ReportWriter::finish() {
              std::to_string(I.tests) + "\" failures=\"" + std::to_string(I.failures) + "\" errors=\"0\" time=\"0\">\n" + I.suites +
              "</testsuites>\n";
     default:
-      return I.ndocs ? I.json + "\n]" : std::string("[]");
+      if (!I.ndocs) return std::string("[]");
+      I.json += "\n]";
+      return std::move(I.json);
   }
 }
 
@@ -1431,10 +1870,7 @@ bool verbose_tree(const DocBatch& docs, uint32_t doc, const Program& prog, const
 
 bool report_document(const DocBatch& docs, uint32_t doc, const std::vector<const Program*>& progs,
                      const std::vector<const TileResult*>& tiles, int indent, std::string& out, ReportError& err) {
-  J fr;
-  if (!build_file_report(docs, doc, progs, tiles, fr, nullptr, err)) return false;
-  pretty(fr, indent, out);
-  return true;
+  return write_file_report(docs, doc, progs, tiles, indent, out, err);
 }
 
 }  // namespace gg

@@ -104,4 +104,14 @@ bool report_batch(const DocBatch& docs, const std::vector<const Program*>& progs
                   const std::function<TileResult(size_t doc, size_t file)>& tile, int32_t fmt, unsigned nthreads,
                   std::string& out, ReportError& err);
 
+// JSON only, for large reports: the FileReports of documents [first, first + ndocs) rendered on
+// `nthreads` host threads into contiguous parts, not concatenated.  The report's text is
+// "[\n" + parts joined by ",\n" + "\n]" ("[]" with no parts): json_parts_size is its length,
+// json_parts_join a malloc'd NUL-terminated copy built in one parallel pass.
+bool report_batch_json_parts(const DocBatch& docs, const std::vector<const Program*>& progs, size_t first, size_t ndocs,
+                             const std::function<TileResult(size_t doc, size_t file)>& tile, unsigned nthreads,
+                             std::vector<std::string>& parts, ReportError& err);
+size_t json_parts_size(const std::vector<std::string>& parts);
+char* json_parts_join(const std::vector<std::string>& parts);
+
 }  // namespace gg

@@ -114,6 +114,9 @@ def lib():
     L.gg_session_report_bytes.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int32),
                                           ctypes.POINTER(ExternError)]
     L.gg_session_report_bytes.restype = ctypes.c_int64
+    for fn in (L.gg_session_save_results, L.gg_session_load_results):
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ExternError)]
+        fn.restype = ctypes.c_int32
     L.gg_program_stats.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint32)]
     L.gg_program_stats.restype = ctypes.c_int32
     _lib = L
@@ -332,6 +335,21 @@ class Session:
 
     def stat(self, what):
         return lib().gg_session_stat(self.s, what)
+
+    def save_results(self, path):
+        """diagnostic: the evaluation's tiles / rule statuses / records to a file"""
+        err = ExternError()
+        lib().gg_session_save_results(self.s, _b(path), ctypes.byref(err))
+        if err.code != 0:
+            _raise(err)
+
+    def load_results(self, path):
+        """diagnostic: results saved by save_results into a session with the same rules and documents
+        (renders reports without a GPU)"""
+        err = ExternError()
+        lib().gg_session_load_results(self.s, _b(path), ctypes.byref(err))
+        if err.code != 0:
+            _raise(err)
 
     def tile_status(self, n):
         buf = (ctypes.c_uint8 * n)()

@@ -76,6 +76,10 @@ int32_t gg_session_eval(gg_session *s, int32_t iters, double *ms_out, extern_err
 char *gg_session_report(gg_session *s, int32_t *exit_code, extern_err_t *err);
 char *gg_session_report_format(gg_session *s, int32_t output_format, int32_t *exit_code, extern_err_t *err);
 int64_t gg_session_stat(gg_session *s, int32_t what);
+/* Diagnostic: save an evaluation's results (tiles, rule statuses, records) / load them into a session
+ * holding the same rules files and documents (no GPU needed to render its reports). */
+int32_t gg_session_save_results(gg_session *s, const char *path, extern_err_t *err);
+int32_t gg_session_load_results(gg_session *s, const char *path, extern_err_t *err);
 int32_t gg_session_tile_status(gg_session *s, uint8_t *out, size_t n);
 double gg_session_last_kernel_ms(gg_session *s);
 int32_t gg_device_available(void);
