@@ -7,6 +7,7 @@
 #include "synth_corpus.h"
 
 #include <cstdio>
+#include <cstdlib>
 
 namespace gg {
 
@@ -172,11 +173,19 @@ void resource(XorShift32& r, int t, int i, Out& o) {
 
 void cfn_synth_doc(uint64_t index, int n_resources, std::string& s) {
   s.clear();
+  // Diagnostic corpus shapes (A/B of lane divergence only; never set by bench.py or the tests):
+  // GG_SYNTH_MOD=k generates doc (index % k); GG_SYNTH_SHAPE_GROUP=g gives the g consecutive docs
+  // of a group one resource-type sequence (their property values still differ).
+  static const uint64_t mod = getenv("GG_SYNTH_MOD") ? strtoull(getenv("GG_SYNTH_MOD"), nullptr, 10) : 0;
+  static const uint64_t grp = getenv("GG_SYNTH_SHAPE_GROUP") ? strtoull(getenv("GG_SYNTH_SHAPE_GROUP"), nullptr, 10) : 0;
+  if (mod) index %= mod;
   XorShift32 r((uint32_t)(42u ^ (uint32_t)index));
+  XorShift32 rt((uint32_t)(0x5eedu ^ (uint32_t)(grp ? index / grp : 0)));
   Out o{s};
   o.raw("{\"AWSTemplateFormatVersion\":\"2010-09-09\",\"Resources\":{");
   for (int k = 0; k < n_resources; k++) {
     int t = (int)(r.next() % 6u);
+    if (grp) t = (int)(rt.next() % 6u);
     if (k) o.raw(",");
     s += "\"Res" + std::to_string(k) + kShort[t] + "\":";
     resource(r, t, k, o);
