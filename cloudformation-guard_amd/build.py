@@ -37,8 +37,12 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", "-I" + YAML_INC, "-Wno-unused-result",
 # failure record) out of the interpreter loops into callee-saved VGPRs, which every call then saves
 # to scratch (99.7 -> 95.8 ms per launch, A/B'd on one box); -O2 instead of -O3 for the evaluator:
 # 96.2 -> 94.6 ms (round-1 A/B logs under profiles/r01_ab_*).
+# IPRA off: with interprocedural register allocation (this backend's default) the big leaves
+# (walk_run, compare_op) clobber callee-saved VGPRs freely and every recursive caller saves all of
+# them on entry, whether or not it touches them; without it the allocator keeps the leaves in
+# caller-saved registers (cfg-2 60.2 -> 58.5 ms with the query driver inlined, profiles/r02_ab_inline.log).
 SRC_FLAGS = {
-    "eval_kernel.hip": ["-mllvm", "-disable-machine-licm", "-O2"],
+    "eval_kernel.hip": ["-mllvm", "-disable-machine-licm", "-O2", "-mllvm", "-enable-ipra=false"],
 }
 
 
