@@ -599,7 +599,7 @@ bool session_report(gg_session* s, std::string& out, int32_t& exit_code, ReportE
     return tile_view(s->tiles.data(), s->rule_status.data(), s->max_top, s->recs.data(), d * nf + f);
   };
   if (fmt == OUT_JSON && cstr) {
-    std::vector<std::string> parts;
+    std::vector<TextBuf> parts;
     if (!report_batch_json_parts(s->docs, progs, 0, nd, tile, report_threads(), parts, err)) { exit_code = -1; return false; }
     *cstr = json_parts_join(parts);
   } else if (!report_batch(s->docs, progs, 0, nd, tile, fmt, report_threads(), out, err)) {
@@ -1063,7 +1063,7 @@ int64_t gg_session_report_bytes(gg_session* s, int32_t output_format, size_t max
       ReportError re;
       bool ok;
       if (output_format == OUT_JSON) {
-        std::vector<std::string> parts;
+        std::vector<TextBuf> parts;
         ok = report_batch_json_parts(s->docs, progs, d0, n, tile, report_threads(), parts, re);
         for (auto& p : parts) bytes += (int64_t)p.size();
         json_parts += parts.size();

@@ -83,7 +83,8 @@ inline std::string ryu_f64(double x) {
   return sign + s.d.substr(0, 1) + "." + s.d.substr(1) + "e" + std::to_string(kk - 1);
 }
 
-inline void json_escape_into(std::string& out, const char* p, size_t n) {
+template <class Out>
+inline void json_escape_into(Out& out, const char* p, size_t n) {
   // serde_json's escaping; plain runs are appended whole (found 16 bytes at a time)
   out.push_back('"');
   size_t run = 0;

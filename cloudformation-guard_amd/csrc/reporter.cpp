@@ -628,11 +628,11 @@ struct Walker {
 // the tree: no per-value allocations, one pass.  Used for the JSON format (validate batches and the
 // FFI's non-verbose run_checks); YAML / SARIF / JUnit still read the tree.
 struct JW {
-  std::string& out;
+  TextBuf& out;
   struct Level { int indent; bool first; };
   std::vector<Level> st;
   int base;
-  JW(std::string& o, int indent) : out(o), base(indent) {}
+  JW(TextBuf& o, int indent) : out(o), base(indent) {}
   int cur() const { return st.empty() ? base : st.back().indent + 1; }
   void open(char c) { out += c; st.push_back(Level{cur(), true}); }
   void close(char c) {
@@ -643,7 +643,7 @@ struct JW {
   }
   void item() {   // element / member prefix inside the innermost container
     Level& L = st.back();
-    out += L.first ? "\n" : ",\n";
+    if (L.first) out.push_back('\n'); else out.append(",\n", 2);
     L.first = false;
     out.append((L.indent + 1) * 2, ' ');
   }
@@ -1038,7 +1038,7 @@ bool build_file_report(const DocBatch& docs, uint32_t doc, const std::vector<con
 
 // build_file_report, streamed (JSON): the same object, written as it is walked
 bool write_file_report(const DocBatch& docs, uint32_t doc, const std::vector<const Program*>& progs,
-                       const std::vector<const TileResult*>& tiles, int indent, std::string& out, ReportError& err) {
+                       const std::vector<const TileResult*>& tiles, int indent, TextBuf& out, ReportError& err) {
   const size_t mark = out.size();
   try {
     uint32_t status = ST_SKIP;
@@ -1278,7 +1278,9 @@ bool ReportWriter::add(const DocBatch& docs, uint32_t doc, const std::vector<con
     const size_t mark = I.json.size();
     I.json += I.ndocs == 0 ? "[\n" : ",\n";
     I.json.append(2, ' ');
-    if (!write_file_report(docs, doc, progs, tiles, 1, I.json, err)) { I.json.resize(mark); return false; }
+    TextBuf t;
+    if (!write_file_report(docs, doc, progs, tiles, 1, t, err)) { I.json.resize(mark); return false; }
+    I.json.append(t.data(), t.size());
     I.ndocs++;
     return true;
   }
@@ -1453,17 +1455,18 @@ bool report_batch(const DocBatch& docs, const std::vector<const Program*>& progs
 
 bool report_batch_json_parts(const DocBatch& docs, const std::vector<const Program*>& progs, size_t first, size_t ndocs,
                              const std::function<TileResult(size_t doc, size_t file)>& tile, unsigned nthreads,
-                             std::vector<std::string>& parts, ReportError& err) {
+                             std::vector<TextBuf>& parts, ReportError& err) {
   const size_t nf = progs.size();
   const size_t T = std::max<size_t>(1, std::min<size_t>(nthreads, (ndocs + 255) / 256));
-  parts.assign(T, std::string());
+  parts.clear();
+  parts.resize(T);
   std::vector<ReportError> errs(T);
   std::vector<size_t> err_doc(T, SIZE_MAX);
   auto work = [&](size_t t) {
     const size_t d0 = first + ndocs * t / T, d1 = first + ndocs * (t + 1) / T;
     std::vector<TileResult> trs(nf);
     std::vector<const TileResult*> tp(nf);
-    std::string& o = parts[t];
+    TextBuf& o = parts[t];
     for (size_t d = d0; d < d1; d++) {
       for (size_t f = 0; f < nf; f++) { trs[f] = tile(d, f); tp[f] = &trs[f]; }
       if (d > d0) o += ",\n";
@@ -1479,20 +1482,20 @@ bool report_batch_json_parts(const DocBatch& docs, const std::vector<const Progr
   work(0);
   for (auto& x : th) x.join();
   for (size_t t = 0; t < T; t++) if (err_doc[t] != SIZE_MAX) { err = errs[t]; return false; }
-  std::vector<std::string> kept;
+  std::vector<TextBuf> kept;
   for (auto& p : parts) if (!p.empty()) kept.push_back(std::move(p));
   parts.swap(kept);
   return true;
 }
 
-size_t json_parts_size(const std::vector<std::string>& parts) {
+size_t json_parts_size(const std::vector<TextBuf>& parts) {
   if (parts.empty()) return 2;   // "[]"
   size_t n = 4 + 2 * (parts.size() - 1);   // "[\n" ... "\n]", ",\n" between parts
   for (auto& p : parts) n += p.size();
   return n;
 }
 
-char* json_parts_join(const std::vector<std::string>& parts) {
+char* json_parts_join(const std::vector<TextBuf>& parts) {
   const size_t n = json_parts_size(parts);
   char* buf = (char*)malloc(n + 1);
   if (!buf) throw std::bad_alloc();
@@ -1870,7 +1873,10 @@ bool verbose_tree(const DocBatch& docs, uint32_t doc, const Program& prog, const
 
 bool report_document(const DocBatch& docs, uint32_t doc, const std::vector<const Program*>& progs,
                      const std::vector<const TileResult*>& tiles, int indent, std::string& out, ReportError& err) {
-  return write_file_report(docs, doc, progs, tiles, indent, out, err);
+  TextBuf t;
+  if (!write_file_report(docs, doc, progs, tiles, indent, t, err)) return false;
+  out.append(t.data(), t.size());
+  return true;
 }
 
 }  // namespace gg

@@ -3,7 +3,11 @@
 // (guard/src/rules/eval_context.rs:1965-2435) and FileReport::combine (:1630-1640) over the
 // compact failure records emitted by the kernel.
 #pragma once
+#include <cstdlib>
+#include <cstdint>
+#include <cstring>
 #include <functional>
+#include <new>
 #include <string>
 #include <vector>
 
@@ -104,14 +108,77 @@ bool report_batch(const DocBatch& docs, const std::vector<const Program*>& progs
                   const std::function<TileResult(size_t doc, size_t file)>& tile, int32_t fmt, unsigned nthreads,
                   std::string& out, ReportError& err);
 
+// Growable text buffer for the streamed JSON writer: malloc / realloc storage (large blocks grow by
+// mremap, without a copy) and std::string's append interface, so fragment appends are an inline bounds
+// check and a memcpy instead of a std::string::append call each.
+struct TextBuf {
+  char* p = nullptr;
+  size_t n = 0, cap = 0;
+  TextBuf() = default;
+  TextBuf(const TextBuf&) = delete;
+  TextBuf& operator=(const TextBuf&) = delete;
+  TextBuf(TextBuf&& o) noexcept : p(o.p), n(o.n), cap(o.cap) { o.p = nullptr; o.n = o.cap = 0; }
+  TextBuf& operator=(TextBuf&& o) noexcept { std::swap(p, o.p); std::swap(n, o.n); std::swap(cap, o.cap); return *this; }
+  ~TextBuf() { free(p); }
+  void reserve(size_t k) {
+    if (k <= cap) return;
+    size_t nc = cap * 2 > k ? cap * 2 : k;
+    if (nc < 4096) nc = 4096;
+    char* q = (char*)realloc(p, nc);
+    if (!q) throw std::bad_alloc();
+    p = q; cap = nc;
+  }
+  // kSlack bytes past the end are always allocated, so short copies may store whole 8 / 16-byte
+  // words past the new end (they are overwritten by later appends or ignored)
+  static constexpr size_t kSlack = 64;
+  char* grow(size_t k) { if (n + k + kSlack > cap) reserve(n + k + kSlack); char* r = p + n; n += k; return r; }
+  void push_back(char c) { *grow(1) = c; }
+  void append(const char* s, size_t k) {
+    char* d = grow(k);
+    if (k >= 8 && k <= 16) {   // two overlapping words: no libc call for the writer's many short tokens
+      uint64_t a, b;
+      memcpy(&a, s, 8); memcpy(&b, s + k - 8, 8);
+      memcpy(d, &a, 8); memcpy(d + k - 8, &b, 8);
+    } else if (k >= 4 && k < 8) {
+      uint32_t a, b;
+      memcpy(&a, s, 4); memcpy(&b, s + k - 4, 4);
+      memcpy(d, &a, 4); memcpy(d + k - 4, &b, 4);
+    } else if (k < 4) {
+      for (size_t i = 0; i < k; i++) d[i] = s[i];
+    } else {
+      memcpy(d, s, k);
+    }
+  }
+  void append(size_t k, char c) {
+    char* d = grow(k);
+    if (c == ' ' && k <= 256) {   // indentation: 16-byte stores of spaces (may run into the slack)
+      static const char sp[16] = {' ', ' ', ' ', ' ', ' ', ' ', ' ', ' ', ' ', ' ', ' ', ' ', ' ', ' ', ' ', ' '};
+      for (size_t i = 0; i < k; i += 16) {
+        if (n - k + i + 16 > cap) { memset(d + i, ' ', k - i); break; }
+        memcpy(d + i, sp, 16);
+      }
+    } else if (k) {
+      memset(d, c, k);
+    }
+  }
+  TextBuf& operator+=(char c) { push_back(c); return *this; }
+  TextBuf& operator+=(const char* s) { append(s, strlen(s)); return *this; }
+  TextBuf& operator+=(const std::string& s) { append(s.data(), s.size()); return *this; }
+  size_t size() const { return n; }
+  bool empty() const { return n == 0; }
+  const char* data() const { return p; }
+  void resize(size_t m) { if (m <= n) n = m; else append(m - n, '\0'); }
+  void clear() { n = 0; }
+};
+
 // JSON only, for large reports: the FileReports of documents [first, first + ndocs) rendered on
 // `nthreads` host threads into contiguous parts, not concatenated.  The report's text is
 // "[\n" + parts joined by ",\n" + "\n]" ("[]" with no parts): json_parts_size is its length,
 // json_parts_join a malloc'd NUL-terminated copy built in one parallel pass.
 bool report_batch_json_parts(const DocBatch& docs, const std::vector<const Program*>& progs, size_t first, size_t ndocs,
                              const std::function<TileResult(size_t doc, size_t file)>& tile, unsigned nthreads,
-                             std::vector<std::string>& parts, ReportError& err);
-size_t json_parts_size(const std::vector<std::string>& parts);
-char* json_parts_join(const std::vector<std::string>& parts);
+                             std::vector<TextBuf>& parts, ReportError& err);
+size_t json_parts_size(const std::vector<TextBuf>& parts);
+char* json_parts_join(const std::vector<TextBuf>& parts);
 
 }  // namespace gg
