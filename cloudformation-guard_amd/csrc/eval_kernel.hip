@@ -209,10 +209,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
       if (n && off + n > A.rec_cap) { c.err = E_RECORDS; n = 0; }
       const uint32_t naux = n ? c.naux : 0, nrec = n - naux;
 #if GG_AB_NOREC != 1 && GG_AB_NOREC != 3   // diagnostic A/B only (2: staging off; 3: copy-out off)
-      for (uint32_t i = 0; i < nrec; i++) A.recs[off + i] = hload<Rec>(c, FRAMES_BYTES + i * (uint32_t)sizeof(Rec));
+      for (uint32_t i = 0; i < nrec; i++) A.recs[off + i] = rec_load(c, i);
 #endif
       for (uint32_t i = 0; i < naux; i++)
-        A.recs[off + nrec + i] = hload<Rec>(c, FRAMES_BYTES + RECS_BYTES - (i + 1) * (uint32_t)sizeof(Rec));
+        A.recs[off + nrec + i] = rec_load(c, RECS_BYTES / (uint32_t)sizeof(Rec) - 1 - i);
       TileOut o;
       o.status = status; o.err = c.err; o.err_a = c.err_a; o.err_b = c.err_b;
       o.rec_off = off; o.rec_n = nrec; o.pad0 = naux; o.pad1 = 0;
