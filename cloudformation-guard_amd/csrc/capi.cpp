@@ -376,6 +376,17 @@ void session_upload(gg_session* s) {
     s->dv->d_res_map.upload(rmap.data(), std::max<size_t>(nd, 1), st);
     s->dv->d_tix_off.upload(toff.data(), std::max<size_t>(nd, 1), st);
     s->dv->d_tix.alloc(std::max<size_t>(total, 1));
+    // the column is a property of the documents (the Type string id of each Resources entry), so it
+    // is built once per upload with the packed arena, not per evaluation
+    if (s->type_key != NONE && nd) {
+      DevBatch B{};
+      B.nodes = s->dv->d_nodes.p; B.klen = s->dv->d_klen.p; B.bytes = s->dv->d_bytes.p; B.roots = s->dv->d_roots.p;
+      B.base = s->dv->d_base.p; B.ndocs = (uint32_t)nd;
+      B.res_map = s->dv->d_res_map.p; B.tix_off = s->dv->d_tix_off.p; B.tix = s->dv->d_tix.p; B.type_key = s->type_key;
+      const uint32_t blocks = std::min<uint32_t>((B.ndocs + 3) / 4, g_dev.ncu * 16);
+      hipLaunchKernelGGL(resource_type_kernel, dim3(blocks), dim3(256), 0, st, B);
+      HIPCHK(hipGetLastError());
+    }
     HIPCHK(hipStreamSynchronize(st));   // the host vectors above die at the end of this scope
   }
   std::vector<DevProg> dps;
@@ -460,11 +471,6 @@ void session_launch(gg_session* s) {
   }
   s->ev0 = s->dv->evq[s->nq].first; s->ev1 = s->dv->evq[s->nq].second; s->nq++;
   HIPCHK(hipEventRecord(s->ev0, st));
-  if (s->type_key != NONE && A.docs.ndocs) {
-    uint32_t blocks = std::min<uint32_t>((A.docs.ndocs + 3) / 4, g_dev.ncu * 16);
-    hipLaunchKernelGGL(resource_type_kernel, dim3(blocks), dim3(256), 0, st, A.docs);
-    HIPCHK(hipGetLastError());
-  }
   if (s->mode != 1) {
     hipLaunchKernelGGL(guard_eval_lanes_kernel, dim3(s->lane_slots), dim3(64), A.lds_prog_words * 4, st, A);
     HIPCHK(hipGetLastError());

@@ -50,7 +50,7 @@ struct DevBatch {
   uint32_t ndocs;
   // CloudFormation resource-type column: for each document whose root has a `Resources` map,
   // tix[tix_off[d] + j] describes entry j of that map (TIX_* or the string id of its `Type`).
-  // Built per launch by resource_type_kernel; `Resources.*[ Type == '...' ]` filters read it
+  // Built once per upload by resource_type_kernel; `Resources.*[ Type == '...' ]` filters read it
   // instead of walking every resource's entries.
   const uint32_t* res_map;   // per doc: document-relative node of root.Resources (map), or NONE
   const uint32_t* tix_off;   // per doc: first column entry

@@ -243,7 +243,8 @@ namespace gg {
 
 // Resource-type column (DevBatch::tix): one wavefront per document, lanes over the entries of the
 // root's `Resources` map (coalesced reads of the contiguous entry block), each lane looking up its
-// resource's exact `Type` key.  Runs at the start of every evaluation launch.
+// resource's exact `Type` key.  Runs once per upload (capi.cpp session_upload): the column depends on
+// the documents only.
 __global__ void __launch_bounds__(256) resource_type_kernel(DevBatch D) {
   const uint32_t lane = __lane_id();
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) / 64u;
