@@ -3,7 +3,7 @@
 # rocprofv3 kernel-trace summary, and the cfg-2 PMC passes (HBM bytes + SQ + TCP/L2 latency counters).
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/final2
+O=$R/gpurun_out/${FINAL_TAG:-final2}
 mkdir -p $O
 cd $R
 echo "bench"
