@@ -22,6 +22,9 @@
 
 #define DEV __device__ __attribute__((always_inline)) inline
 #define DEVN __device__ __attribute__((noinline))
+#ifndef GG_STEAL
+#define GG_STEAL 1   // cross-XCD batch stealing at the end of a launch (profiles/r02_ab_inline.log)
+#endif
 
 namespace gg {
 namespace wv {
@@ -154,12 +157,27 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
   __syncthreads();
   uint32_t staged = NONE;
   const DevProg* P = nullptr;
+#if GG_STEAL
+  // a wave whose XCD queue is empty takes batches from the other XCDs' queues, in order, so the
+  // launch does not end with one XCD still working through its eighth
+  uint32_t qi = 0;
+#endif
   for (;;) {
     uint32_t b = 0;
+#if GG_STEAL
+    const uint32_t q = (xcd + qi) & 7u;
+    const uint32_t q0 = (uint32_t)(((uint64_t)nchunks * q) / 8u), q1 = (uint32_t)(((uint64_t)nchunks * (q + 1u)) / 8u);
+    if (lane == 0) b = atomicAdd(A.xcd_cursor + q, 1u);
+    b = __shfl(b, 0);
+    if (b >= (q1 - q0) * A.nfiles) { if (++qi == 8u) break; continue; }
+    const uint32_t file = b % A.nfiles, chunk = q0 + b / A.nfiles;
+    (void)nbatches; (void)c1;
+#else
     if (lane == 0) b = atomicAdd(A.xcd_cursor + xcd, 1u);
     b = __shfl(b, 0);
     if (b >= nbatches) break;
     const uint32_t file = b % A.nfiles, chunk = c0 + b / A.nfiles;
+#endif
     const uint32_t doc = chunk * 64u + lane;
     const bool active = doc < A.docs.ndocs;
     if (file != staged) { P = stage_program(&A.progs[file], &g_prog, s_blob, A.lds_prog_words); staged = file; }
