@@ -1261,10 +1261,19 @@ int32_t gg_session_add_synthetic(gg_session* s, uint64_t first, size_t n, int32_
     auto work = [&](int t) {
       size_t lo = n * t / nthreads, hi = n * (t + 1) / nthreads;
       std::string text;
+      DocBatch& B = parts[t];
       for (size_t i = lo; i < hi; i++) {
         cfn_synth_doc(first + i, n_resources, text);
-        if (!load_document(parts[t], text.data(), text.size(), "synthetic-" + std::to_string(first + i) + ".json",
+        if (!load_document(B, text.data(), text.size(), "synthetic-" + std::to_string(first + i) + ".json",
                            LOAD_LIBYAML, errs[t])) { failed[t] = 1; return; }
+        // size the part's columns once from its first documents (the generator's documents are
+        // alike) instead of growing them by doubling, which copies them again and again
+        if (i == lo + 7 && hi - lo > 16) {
+          const size_t est = B.nodes.size() / 8 * (hi - lo) / 16 * 17;
+          B.nodes.reserve(est); B.line.reserve(est); B.col.reserve(est); B.kline.reserve(est); B.kcol.reserve(est);
+          B.bytes.reserve(B.bytes.size() / 8 * (hi - lo) / 16 * 17);
+          B.base.reserve(hi - lo); B.roots.reserve(hi - lo); B.names.reserve(hi - lo);
+        }
       }
     };
     std::vector<std::thread> th;

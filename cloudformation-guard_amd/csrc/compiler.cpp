@@ -185,8 +185,7 @@ struct Compiler {
   uint32_t lit_grow(uint32_t n) {
     DocBatch& L = P.lit;
     uint32_t first = (uint32_t)L.nodes.size();
-    size_t s = L.nodes.size() + n;
-    L.nodes.resize(s); L.line.resize(s); L.col.resize(s); L.kline.resize(s); L.kcol.resize(s);
+    L.grow_zeroed(L.nodes.size() + n);
     return first;
   }
   uint32_t literal(const LitValue& v) {
@@ -504,8 +503,8 @@ struct Compiler {
   }
   uint32_t top_first = 0;
 
-  template <class T>
-  void put(std::vector<uint32_t>& blob, uint32_t& off, uint32_t& n, const std::vector<T>& v) {
+  template <class T, class A>
+  void put(std::vector<uint32_t>& blob, uint32_t& off, uint32_t& n, const std::vector<T, A>& v) {
     while (blob.size() & 3) blob.push_back(0);   // 16-byte aligned sections
     off = (uint32_t)blob.size();
     n = (uint32_t)v.size();

@@ -281,8 +281,7 @@ struct Emitter {
     }
   }
   void grow(uint32_t cnt) {
-    size_t s = b.nodes.size() + cnt;
-    b.nodes.resize(s); b.line.resize(s); b.col.resize(s); b.kline.resize(s); b.kcol.resize(s);
+    b.grow_zeroed(b.nodes.size() + cnt);
   }
 };
 

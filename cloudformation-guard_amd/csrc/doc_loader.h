@@ -8,18 +8,34 @@
 // The YAML event stream comes from libyaml 0.2.5 (the reference links unsafe-libyaml 0.2.11,
 // a transpile of the same C library).
 #pragma once
+#include <memory>
+#include <new>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "guard_types.h"
 
 namespace gg {
 
+// Allocator whose value-less construct() default-initialises: resize() of the arena columns (trivial
+// element types, every element written right after) skips the zero fill.  At 1M templates the
+// columns are ~29 GB, so zero-filling them before the copy doubled the loader's memory traffic.
+template <class T>
+struct default_init_allocator : std::allocator<T> {
+  template <class U> struct rebind { using other = default_init_allocator<U>; };
+  using std::allocator<T>::allocator;
+  template <class U> void construct(U* p) noexcept { ::new ((void*)p) U; }
+  template <class U, class... A> void construct(U* p, A&&... a) { ::new ((void*)p) U(std::forward<A>(a)...); }
+};
+template <class T>
+using column = std::vector<T, default_init_allocator<T>>;
+
 struct DocBatch {
-  std::vector<DNode> nodes;
+  column<DNode> nodes;
   std::string bytes;
-  std::vector<uint32_t> line, col;       // per node mark (PathAwareValue location)
-  std::vector<uint32_t> kline, kcol;     // per map-entry node: its key's mark
+  column<uint32_t> line, col;            // per node mark (PathAwareValue location)
+  column<uint32_t> kline, kcol;          // per map-entry node: its key's mark
   // Node indices inside a document are DOCUMENT-RELATIVE (child/parent fields, roots, records):
   // doc k's nodes are nodes[base[k] .. base[k+1]) and its root is nodes[base[k] + roots[k]].
   // The literal arena of a compiled rules file has no `base` (one implicit document at 0).
@@ -42,6 +58,13 @@ struct DocBatch {
   // indexes a string already in the pool at `off` (a pool built on the device, json_gpu.hip)
   void adopt(uint32_t off, uint32_t n);
 
+  // resizes every per-node column to s nodes, zero-filling new nodes (the columns default-initialise;
+  // loaders that do not write every field of a new node use this)
+  void grow_zeroed(size_t s) {
+    const size_t o = nodes.size();
+    nodes.resize(s); line.resize(s); col.resize(s); kline.resize(s); kcol.resize(s);
+    for (size_t i = o; i < s; i++) { nodes[i] = DNode{}; line[i] = col[i] = kline[i] = kcol[i] = 0; }
+  }
   size_t ndocs() const { return roots.size(); }
   std::string path(uint64_t base, uint32_t node) const;  // JSON pointer ("" for a root)
   std::string path_display(uint64_t base, uint32_t node) const;  // "{pointer}[L:{line},C:{col}]"
