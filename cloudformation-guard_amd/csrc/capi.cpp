@@ -215,6 +215,7 @@ struct DeviceBufs {
   DBuf<uint64_t> d_base;
   DBuf<uint32_t> d_res_map;     // per doc: root.Resources node (resource-type column, DevBatch)
   DBuf<uint32_t> d_tix_off;
+  DBuf<uint32_t> d_order;       // lane-mode document order (shape-sorted batches), empty = identity
   DBuf<uint32_t> d_tix;
   DBuf<DevProg> d_progs;
   DBuf<uint8_t> d_heaps;        // wave mode: one heap per wave slot
@@ -280,6 +281,7 @@ struct gg_session {
   // device residency: buffers borrowed from the device-state pool at upload (DeviceBufs)
   DeviceBufs* dv = nullptr;
   uint32_t type_key = NONE;
+  bool has_order = false;   // d_order holds a lane-mode document order (shape-sorted batches)
   size_t ncounts = 0;
   hipStream_t stream = nullptr;        // caller stream (e.g. torch's current stream); null = the buffers' own stream
   hipEvent_t ev0 = nullptr, ev1 = nullptr;   // brackets of the most recent launch (= dv->evq[nq - 1])
@@ -373,6 +375,52 @@ void session_upload(gg_session* s) {
       }
     }
     if (total > 0xFFFFFFF0u) { std::fill(rmap.begin(), rmap.end(), NONE); total = 0; }
+    // Shape-sorted batches: the lane kernel's 64 lanes run in lock-step, so a batch costs the union of
+    // its documents' paths.  Documents are ordered by their resource-type counts (the 8 most frequent
+    // Type strings of the batch, most frequent first) inside each XCD's eighth of the chunks -- every
+    // XCD keeps a representative share -- so a batch's documents have similar shapes (cfg-2: lane
+    // kernel 56.4 -> 49.9 ms, profiles/r02_ab_inline.log).  Results do not depend on the order: tiles
+    // stay indexed by document.  GG_SHAPE_SORT=0 keeps load order.
+    s->has_order = false;
+    const bool sort_on = !getenv("GG_SHAPE_SORT") || atoi(getenv("GG_SHAPE_SORT")) != 0;
+    if (sort_on && s->type_key != NONE && nd > 64) {
+      std::unordered_map<uint32_t, uint32_t> freq;
+      std::vector<std::vector<uint32_t>> types(nd);
+      for (size_t d = 0; d < nd; d++) {
+        if (rmap[d] == NONE) continue;
+        const DNode* N = D.nodes.data() + D.base[d];
+        const DNode& m = N[rmap[d]];
+        for (uint32_t j = 0; j < m.count; j++) {
+          const DNode& r = N[m.a + j];
+          if (r.kind != K_MAP) continue;
+          for (uint32_t k = 0; k < r.count; k++) {
+            const DNode& e = N[r.a + k];
+            if (e.key_hash == s->type_key && e.kind == K_STRING) { types[d].push_back(e.b); freq[e.b]++; break; }
+          }
+        }
+      }
+      std::vector<std::pair<uint32_t, uint32_t>> top(freq.begin(), freq.end());
+      std::sort(top.begin(), top.end(), [](auto& a, auto& b) { return a.second != b.second ? a.second > b.second : a.first < b.first; });
+      std::unordered_map<uint32_t, uint32_t> rank;
+      for (size_t i = 0; i < top.size() && i < 8; i++) rank[top[i].first] = (uint32_t)i;
+      std::vector<uint64_t> key(nd, 0);
+      for (size_t d = 0; d < nd; d++) {
+        uint32_t cnt[8] = {0};
+        for (uint32_t t : types[d]) { auto it = rank.find(t); if (it != rank.end()) cnt[it->second]++; }
+        uint64_t k = 0;
+        for (int i = 0; i < 8; i++) k = (k << 8) | std::min<uint32_t>(cnt[i], 255u);
+        key[d] = k;
+      }
+      std::vector<uint32_t> order(nd);
+      for (size_t d = 0; d < nd; d++) order[d] = (uint32_t)d;
+      const size_t nchunks = (nd + 63) / 64;
+      for (size_t x = 0; x < 8; x++) {
+        const size_t p0 = std::min(nd, (size_t)(nchunks * x / 8) * 64), p1 = std::min(nd, (size_t)(nchunks * (x + 1) / 8) * 64);
+        std::stable_sort(order.begin() + p0, order.begin() + p1, [&](uint32_t a, uint32_t b) { return key[a] < key[b]; });
+      }
+      s->dv->d_order.upload(order.data(), nd, st);
+      s->has_order = true;
+    }
     s->dv->d_res_map.upload(rmap.data(), std::max<size_t>(nd, 1), st);
     s->dv->d_tix_off.upload(toff.data(), std::max<size_t>(nd, 1), st);
     s->dv->d_tix.alloc(std::max<size_t>(total, 1));
@@ -448,6 +496,7 @@ void session_launch(gg_session* s) {
   LaunchArgs A{};
   A.docs.nodes = s->dv->d_nodes.p; A.docs.klen = s->dv->d_klen.p; A.docs.bytes = s->dv->d_bytes.p; A.docs.roots = s->dv->d_roots.p; A.docs.base = s->dv->d_base.p; A.docs.ndocs = (uint32_t)s->docs.ndocs();
   A.docs.res_map = s->dv->d_res_map.p; A.docs.tix_off = s->dv->d_tix_off.p; A.docs.tix = s->dv->d_tix.p; A.docs.type_key = s->type_key;
+  A.order = s->has_order ? s->dv->d_order.p : nullptr;
   A.progs = s->dv->d_progs.p; A.nfiles = (uint32_t)s->progs.size();
   A.ntiles = ntiles; A.tile_base = 0;
   A.heaps = s->dv->d_heaps.p; A.heap_bytes = s->heap_bytes; A.nslots = s->nslots;

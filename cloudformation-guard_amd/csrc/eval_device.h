@@ -60,6 +60,9 @@ struct DevBatch {
 
 struct LaunchArgs {
   DevBatch docs;
+  // lane-mode batch order: position p of the (chunk-major) document order evaluates document
+  // order[p]; null = identity.  Tiles stay indexed by document, so results do not depend on it.
+  const uint32_t* order;
   const DevProg* progs;    // per rules file
   uint32_t nfiles;
   uint32_t ntiles;         // ndocs * nfiles (tile = doc * nfiles + file)

@@ -178,8 +178,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
     if (b >= nbatches) break;
     const uint32_t file = b % A.nfiles, chunk = c0 + b / A.nfiles;
 #endif
-    const uint32_t doc = chunk * 64u + lane;
-    const bool active = doc < A.docs.ndocs;
+    const uint32_t pos = chunk * 64u + lane;
+    const bool active = pos < A.docs.ndocs;
+    const uint32_t doc = (A.order && active) ? A.order[pos] : pos;
     if (file != staged) { P = stage_program(&A.progs[file], &g_prog, s_blob, A.lds_prog_words); staged = file; }
     const uint32_t tile = doc * A.nfiles + file;
     uint32_t status = ST_SKIP, n = 0;
