@@ -34,6 +34,7 @@ __global__ void guard_eval_kernel(LaunchArgs A);
 __global__ void guard_eval_verbose_kernel(LaunchArgs A);
 __global__ void guard_eval_lanes_kernel(LaunchArgs A);
 __global__ void resource_type_kernel(DevBatch D);
+__global__ void shape_key_kernel(DevBatch D, const uint32_t* top8, unsigned long long* key);
 __global__ void pack_nodes_kernel(const DNode* in, DNodeP* out, uint32_t* klen, uint64_t n, uint32_t* bad);
 __global__ void rule_count_kernel(const TileOut* tiles, const uint8_t* rule_status, const DevProg* progs, uint32_t nfiles,
                                   uint32_t ntiles, uint32_t max_top, unsigned long long* counts);
@@ -375,52 +376,8 @@ void session_upload(gg_session* s) {
       }
     }
     if (total > 0xFFFFFFF0u) { std::fill(rmap.begin(), rmap.end(), NONE); total = 0; }
-    // Shape-sorted batches: the lane kernel's 64 lanes run in lock-step, so a batch costs the union of
-    // its documents' paths.  Documents are ordered by their resource-type counts (the 8 most frequent
-    // Type strings of the batch, most frequent first) inside each XCD's eighth of the chunks -- every
-    // XCD keeps a representative share -- so a batch's documents have similar shapes (cfg-2: lane
-    // kernel 56.4 -> 49.9 ms, profiles/r02_ab_inline.log).  Results do not depend on the order: tiles
-    // stay indexed by document.  GG_SHAPE_SORT=0 keeps load order.
     s->has_order = false;
-    const bool sort_on = !getenv("GG_SHAPE_SORT") || atoi(getenv("GG_SHAPE_SORT")) != 0;
-    if (sort_on && s->type_key != NONE && nd > 64) {
-      std::unordered_map<uint32_t, uint32_t> freq;
-      std::vector<std::vector<uint32_t>> types(nd);
-      for (size_t d = 0; d < nd; d++) {
-        if (rmap[d] == NONE) continue;
-        const DNode* N = D.nodes.data() + D.base[d];
-        const DNode& m = N[rmap[d]];
-        for (uint32_t j = 0; j < m.count; j++) {
-          const DNode& r = N[m.a + j];
-          if (r.kind != K_MAP) continue;
-          for (uint32_t k = 0; k < r.count; k++) {
-            const DNode& e = N[r.a + k];
-            if (e.key_hash == s->type_key && e.kind == K_STRING) { types[d].push_back(e.b); freq[e.b]++; break; }
-          }
-        }
-      }
-      std::vector<std::pair<uint32_t, uint32_t>> top(freq.begin(), freq.end());
-      std::sort(top.begin(), top.end(), [](auto& a, auto& b) { return a.second != b.second ? a.second > b.second : a.first < b.first; });
-      std::unordered_map<uint32_t, uint32_t> rank;
-      for (size_t i = 0; i < top.size() && i < 8; i++) rank[top[i].first] = (uint32_t)i;
-      std::vector<uint64_t> key(nd, 0);
-      for (size_t d = 0; d < nd; d++) {
-        uint32_t cnt[8] = {0};
-        for (uint32_t t : types[d]) { auto it = rank.find(t); if (it != rank.end()) cnt[it->second]++; }
-        uint64_t k = 0;
-        for (int i = 0; i < 8; i++) k = (k << 8) | std::min<uint32_t>(cnt[i], 255u);
-        key[d] = k;
-      }
-      std::vector<uint32_t> order(nd);
-      for (size_t d = 0; d < nd; d++) order[d] = (uint32_t)d;
-      const size_t nchunks = (nd + 63) / 64;
-      for (size_t x = 0; x < 8; x++) {
-        const size_t p0 = std::min(nd, (size_t)(nchunks * x / 8) * 64), p1 = std::min(nd, (size_t)(nchunks * (x + 1) / 8) * 64);
-        std::stable_sort(order.begin() + p0, order.begin() + p1, [&](uint32_t a, uint32_t b) { return key[a] < key[b]; });
-      }
-      s->dv->d_order.upload(order.data(), nd, st);
-      s->has_order = true;
-    }
+
     s->dv->d_res_map.upload(rmap.data(), std::max<size_t>(nd, 1), st);
     s->dv->d_tix_off.upload(toff.data(), std::max<size_t>(nd, 1), st);
     s->dv->d_tix.alloc(std::max<size_t>(total, 1));
@@ -434,6 +391,67 @@ void session_upload(gg_session* s) {
       const uint32_t blocks = std::min<uint32_t>((B.ndocs + 3) / 4, g_dev.ncu * 16);
       hipLaunchKernelGGL(resource_type_kernel, dim3(blocks), dim3(256), 0, st, B);
       HIPCHK(hipGetLastError());
+      // Shape-sorted batches: the lane kernel's 64 lanes run in lock-step, so a batch costs the union
+      // of its documents' paths.  Documents are ordered by their counts of the 8 most frequent Type
+      // strings (taken from the first documents; most frequent first) inside each XCD's eighth of the
+      // chunks -- every XCD keeps a representative share -- so a batch's documents have similar shapes
+      // (cfg-2: lane kernel 56.4 -> 49.9 ms, profiles/r02_ab_inline.log).  Results do not depend on the
+      // order: tiles stay indexed by document.  GG_SHAPE_SORT=0 keeps load order.
+      const bool sort_on = !getenv("GG_SHAPE_SORT") || atoi(getenv("GG_SHAPE_SORT")) != 0;
+      if (sort_on && nd > 64) {
+        std::unordered_map<uint32_t, uint32_t> freq, tlen;
+        for (size_t d = 0; d < std::min<size_t>(nd, 4096); d++) {
+          if (rmap[d] == NONE) continue;
+          const DNode* N = D.nodes.data() + D.base[d];
+          const DNode& m = N[rmap[d]];
+          for (uint32_t j = 0; j < m.count; j++) {
+            const DNode& r = N[m.a + j];
+            if (r.kind != K_MAP) continue;
+            for (uint32_t k = 0; k < r.count; k++) {
+              const DNode& e = N[r.a + k];
+              if (e.key_hash == s->type_key && e.kind == K_STRING) { freq[e.b]++; tlen[e.b] = e.count; break; }
+            }
+          }
+        }
+        // rank: types the rules files name (as a literal) first -- by how many files name them --
+        // then by frequency, so the primary sort key aligns the most-checked resource type
+        std::vector<std::pair<uint32_t, uint32_t>> top(freq.begin(), freq.end());
+        std::unordered_map<uint32_t, uint32_t> named;
+        for (auto& tp : top) {
+          const std::string tstr(D.bytes.data() + tp.first, tlen[tp.first]);
+          uint32_t nf = 0;
+          for (auto& gp : s->progs) if (!tstr.empty() && gp->prog.lit.bytes.find(tstr) != std::string::npos) nf++;
+          named[tp.first] = nf;
+        }
+        std::sort(top.begin(), top.end(), [&](auto& a, auto& b) {
+          if (named[a.first] != named[b.first]) return named[a.first] > named[b.first];
+          return a.second != b.second ? a.second > b.second : a.first < b.first;
+        });
+        uint32_t top8[8];
+        for (int i = 0; i < 8; i++) top8[i] = i < (int)top.size() ? top[i].first : TIX_UNDECIDED;
+        DBuf<uint32_t> d_top;
+        d_top.upload(top8, 8, st);
+        DBuf<unsigned long long> d_key;
+        d_key.alloc(nd);
+        hipLaunchKernelGGL(shape_key_kernel, dim3(std::min<uint32_t>((uint32_t)((nd + 255) / 256), g_dev.ncu * 16)), dim3(256), 0, st,
+                           B, (const uint32_t*)d_top.p, d_key.p);
+        HIPCHK(hipGetLastError());
+        std::vector<unsigned long long> key(nd);
+        HIPCHK(hipMemcpyAsync(key.data(), d_key.p, nd * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        std::vector<uint32_t> order(nd);
+        for (size_t d = 0; d < nd; d++) order[d] = (uint32_t)d;
+        const size_t nchunks = (nd + 63) / 64;
+        std::vector<std::thread> th;
+        for (size_t x = 0; x < 8; x++)
+          th.emplace_back([&, x]() {
+            const size_t p0 = std::min(nd, (size_t)(nchunks * x / 8) * 64), p1 = std::min(nd, (size_t)(nchunks * (x + 1) / 8) * 64);
+            std::stable_sort(order.begin() + p0, order.begin() + p1, [&](uint32_t a, uint32_t b) { return key[a] < key[b]; });
+          });
+        for (auto& t : th) t.join();
+        s->dv->d_order.upload(order.data(), nd, st);
+        s->has_order = true;
+      }
     }
     HIPCHK(hipStreamSynchronize(st));   // the host vectors above die at the end of this scope
   }

@@ -291,6 +291,31 @@ __global__ void __launch_bounds__(256) resource_type_kernel(DevBatch D) {
   }
 }
 
+// Shape key per document for the lane kernel's batch order (capi.cpp session_upload): its counts of
+// the batch's 8 most frequent Type strings, 8 bits each, most frequent first; from the type column.
+__global__ void __launch_bounds__(256) shape_key_kernel(DevBatch D, const uint32_t* top8, unsigned long long* key) {
+  uint32_t t[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) t[i] = top8[i];
+  for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < D.ndocs; d += gridDim.x * blockDim.x) {
+    uint32_t cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const uint32_t rm = D.res_map[d];
+    if (rm != NONE) {
+      const uint32_t n = D.nodes[D.base[d] + rm].kc >> 4;
+      const uint32_t* col = D.tix + D.tix_off[d];
+      for (uint32_t j = 0; j < n; j++) {
+        const uint32_t v = col[j];
+#pragma unroll
+        for (int i = 0; i < 8; i++) cnt[i] += v == t[i] ? 1u : 0u;
+      }
+    }
+    unsigned long long k = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) k = (k << 8) | (cnt[i] < 255u ? cnt[i] : 255u);
+    key[d] = k;
+  }
+}
+
 // Per-(rules file, top rule) PASS/FAIL/SKIP tallies over every tile of one evaluation, plus a
 // per-file line (index max_top) holding file statuses and errored tiles (status slot 3).
 // counts[((file * (max_top + 1) + rule) * 4) + status]; the same buffer is what the multi-GPU
