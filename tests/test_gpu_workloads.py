@@ -178,3 +178,30 @@ def test_cfg3_lane_matches_wave():
     docs = synth.cfn_corpus(130, start=9000, n_resources=50)
     rules = _pack("cfg3_rulepack")
     assert _session_report(docs, rules, 0, "t") == _session_report(docs, rules, 1, "t")
+
+
+def test_shape_sorted_batch_matches_load_order():
+    """Shape-sorted lane batches (capi.cpp session_upload) change only which documents share a
+    wavefront: a 640-document cfg-2 batch reports byte-identically with the sort on and off, in every
+    format, and equals the oracle on its first documents."""
+    import rulepack
+    docs = synth.cfn_corpus(640, start=9000, n_resources=50)
+    rules = rulepack.rule_pack("cfg2")
+    outs = {}
+    try:
+        for flag in ("1", "0"):
+            os.environ["GG_SHAPE_SORT"] = flag
+            s = guard_amd.Session()
+            for name, text in rules:
+                s.add_rules(text, name)
+            s.add_docs(docs, ["s-%d.json" % i for i in range(len(docs))])
+            s.eval(1)
+            outs[flag] = [s.report(fmt) for fmt in ("json", "yaml", "sarif", "junit")]
+            s.close()
+    finally:
+        os.environ.pop("GG_SHAPE_SORT", None)
+    assert outs["1"] == outs["0"]
+    data = [("s-%d.json" % i, d) for i, d in enumerate(docs[:40])]
+    exp, ecode, _ = oracle_validate(rules, data)
+    out, code = guard_amd.validate_structured(rules, data)
+    assert (code, out) == (ecode, exp)
