@@ -311,7 +311,12 @@ struct gg_session {
   bool evaluated = false;
   double last_kernel_ms = 0;
   std::string last_error;
-  ~gg_session() { release_bufs(dv); }
+  ~gg_session() {
+    // work enqueued on a caller stream (gg_session_set_stream) may still read or write these buffers:
+    // drain it before the set goes back to the pool, where the next session's uploads reuse it
+    if (dv && stream) hipStreamSynchronize(stream);
+    release_bufs(dv);
+  }
 };
 
 namespace {
@@ -742,10 +747,7 @@ void merge_batches(DocBatch& dst, std::vector<DocBatch>& parts) {
       dst.base[rbase[t] + r] = src.base[r] + nb;
     }
   };
-  std::vector<std::thread> th;
-  for (size_t t = 1; t < np; t++) th.emplace_back(work, t);
-  if (np) work(0);
-  for (auto& x : th) x.join();
+  parallel_run(np, work);
   for (auto& p : parts) {
     dst.names.insert(dst.names.end(), std::make_move_iterator(p.names.begin()), std::make_move_iterator(p.names.end()));
     p = DocBatch();
@@ -958,8 +960,9 @@ char* cfn_guard_test(validate_input_t rules, const validate_input_t* specs, size
     std::string perr;
     const char* rtext = rules.content ? rules.content : "";
     if (!add_rules(&s, rtext, rname, perr)) {
-      // test.rs:300-303 (text) and 345-350 (structured TestResult::Err): a report, exit code 1
-      if (exit_code) *exit_code = 1;
+      // test.rs:300-303 (text): exit code 1; 338-350 (structured TestResult::Err): the report, and
+      // handle_structured_single_report's exit_code stays SUCCESS_STATUS_CODE on that branch
+      if (exit_code) *exit_code = output_format == OUT_TEXT ? 1 : 0;
       if (output_format == OUT_TEXT) return dup_str("Parse Error on ruleset file " + error_display("ParseError", perr) + "\n");
       std::vector<TestSpecFile> ef(1);
       ef[0].error = error_display("ParseError", perr);
@@ -1082,6 +1085,10 @@ int32_t gg_session_launch(gg_session* s, extern_err_t* err) {
     std::string why;
     if (!ensure_device(why)) { set_err(err, -1, why); return -1; }
     if (!s->uploaded) session_upload(s);
+    // launch / fetch callers (multi-GPU: launch, all-reduce the tallies, fetch) get no second launch,
+    // so the large-heap pass must exist from the first one: a tile that outgrows the wave heap is then
+    // evaluated, not left with E_HEAP (session_run allocates it lazily and re-launches instead)
+    if (!s->dv->d_big_heaps.p) s->dv->d_big_heaps.alloc((size_t)gg_session::kBigSlots * gg_session::kBigHeap);
     session_launch(s);
     return 0;
   } catch (std::exception& e) { set_err(err, -1, e.what()); return -1; }
@@ -1198,9 +1205,9 @@ int32_t gg_session_add_docs(gg_session* s, const char* const* texts, const size_
       if (!load_document(parts[t], texts[i], lens[i], names ? names[i] : std::string(), (LoadMode)mode, errs[t])) { failed[t] = (int)i; return; }
     }
   };
-  std::vector<std::thread> th;
-  for (int t = 0; t < nthreads; t++) th.emplace_back(work, t);
-  for (auto& x : th) x.join();
+  try {
+    parallel_run((size_t)nthreads, work);
+  } catch (std::exception& e) { set_err(err, -1, e.what()); return -1; }
   for (int t = 0; t < nthreads; t++) {
     if (failed[t] >= 0) { set_err(err, ffi_code(errs[t].kind), error_display(errs[t].kind, errs[t].msg)); return 5; }
   }
@@ -1242,6 +1249,18 @@ static void dump_node(const DocBatch& D, uint64_t base, uint32_t i, std::string&
         dump_node(D, base, n.a + j, o);
       }
       o += "}";
+      if (n.b) {
+        // MapValue.keys of a map with a repeated key: every occurrence with its mark
+        const uint32_t nk = D.nodes[base + n.b].count;
+        o += " keys [";
+        for (uint32_t j = 0; j < nk; j++) {
+          const uint64_t g = base + n.b + j;
+          if (j) o += ", ";
+          o += rust_debug_str(str(D.nodes[g].key_off, D.nodes[g].key_len)) + "@" + std::to_string(D.kline[g]) + ":" +
+               std::to_string(D.kcol[g]);
+        }
+        o += "]";
+      }
       break;
     default: o += "?"; break;
   }
@@ -1343,9 +1362,7 @@ int32_t gg_session_add_synthetic(gg_session* s, uint64_t first, size_t n, int32_
         }
       }
     };
-    std::vector<std::thread> th;
-    for (int t = 0; t < nthreads; t++) th.emplace_back(work, t);
-    for (auto& x : th) x.join();
+    parallel_run((size_t)nthreads, work);
     for (int t = 0; t < nthreads; t++)
       if (failed[t]) { set_err(err, ffi_code(errs[t].kind), error_display(errs[t].kind, errs[t].msg)); return 5; }
     merge_batches(s->docs, parts);
@@ -1393,9 +1410,7 @@ int32_t gg_session_add_synthetic_device(gg_session* s, uint64_t first, size_t n,
         names[i] = "synthetic-" + std::to_string(first + i) + ".json";
       }
     };
-    std::vector<std::thread> th;
-    for (int t = 0; t < nthreads; t++) th.emplace_back(work, t);
-    for (auto& x : th) x.join();
+    parallel_run((size_t)nthreads, work);
     std::vector<const char*> p(n), nm(n);
     std::vector<size_t> l(n);
     for (size_t i = 0; i < n; i++) { p[i] = texts[i].data(); l[i] = texts[i].size(); nm[i] = names[i].c_str(); }

@@ -265,6 +265,30 @@ struct Emitter {
         grow(cnt);
         DNode& dd = b.nodes[slot];
         dd.a = (uint32_t)(first - base); dd.count = cnt;
+        const uint32_t nall = (uint32_t)t.n[ti].keys.size();
+        if (!serde && nall > cnt) {
+          // a repeated key (libyaml loader: the IndexMap is keyed by (key, mark), loader.rs:172-185):
+          // MapValue.keys keeps every occurrence while MapValue.values keeps one entry per key
+          // (path_value.rs:453-470).  The keys list goes to a block of nall key slots -- key id,
+          // length and mark of each occurrence in document order, parent = the map, kind K_NULL,
+          // count = nall -- referenced by the map node's `b` (0 = no repeated key; index 0 is the
+          // root, never such a block).  `*` captures (accumulate_map's zip of keys with values,
+          // eval_context.rs:216) and `keys` filters (:850-856) read it; nothing else does.
+          size_t kfirst = b.nodes.size();
+          grow(nall);
+          b.nodes[slot].b = (uint32_t)(kfirst - base);
+          for (uint32_t j = 0; j < nall; j++) {
+            const std::string& k = t.n[ti].keys[j];
+            DNode& kn = b.nodes[kfirst + j];
+            kn.kind = K_NULL; kn.count = nall; kn.a = 0; kn.b = 0; kn.parent = (uint32_t)(slot - base);
+            kn.key_len = (uint32_t)k.size();
+            kn.key_off = b.intern(k.data(), kn.key_len, fnv1a(k.data(), k.size()));
+            kn.key_hash = kn.key_off;
+            b.line[kfirst + j] = 0; b.col[kfirst + j] = 0;
+            b.kline[kfirst + j] = t.n[ti].kmarks[j].first;
+            b.kcol[kfirst + j] = t.n[ti].kmarks[j].second;
+          }
+        }
         for (uint32_t j = 0; j < cnt; j++) {
           DNode& c = b.nodes[first + j];
           c.key_len = (uint32_t)keys[j].size();
@@ -488,6 +512,11 @@ bool serde_yaml_load(const char* text, size_t len, Tree& t, uint32_t& root, std:
           for (size_t j = 0; j + 1 < f.items.size(); j += 2) {
             const TN& k = t.n[f.items[j]];
             if (k.kind != K_STRING) { yaml_event_delete(&ev); msg = "non string key"; return false; }
+            // serde_yaml 0.9 Mapping::deserialize refuses a repeated key (DuplicateKeyError, "duplicate
+            // entry with key {:?}"), so run_checks' YAML fallback fails with a YamlError (code 2);
+            // serde_yaml appends a position this loader does not reproduce
+            for (const std::string& prev : n.keys)
+              if (prev == k.s) { yaml_event_delete(&ev); msg = "duplicate entry with key " + rust_debug_str(k.s); return false; }
             n.keys.push_back(k.s); n.kmarks.push_back({0, 0}); n.kids.push_back(f.items[j + 1]);
           }
         } else {

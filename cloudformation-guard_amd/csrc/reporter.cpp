@@ -117,6 +117,11 @@ struct R {
   const RecSpan* aux = nullptr;   // the tile's side records (join-key lists, R4 / R5)
 
   static const uint32_t KEY_BIT = 0x20000000u;   // "the key of map entry X" (MapValue.keys)
+  // an unresolved result whose traversed_to is a count() value: SYN_BIT | the side record holding it
+  // (eval_core.inc publishable) -- an Int at the path and location of the count's first argument
+  static const uint32_t SYN_BIT = 0x40000000u;
+  bool is_syn(uint32_t ref) const { return ref != NONE && (ref & SYN_BIT) != 0; }
+  const QR& syn_of(uint32_t ref) const { return aux_at(ref & ~SYN_BIT).from; }
   const DocBatch& B(uint32_t ref) const { return (ref & LIT_BIT) ? prog.lit : docs; }
   uint32_t I(uint32_t ref) const { return ref & ~(LIT_BIT | KEY_BIT); }
   uint64_t base_of(uint32_t ref) const { return (ref & LIT_BIT) ? 0 : dbase; }
@@ -129,7 +134,14 @@ struct R {
     d.key_off = NONE; d.key_len = 0; d.key_hash = 0; d.parent = NONE;
     return d;
   }
-  DNode N(uint32_t ref) const { return is_key(ref) ? key_node(ref) : B(ref).nodes[G(ref)]; }
+  DNode N(uint32_t ref) const {
+    if (is_syn(ref)) {
+      const QR& q = syn_of(ref);
+      DNode d{}; d.kind = K_INT; d.a = q.uref; d.b = q.aux; d.key_off = NONE; d.parent = NONE;
+      return d;
+    }
+    return is_key(ref) ? key_node(ref) : B(ref).nodes[G(ref)];
+  }
   std::string str(uint32_t ref) const { DNode n = N(ref); return B(ref).bytes.substr(n.a, n.count); }
   std::string key(uint32_t ref) const { DNode n = N(ref); return B(ref).bytes.substr(n.key_off, n.key_len); }
   uint32_t child(uint32_t ref, uint32_t j) const { return (ref & LIT_BIT) | (N(ref).a + j); }
@@ -138,16 +150,19 @@ struct R {
   bool key_serde(uint32_t ref) const { return (ref & LIT_BIT) || docs.serde; }
   uint32_t parent_of(uint32_t ref) const { return B(ref).nodes[G(ref)].parent; }
   std::string path(uint32_t ref) const {
+    if (is_syn(ref)) { const uint32_t src = syn_of(ref).node; return src == NONE ? std::string() : path(src); }
     if (!is_key(ref)) return B(ref).path(base_of(ref), I(ref));
     std::string mp = B(ref).path(base_of(ref), parent_of(ref));
     if (key_serde(ref)) { const DNode& e = B(ref).nodes[G(ref)]; return mp + "/" + B(ref).bytes.substr(e.key_off, e.key_len); }
     return mp;
   }
   uint32_t line(uint32_t ref) const {
+    if (is_syn(ref)) { const uint32_t src = syn_of(ref).node; return src == NONE ? 0 : line(src); }
     if (!is_key(ref)) return B(ref).line[G(ref)];
     return key_serde(ref) ? 0 : B(ref).kline[G(ref)];
   }
   uint32_t col(uint32_t ref) const {
+    if (is_syn(ref)) { const uint32_t src = syn_of(ref).node; return src == NONE ? 0 : col(src); }
     if (!is_key(ref)) return B(ref).col[G(ref)];
     return key_serde(ref) ? 0 : B(ref).kcol[G(ref)];
   }
@@ -241,15 +256,23 @@ struct R {
       case K_MAP: {
         std::string keys, vals;
         std::string mp = path(ref);
-        for (uint32_t j = 0; j < n.count; j++) {
-          uint32_t c = child(ref, j);
+        const bool lit = (ref & LIT_BIT) != 0;
+        // MapValue.keys: the entries' keys, or the key block of a map with a repeated key (every
+        // occurrence; doc_loader.cpp Emitter)
+        const uint32_t kb = lit ? 0u : n.b;
+        const uint32_t nkeys = kb ? B(ref).nodes[base_of(ref) + kb].count : n.count;
+        for (uint32_t j = 0; j < nkeys; j++) {
+          const uint32_t c = kb ? kb + j : child(ref, j);
           std::string k = key(c);
-          if (j) { keys += ", "; vals += ", "; }
-          // MapValue.keys: libyaml mode -> parent path at the key mark; serde mode -> path/key at L0,C0
-          bool lit = (ref & LIT_BIT) != 0;
+          if (j) keys += ", ";
+          // libyaml mode -> parent path at the key mark; serde mode -> path/key at L0,C0
           if (serde || lit) keys += "String((" + dbg_path(mp + "/" + k, 0, 0) + ", " + rust_debug_str(k) + "))";
           else keys += "String((" + dbg_path(mp, B(c).kline[G(c)], B(c).kcol[G(c)]) + ", " + rust_debug_str(k) + "))";
-          vals += rust_debug_str(k) + ": " + debug(c);
+        }
+        for (uint32_t j = 0; j < n.count; j++) {
+          uint32_t c = child(ref, j);
+          if (j) vals += ", ";
+          vals += rust_debug_str(key(c)) + ": " + debug(c);
         }
         return "Map((" + p + ", MapValue { keys: [" + keys + "], values: {" + vals + "} }))";
       }
@@ -985,7 +1008,15 @@ void tile_error(const DocBatch& docs, uint32_t doc, const Program& prog, const T
     case E_RECORDS: err.kind = "Unsupported"; err.msg = "MI355X path: failure-record buffer exhausted"; break;
     case E_DEPTH: err.kind = "Unsupported"; err.msg = "MI355X path: evaluation depth limit exceeded"; break;
     default: {
-      static const char* why[] = {"", "variable captures", "filter after this query part", "traversal of a synthesized value",
+      if (t.err_a == 2) {
+        // a filter on a map after a step other than `*`, `[*]` or a key (e.g. `x[0][ ... ]`): the
+        // reference's `_ => unreachable!()` (eval_context.rs:752), a panic -- ffi-support's code -1
+        // with the panic payload as the message
+        err.kind = "Panic";
+        err.msg = "internal error: entered unreachable code";
+        break;
+      }
+      static const char* why[] = {"", "variable captures", "filter after this query part", "(unused)",
                                   "join index out of bounds report", "unresolved join keys report", "map key filters (KEYS)",
                                   "functions other than count()", "clause kind"};
       err.kind = "Unsupported";
@@ -1435,10 +1466,7 @@ bool report_batch(const DocBatch& docs, const std::vector<const Program*>& progs
     }
     if (fmt == OUT_YAML && d1 > d0) yaml_out[t] = w[t]->finish();
   };
-  std::vector<std::thread> th;
-  for (size_t t = 1; t < T; t++) th.emplace_back(work, t);
-  work(0);
-  for (auto& x : th) x.join();
+  parallel_run(T, work);
   // the first document (in order) whose report aborts decides the error (structured.rs:99-133)
   for (size_t t = 0; t < T; t++) if (err_doc[t] != SIZE_MAX) { err = errs[t]; return false; }
   if (fmt == OUT_YAML) {
@@ -1477,10 +1505,7 @@ bool report_batch_json_parts(const DocBatch& docs, const std::vector<const Progr
       if (d == d0 + 7 && d1 - d0 > 16) o.reserve(o.size() / 8 * (d1 - d0) / 8 * 9);
     }
   };
-  std::vector<std::thread> th;
-  for (size_t t = 1; t < T; t++) th.emplace_back(work, t);
-  work(0);
-  for (auto& x : th) x.join();
+  parallel_run(T, work);
   for (size_t t = 0; t < T; t++) if (err_doc[t] != SIZE_MAX) { err = errs[t]; return false; }
   std::vector<TextBuf> kept;
   for (auto& p : parts) if (!p.empty()) kept.push_back(std::move(p));
@@ -1509,10 +1534,7 @@ char* json_parts_join(const std::vector<TextBuf>& parts) {
     memcpy(buf + off[k], parts[k].data(), parts[k].size());
     memcpy(buf + off[k] + parts[k].size(), k + 1 < parts.size() ? ",\n" : "\n]", 2);
   };
-  std::vector<std::thread> th;
-  for (size_t k = 1; k < parts.size(); k++) th.emplace_back(copy, k);
-  copy(0);
-  for (auto& x : th) x.join();
+  parallel_run(parts.size(), copy);
   buf[n] = 0;
   return buf;
 }

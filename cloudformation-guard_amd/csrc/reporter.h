@@ -6,9 +6,11 @@
 #include <cstdlib>
 #include <cstdint>
 #include <cstring>
+#include <exception>
 #include <functional>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "doc_loader.h"
@@ -16,6 +18,25 @@
 #include "program.h"
 
 namespace gg {
+
+// Runs work(0) .. work(n - 1), work(0) on the calling thread and the others on their own threads.
+// An exception escaping a worker (std::bad_alloc on a large report, a writer's runtime_error) would
+// otherwise reach std::terminate on that thread; each is caught, all threads are joined, and the
+// lowest-indexed worker's exception is rethrown on the caller, where the C API turns it into an
+// extern_err_t.
+template <class F>
+void parallel_run(size_t n, F&& work) {
+  std::vector<std::exception_ptr> ex(n);
+  auto guarded = [&](size_t t) {
+    try { work(t); } catch (...) { ex[t] = std::current_exception(); }
+  };
+  std::vector<std::thread> th;
+  th.reserve(n ? n - 1 : 0);
+  for (size_t t = 1; t < n; t++) th.emplace_back(guarded, t);
+  if (n) guarded(0);
+  for (auto& x : th) x.join();
+  for (auto& e : ex) if (e) std::rethrow_exception(e);
+}
 
 // Non-owning view of one tile's device results (the session's fetched buffers).
 struct RecSpan {

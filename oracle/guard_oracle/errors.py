@@ -23,6 +23,7 @@ _DISPLAY = {
     "IllegalArguments": "{0}",
     "InternalError": "{0}",
     "Unsupported": "{0}",
+    "Panic": "{0}",   # a Rust panic (unreachable!()): ffi-support code -1, its payload as the message
 }
 
 FFI_CODES = {

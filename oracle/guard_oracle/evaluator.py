@@ -521,7 +521,8 @@ def query_retrieval(query_index, query, current, resolver, converter):
                     return accumulate_map(current, current.val, query_index, query, resolver, converter,
                                           check_and_delegate(conjunctions, name))
                 return []
-            raise GuardError("Unsupported", "unreachable filter predecessor")
+            # `_ => unreachable!()` (eval_context.rs:752): a panic, ffi-support code -1 with its payload
+            raise GuardError("Panic", "internal error: entered unreachable code")
         if current.kind == P.LIST:
             selected = []
             for each in current.val:

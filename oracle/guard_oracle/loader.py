@@ -18,7 +18,7 @@ import re
 from yaml._yaml import CParser
 
 from .errors import GuardError
-from .pv import PV, MapValue, STRING, INT, FLOAT, BOOL, NULL, LIST, MAP
+from .pv import rust_debug_str, PV, MapValue, STRING, INT, FLOAT, BOOL, NULL, LIST, MAP
 
 SHORT_FORM_TO_LONG = {
     "Ref": "Ref", "GetAtt": "Fn::GetAtt", "Base64": "Fn::Base64", "Sub": "Fn::Sub",
@@ -399,6 +399,9 @@ def serde_tree_to_pv(node, path=""):
         if not isinstance(kn, PV) or kn.kind != STRING:
             raise GuardError("InternalError", "non string type detected for key in a map at , "
                              "cfn-guard only supports keys that are string types")
+        if any(kn.val == k for k, _ in pairs):
+            # serde_yaml 0.9 Mapping::deserialize: DuplicateKeyError (its position suffix not restated)
+            raise GuardError("YamlError", "duplicate entry with key %s" % rust_debug_str(kn.val))
         pairs.append((kn.val, vn))
     for key, _ in pairs:
         mv.keys.append(PV(STRING, path + "/" + key, 0, 0, key))

@@ -82,10 +82,11 @@ def run_test(rules_text, rules_name, specs, output="text"):
     try:
         rf = parse_rules(rules_text, rules_name)
     except GuardError as e:
-        # test.rs:300-303 (plain text) / 345-350 (structured TestResult::Err), TEST_ERROR_STATUS_CODE
+        # test.rs:300-303 (plain text): TEST_ERROR_STATUS_CODE; 345-350 (structured TestResult::Err):
+        # handle_structured_single_report's exit_code stays SUCCESS_STATUS_CODE on this branch
         if output == "text":
             return "Parse Error on ruleset file %s\n" % e.display(), TEST_ERROR
-        return _structured_error(rules_name, e.display(), output)
+        return _structured_error(rules_name, e.display(), output, SUCCESS)
     if rf is None:
         # Ok(None): nothing written, SUCCESS_STATUS_CODE (test.rs:315, 366)
         return "", SUCCESS
@@ -181,15 +182,17 @@ def _structured(rf, rules_name, specs, output):
     return "\n".join(lines) + "\n", code
 
 
-def _structured_error(rules_name, error, output):
+def _structured_error(rules_name, error, output, code=TEST_ERROR):
+    """TestResult::Err report; `code`: TEST_ERROR for a spec file that does not load (structured.rs:57-59
+    get_exit_code), SUCCESS for an unparsable rules file (test.rs:338-350)"""
     result = OMap([("rule_file", rules_name), ("error", error)])
     if output == "json":
-        return to_json_pretty(result), TEST_ERROR
+        return to_json_pretty(result), code
     if output == "yaml":
-        return to_yaml(result), TEST_ERROR
+        return to_yaml(result), code
     return ("\n".join(['<?xml version="1.0" encoding="UTF-8"?>',
                        '<testsuites name="cfn-guard test report" tests="1" failures="0" errors="1" time="0">',
                        '    <testsuite name="%s" errors="1" failures="0" time="0">' % _xml_escape(rules_name),
                        '        <testcase name="%s" time="0" status="error">' % _xml_escape(rules_name),
                        '            <error>%s</error>' % _xml_escape(error),
-                       '        </testcase>', '    </testsuite>', '</testsuites>']) + "\n", TEST_ERROR)
+                       '        </testcase>', '    </testsuite>', '</testsuites>']) + "\n", code)

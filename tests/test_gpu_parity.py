@@ -292,8 +292,8 @@ def test_parallel_report_matches_serial():
 def test_duplicate_yaml_keys_vs_oracle():
     """a repeated mapping key keeps its first position and takes the last value
     (MapValue.values is an IndexMap, path_value.rs:453-470); value queries over such documents,
-    in every output format, against the oracle (PyYAML keeps the same first-position / last-value
-    mapping).  `keys` filters over a duplicate key are the documented exception."""
+    in every output format, against the oracle (its libyaml loader keeps the same first-position /
+    last-value mapping; `keys` filters and captures: the test below)."""
     data = [("dup.yaml", "Resources:\n  b:\n    Type: AWS::S3::Bucket\n    Properties:\n      Port: 1\n      Name: x\n"
                          "      Port: 2\n  c:\n    Type: AWS::S3::Bucket\n    Type: AWS::EC2::Volume\n    Properties:\n"
                          "      Size: 300\n")]
@@ -304,3 +304,74 @@ def test_duplicate_yaml_keys_vs_oracle():
         exp, ecode, _ = oracle_validate(rules, data, output=fmt)
         out, code = guard_amd.validate_structured(rules, data, output=fmt)
         assert (code, out) == (ecode, exp), fmt
+
+
+def _dup_pack():
+    p = os.path.join(G, "dupkey_rulepack")
+    return [("dup.guard", open(os.path.join(p, "dup.guard")).read())], \
+        [("dup.yaml", open(os.path.join(p, "dup.yaml.txt")).read())]
+
+
+def test_duplicate_keys_keys_filters_and_captures_vs_oracle():
+    """SURVEY.md App. B #7 reproduced: MapValue.keys keeps every occurrence of a repeated key
+    (loader.rs:172-185) while values keep one entry each (path_value.rs:453-470), so
+    * `keys ==` / `keys in` filters compare every occurrence and select values.get(key) once per
+      passing occurrence (eval_context.rs:850-880);
+    * `Resources[ id ]` / `x[ id | filter ]` captures take accumulate_map's misaligned zip of keys
+      with values (eval_context.rs:216);
+    * the Debug of such a map (reason R8 / R1 texts) lists the duplicate keys with their marks.
+    Byte-identical with the oracle in every format, in lane and wave mode."""
+    rules, data = _dup_pack()
+    for fmt in ("json", "yaml", "sarif", "junit"):
+        exp, ecode, _ = oracle_validate(rules, data, output=fmt)
+        out, code = guard_amd.validate_structured(rules, data, output=fmt)
+        assert (code, out) == (ecode, exp), fmt
+    outs = []
+    for mode in (0, 1):
+        s = guard_amd.Session()
+        s.configure(mode, 0)
+        s.add_rules(rules[0][1], rules[0][0])
+        s.add_docs([data[0][1]] * 70, ["dup.yaml"] * 70)
+        s.eval(1)
+        outs.append(s.report())
+        s.close()
+    assert outs[0] == outs[1]
+
+
+def test_count_result_traversal_vs_oracle():
+    """A count() result is an ordinary Int to the query engine: key / index / map-key-filter steps
+    on it are UnResolved R8 / R9 / R11 (eval_context.rs:573-581, 587-607, 913-919), `[*]` / `*`
+    pass it through (:609-721), a block or a `[*]` filter evaluates over it -- no E_UNSUPPORTED.
+    Also the scalar-under-`[*]` filter's clauses are reported with the enclosing clause (no Filter
+    container, :790-815).  Every format, lane and wave mode."""
+    p = os.path.join(G, "count_rulepack")
+    rules = [("cnt.guard", open(os.path.join(p, "cnt.guard")).read())]
+    docs = ['{"Resources": {"a": {"Type": "X", "Props": {"Size": 5, "Tags": "t"}}, "b": {"Type": "Y", "Props": {"Size": 50}}}}',
+            '{"Other": 1}', '{"Resources": {}}', 'Resources:\n  q:\n    Props:\n      Size: 1\n']
+    data = [("t%d.json" % i, d) for i, d in enumerate(docs)]
+    for fmt in ("json", "yaml", "sarif", "junit"):
+        exp, ecode, _ = oracle_validate(rules, data, output=fmt)
+        out, code = guard_amd.validate_structured(rules, data, output=fmt)
+        assert (code, out) == (ecode, exp), fmt
+    outs = []
+    for mode in (0, 1):
+        s = guard_amd.Session()
+        s.configure(mode, 0)
+        s.add_rules(rules[0][1], rules[0][0])
+        s.add_docs(docs * 20, ["t%d.json" % (i % 4) for i in range(80)])
+        s.eval(1)
+        outs.append(s.report())
+        s.close()
+    assert outs[0] == outs[1]
+
+
+def test_unreachable_filter_predecessor_panics_like_the_reference():
+    """`x[0][ filter ]` on a map: the reference's `_ => unreachable!()` (eval_context.rs:752) panics;
+    through guard-ffi that is code -1 with the panic payload, which the device path reports too"""
+    rules = [("u.guard", "Resources.list[0][ a exists ] !empty\n")]
+    data = [("u.json", '{"Resources": {"list": [{"a": 1}]}}')]
+    _, ecode, err = oracle_validate(rules, data)
+    assert ecode == -1 and "entered unreachable code" in err
+    with pytest.raises(guard_amd.GuardError) as ei:
+        guard_amd.validate_structured(rules, data)
+    assert ei.value.code == -1 and ei.value.message == "internal error: entered unreachable code"

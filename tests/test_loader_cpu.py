@@ -56,6 +56,18 @@ def test_json_words_stay_strings():
 
 def test_duplicate_keys_first_position_last_value():
     # path_value.rs:453-470: MapValue.values is an IndexMap, so a repeated key keeps its first
-    # position and takes the last value (the duplicate key itself only survives in MapValue.keys,
-    # loader.rs:172-185 -- see DESIGN.md for the consequence for `keys` filters)
-    assert guard_amd.load_dump("a: 1\nb: 0\na: 2\n", 0) == '{"a": Int(2), "b": Int(0)}'
+    # position and takes the last value; MapValue.keys keeps every occurrence with its own mark
+    # (the libyaml loader's IndexMap is keyed by (key, Location), loader.rs:172-185)
+    assert guard_amd.load_dump("a: 1\nb: 0\na: 2\n", 0) == '{"a": Int(2), "b": Int(0)} keys ["a"@0:0, "b"@1:0, "a"@2:0]'
+    assert guard_amd.load_dump("x:\n  - {k: 1, k: 2, j: 3}\n", 0) == '{"x": [{"k": Int(2), "j": Int(3)} keys ["k"@1:5, "k"@1:11, "j"@1:17]]}'
+    # no repeated key: no key block
+    assert guard_amd.load_dump("a: 1\nb: 0\n", 0) == '{"a": Int(1), "b": Int(0)}'
+
+
+def test_duplicate_keys_serde_loaders():
+    # guard-ffi run_checks: serde_json keeps one key (preserve_order IndexMap, last value, first
+    # position); its serde_yaml 0.9 fallback refuses the mapping (DuplicateKeyError) -> code 2
+    assert guard_amd.load_dump('{"a": 1, "b": 0, "a": 2}', 1) == '{"a": Int(2), "b": Int(0)}'
+    with pytest.raises(guard_amd.GuardError) as ei:
+        guard_amd.load_dump("a: 1\nb: 0\na: 2\n", 1)
+    assert ei.value.code == 2 and 'duplicate entry with key "a"' in ei.value.message
