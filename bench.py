@@ -12,7 +12,7 @@ collective; documents shard with no data-path exchange, so scaling is weak: each
 --docs templates).  Records for failing clauses are written to HBM each step, as the reporter
 consumes them.
 
-roofline: HBM-bound.  Algorithmic bytes per launch = arena bytes (nodes x 32 B + string pool +
+roofline: HBM-bound.  Algorithmic bytes per launch = arena bytes (nodes x 16 B + string pool +
 roots, each template counted once however many rules files read it) + per-tile outputs
 (32 B TileOut + 1 B per top-level rule) + record bytes (48 B each).  `achieved` divides that
 by the evaluation kernel's mean duration, timed with HIP events on the launch stream (torch's
@@ -160,6 +160,9 @@ def main():
     ap.add_argument("--threads", type=int, default=0, help="host loader threads (default: CPU share)")
     ap.add_argument("--loader", choices=("host", "device"), default="host",
                     help="document loader: host threads, or the MI355X JSON loader (csrc/json_gpu.hip)")
+    ap.add_argument("--gather-docs", type=int, default=200,
+                    help="N > 1: each rank renders the structured JSON report of its first GATHER_DOCS documents "
+                         "and rank 0 gathers them (sharding.gather_report; outside the timed region)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-per-core", type=int, default=0)
     ap.add_argument("--dist-backend", default="nccl",
@@ -274,6 +277,22 @@ def main():
     tally_sum = int(counts.sum().item())   # the all-reduced tensor: every rank's last-step tallies
     n_fail, n_pass, n_skip, n_err = sess.stat(4), sess.stat(5), sess.stat(6), sess.stat(7)
 
+    gather = None
+    if world > 1 and args.gather_docs > 0:
+        # the report half of the multi-GPU path: every rank renders its documents'
+        # reports, rank 0 receives them over the collective backend (RCCL: device buffers) and
+        # stitches them in rank order with the job's exit code
+        t0 = time.time()
+        text, code = sess.report_range("json", 0, min(ndocs, args.gather_docs))
+        t_render = time.time() - t0
+        t0 = time.time()
+        merged, job_code = sharding.gather_report(text, code, dist, output="json")
+        t_gather = time.time() - t0
+        if rank == 0:
+            gather = {"docs_per_rank": min(ndocs, args.gather_docs), "render_s": round(t_render, 3),
+                      "gather_s": round(t_gather, 3), "bytes": len(merged.encode()), "exit_code": job_code,
+                      "file_reports": merged.count('\n  {\n    "name": ')}
+
     e2e = None
     if rank == 0 and world == 1 and not args.no_e2e:
         rdocs = min(ndocs, args.e2e_report_docs) if args.e2e_report_docs else ndocs
@@ -334,6 +353,8 @@ def main():
         }
         line["cpu_baseline"] = cpu
         line["e2e"] = e2e
+        if gather is not None:
+            line["report_gather"] = gather
         print(json.dumps(line), flush=True)
     sess.close()
     if dist is not None:

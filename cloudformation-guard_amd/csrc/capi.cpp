@@ -279,6 +279,7 @@ struct gg_session {
   DocBatch docs;
   std::vector<std::unique_ptr<GpuProgram>> progs;
   std::vector<std::string> parse_errors;   // rules files that failed to parse (exit code 5)
+  std::unique_ptr<DocBatch> params;        // merged input parameters (validate -i), one document
   // device residency: buffers borrowed from the device-state pool at upload (DeviceBufs)
   DeviceBufs* dv = nullptr;
   uint32_t type_key = NONE;
@@ -657,14 +658,19 @@ unsigned report_threads() {
 
 // structured report over (docs x programs) in format `fmt` (OutFormat); false + err for an aborting error
 // (cstr != null and JSON: the report goes to *cstr, a malloc'd buffer, without an intermediate string)
+// Documents [first, first + count) only (count SIZE_MAX: to the end): the report a run over just those
+// documents writes -- a rank's shard of a multi-GPU job (sharding.gather_report stitches them).
 bool session_report(gg_session* s, std::string& out, int32_t& exit_code, ReportError& err, int32_t fmt = OUT_JSON,
-                    char** cstr = nullptr) {
+                    char** cstr = nullptr, size_t first = 0, size_t count = SIZE_MAX) {
   exit_code = s->parse_errors.empty() ? 0 : 5;
   std::vector<const Program*> progs;
   for (auto& p : s->progs) progs.push_back(&p->prog);
   size_t nf = progs.size();
+  first = std::min(first, s->docs.ndocs());
+  const size_t nd = std::min(count, s->docs.ndocs() - first);
+  const size_t t0 = first * nf, t1 = (first + nd) * nf;
   // the first tile in (doc, rules-file) order that raised an error aborts the run (structured.rs:110)
-  for (size_t t = 0; t < s->tiles.size(); t++) {
+  for (size_t t = t0; t < t1; t++) {
     if (s->tiles[t].err) {
       tile_error(s->docs, (uint32_t)(t / nf), *progs[t % nf], s->tiles[t], err);
       exit_code = -1;
@@ -672,15 +678,14 @@ bool session_report(gg_session* s, std::string& out, int32_t& exit_code, ReportE
     }
   }
   out.clear();
-  const size_t nd = s->docs.ndocs();
   auto tile = [&](size_t d, size_t f) {
     return tile_view(s->tiles.data(), s->rule_status.data(), s->max_top, s->recs.data(), d * nf + f);
   };
   if (fmt == OUT_JSON && cstr) {
     std::vector<TextBuf> parts;
-    if (!report_batch_json_parts(s->docs, progs, 0, nd, tile, report_threads(), parts, err)) { exit_code = -1; return false; }
+    if (!report_batch_json_parts(s->docs, progs, first, nd, tile, report_threads(), parts, err)) { exit_code = -1; return false; }
     *cstr = json_parts_join(parts);
-  } else if (!report_batch(s->docs, progs, 0, nd, tile, fmt, report_threads(), out, err)) {
+  } else if (!report_batch(s->docs, progs, first, nd, tile, fmt, report_threads(), out, err)) {
     exit_code = -1;
     return false;
   }
@@ -688,7 +693,7 @@ bool session_report(gg_session* s, std::string& out, int32_t& exit_code, ReportE
   // (structured.rs:40-43).  CommonStructuredReporter overwrites it with 19 (structured.rs:110-112);
   // JunitReporter::update_exit_code keeps 5 (reporters/mod.rs:97-103, validate/xml.rs:62-66).
   bool anyfail = false;
-  for (auto& t : s->tiles) if (t.status == ST_FAIL) anyfail = true;
+  for (size_t t = t0; t < t1; t++) if (s->tiles[t].status == ST_FAIL) anyfail = true;
   if (anyfail && !(fmt == OUT_JUNIT && exit_code == 5)) exit_code = 19;
   return true;
 }
@@ -758,6 +763,34 @@ void merge_batch(DocBatch& dst, DocBatch& src) {
   std::vector<DocBatch> one(1);
   one[0] = std::move(src);
   merge_batches(dst, one);
+}
+
+// Input parameters (validate.rs:317-350): each file loaded like a data file (build_data_file), then
+// merged in order, `primary = primary.merge(path_value)?` -- a merge error aborts (no unwrap here)
+bool load_params(const validate_input_t* params, size_t n, std::unique_ptr<DocBatch>& out, LoadError& le) {
+  out.reset();
+  for (size_t i = 0; i < n; i++) {
+    const char* t = params[i].content ? params[i].content : "";
+    std::unique_ptr<DocBatch> next(new DocBatch());
+    if (!load_document(*next, t, strlen(t), params[i].file_name ? params[i].file_name : "", LOAD_LIBYAML, le)) return false;
+    if (out && !merge_into_last(*next, 0, *out, 0, le)) return false;
+    out = std::move(next);
+  }
+  return true;
+}
+
+// Rust Debug of a merge Error (derived: `Variant("message")`), as `.unwrap()` prints it
+std::string merge_error_debug(const LoadError& le) { return le.kind + "(" + rust_debug_str(le.msg) + ")"; }
+
+// merged_data (structured.rs:51-65): `data.clone().merge(file.path_value.clone()).unwrap()` -- a
+// merge error is a panic there; here code -1 with the panic message
+bool merge_params_last(DocBatch& b, const DocBatch* params, LoadError& le) {
+  if (!params || b.ndocs() == 0) return true;
+  LoadError me;
+  if (merge_into_last(b, b.ndocs() - 1, *params, 0, me)) return true;
+  le.kind = "Panic";
+  le.msg = "called `Result::unwrap()` on an `Err` value: " + merge_error_debug(me);
+  return false;
 }
 
 bool add_rules(gg_session* s, const std::string& text, const std::string& name, std::string& perr) {
@@ -842,6 +875,12 @@ char* cfn_guard_validate_batch(const validate_input_t* docs, size_t n_docs, cons
 
 char* cfn_guard_validate_batch_format(const validate_input_t* docs, size_t n_docs, const validate_input_t* rules,
                                       size_t n_rules, int32_t output_format, int32_t* exit_code, extern_err_t* err) {
+  return cfn_guard_validate_batch_params(docs, n_docs, rules, n_rules, nullptr, 0, output_format, exit_code, err);
+}
+
+char* cfn_guard_validate_batch_params(const validate_input_t* docs, size_t n_docs, const validate_input_t* rules,
+                                      size_t n_rules, const validate_input_t* params, size_t n_params,
+                                      int32_t output_format, int32_t* exit_code, extern_err_t* err) {
   set_err(err, 0, "");
   if (output_format < OUT_JSON || output_format > OUT_JUNIT) {
     set_err(err, 18, "IllegalArguments: unknown output format");
@@ -859,6 +898,12 @@ char* cfn_guard_validate_batch_format(const validate_input_t* docs, size_t n_doc
       if (!add_rules(&s, rules[i].content ? rules[i].content : "", name, perr))
         s.parse_errors.push_back("Parsing error handling rule file = " + name + ", Error = " + error_display("ParseError", perr) + "\n---");
     }
+    // Validate::execute order: data files (validate.rs:274-315), then the parameter files (317-350),
+    // then the merge into every data file (structured.rs:51-65, a panic on conflict)
+    LoadError pe;
+    const bool params_ok = load_params(params, n_params, s.params, pe);
+    LoadError panic;
+    bool panicked = false;
     for (size_t i = 0; i < n_docs; i++) {
       LoadError le;
       const char* t = docs[i].content ? docs[i].content : "";
@@ -867,6 +912,13 @@ char* cfn_guard_validate_batch_format(const validate_input_t* docs, size_t n_doc
         if (exit_code) *exit_code = -1;
         return nullptr;
       }
+      if (params_ok && !panicked && !merge_params_last(s.docs, s.params.get(), panic)) panicked = true;
+    }
+    if (!params_ok || panicked) {
+      const LoadError& e = !params_ok ? pe : panic;
+      set_err(err, ffi_code(e.kind), error_display(e.kind, e.msg));
+      if (exit_code) *exit_code = -1;
+      return nullptr;
     }
     session_upload(&s);
     session_run(&s, true);
@@ -1199,10 +1251,12 @@ int32_t gg_session_add_docs(gg_session* s, const char* const* texts, const size_
   std::vector<DocBatch> parts(nthreads);
   std::vector<LoadError> errs(nthreads);
   std::vector<int> failed(nthreads, -1);
+  const DocBatch* params = s->params.get();
   auto work = [&](int t) {
     size_t lo = n * t / nthreads, hi = n * (t + 1) / nthreads;
     for (size_t i = lo; i < hi; i++) {
-      if (!load_document(parts[t], texts[i], lens[i], names ? names[i] : std::string(), (LoadMode)mode, errs[t])) { failed[t] = (int)i; return; }
+      if (!load_document(parts[t], texts[i], lens[i], names ? names[i] : std::string(), (LoadMode)mode, errs[t]) ||
+          !merge_params_last(parts[t], params, errs[t])) { failed[t] = (int)i; return; }
     }
   };
   try {
@@ -1216,6 +1270,26 @@ int32_t gg_session_add_docs(gg_session* s, const char* const* texts, const size_
   } catch (std::exception& e) { set_err(err, -1, e.what()); return -1; }
   s->uploaded = false;
   return 0;
+}
+
+int32_t gg_session_set_params(gg_session* s, const char* const* texts, const size_t* lens, const char* const* names,
+                              size_t n, extern_err_t* err) {
+  set_err(err, 0, "");
+  try {
+    std::vector<validate_input_t> in(n);
+    std::vector<std::string> tx(n);
+    for (size_t i = 0; i < n; i++) {
+      tx[i].assign(texts[i], lens[i]);   // NUL-terminated copies (load_params reads C strings)
+      in[i].content = tx[i].c_str();
+      in[i].file_name = names ? names[i] : "";
+    }
+    LoadError le;
+    if (!load_params(in.data(), n, s->params, le)) {
+      set_err(err, ffi_code(le.kind), error_display(le.kind, le.msg));
+      return ffi_code(le.kind);
+    }
+    return 0;
+  } catch (std::exception& e) { set_err(err, -1, e.what()); return -1; }
 }
 
 int32_t gg_loader_selfcheck(const char* text, size_t len) { return loader_selfcheck(text, len); }
@@ -1351,7 +1425,8 @@ int32_t gg_session_add_synthetic(gg_session* s, uint64_t first, size_t n, int32_
       for (size_t i = lo; i < hi; i++) {
         cfn_synth_doc(first + i, n_resources, text);
         if (!load_document(B, text.data(), text.size(), "synthetic-" + std::to_string(first + i) + ".json",
-                           LOAD_LIBYAML, errs[t])) { failed[t] = 1; return; }
+                           LOAD_LIBYAML, errs[t]) ||
+            !merge_params_last(B, s->params.get(), errs[t])) { failed[t] = 1; return; }
         // size the part's columns once from its first documents (the generator's documents are
         // alike) instead of growing them by doubling, which copies them again and again
         if (i == lo + 7 && hi - lo > 16) {
@@ -1386,6 +1461,7 @@ int32_t gg_session_add_docs_device(gg_session* s, const char* const* texts, cons
     std::string why;
     if (!ensure_device(why)) { set_err(err, -1, why); return -1; }
     if (s->docs.ndocs()) { set_err(err, 18, "IllegalArguments: the device loader fills an empty session"); return -1; }
+    if (s->params) { set_note(err, "input parameters are merged by the host loader (gg_session_add_docs)"); return 1; }
     std::vector<std::string> nm(n);
     for (size_t i = 0; i < n; i++) nm[i] = names ? names[i] : std::string();
     GpuLoadStats st;
@@ -1503,6 +1579,26 @@ char* gg_session_report_format(gg_session* s, int32_t output_format, int32_t* ex
   }
   if (exit_code) *exit_code = code;
   return cs ? cs : dup_str(out);
+}
+
+char* gg_session_report_range(gg_session* s, int32_t output_format, size_t first, size_t count, int32_t* exit_code,
+                              extern_err_t* err) {
+  set_err(err, 0, "");
+  if (!s->evaluated) { set_err(err, -1, "session not evaluated"); return nullptr; }
+  if (output_format < OUT_JSON || output_format > OUT_JUNIT) { set_err(err, 18, "IllegalArguments: unknown output format"); return nullptr; }
+  try {
+    std::string out;
+    char* cs = nullptr;
+    int32_t code = 0;
+    ReportError re;
+    if (!session_report(s, out, code, re, output_format, &cs, first, count)) {
+      if (exit_code) *exit_code = -1;
+      set_err(err, ffi_code(re.kind), error_display(re.kind, re.msg));
+      return nullptr;
+    }
+    if (exit_code) *exit_code = code;
+    return cs ? cs : dup_str(out);
+  } catch (std::exception& e) { set_err(err, -1, e.what()); return nullptr; }
 }
 
 // statistics: 0 ndocs, 1 nfiles, 2 nodes, 3 string bytes, 4 tiles FAIL, 5 tiles PASS, 6 tiles SKIP,

@@ -1057,6 +1057,123 @@ bool load_document(DocBatch& b, const char* text, size_t len, const std::string&
   return emit_root(b, t, root, name, true, err);
 }
 
+// ------------------------------------------------------ input parameters ---
+namespace {
+const char* merge_type_info(uint32_t k) {   // PathAwareValue::type_info (path_value.rs:985-1000)
+  static const char* t[] = {"null", "String", "Regex", "bool", "int", "float", "char", "array", "map",
+                            "range(int, int)", "range(float, float)", "range(char, char)"};
+  return k < 12 ? t[k] : "?";
+}
+}  // namespace
+
+bool merge_into_last(DocBatch& b, size_t d, const DocBatch& P, size_t pd, LoadError& err) {
+  const uint64_t base = b.base[d];
+  const uint64_t pbase = P.base[pd];
+  const uint64_t pend = pd + 1 < P.base.size() ? P.base[pd + 1] : P.nodes.size();
+  const uint32_t np = (uint32_t)(pend - pbase);
+  const DNode A = P.nodes[pbase + P.roots[pd]];     // self
+  const DNode Bn = b.nodes[base + b.roots[d]];       // other
+  const uint32_t broot = b.roots[d];
+  if (!((A.kind == K_MAP && Bn.kind == K_MAP) || (A.kind == K_LIST && Bn.kind == K_LIST))) {
+    err.kind = "IncompatibleError";
+    err.msg = std::string("Types are not compatible for merges ") + merge_type_info(A.kind) + ", " + merge_type_info(Bn.kind);
+    return false;
+  }
+  auto pkey = [&](const DNode& e) { return std::string(P.bytes.data() + e.key_off, e.key_len); };
+  if (A.kind == K_MAP) {
+    // `for (key, value) in other_map.values`: the first of other's keys that self already holds
+    std::unordered_map<std::string, int> have;
+    for (uint32_t j = 0; j < A.count; j++) have[pkey(P.nodes[pbase + A.a + j])] = 1;
+    for (uint32_t j = 0; j < Bn.count; j++) {
+      const DNode& e = b.nodes[base + Bn.a + j];
+      std::string k(b.bytes.data() + e.key_off, e.key_len);
+      if (have.count(k)) { err.kind = "MultipleValues"; err.msg = "Key " + k + ", already exists in map"; return false; }
+    }
+  }
+  const uint64_t rel0 = b.nodes.size() - base;   // relative index of the first appended node
+  if (rel0 + np + 8 + 2ull * (A.count + Bn.count) + (A.kind == K_MAP && A.b ? P.nodes[pbase + A.b].count : 0) > kMaxDocNodes) {
+    err.kind = "IncompatibleError"; err.msg = "document too large for the MI355X arena"; return false;
+  }
+  const uint32_t O = (uint32_t)rel0;
+  // 1. self's nodes, rebased to O, strings re-interned into b's pool
+  b.grow_zeroed(base + rel0 + np);
+  std::unordered_map<uint32_t, uint32_t> sid;   // P string id -> b string id
+  auto str_id = [&](uint32_t off, uint32_t len) {
+    auto it = sid.find(off);
+    if (it != sid.end()) return it->second;
+    const uint32_t id = b.intern(P.bytes.data() + off, len, fnv1a(P.bytes.data() + off, len));
+    sid[off] = id;
+    return id;
+  };
+  for (uint32_t i = 0; i < np; i++) {
+    DNode n = P.nodes[pbase + i];
+    const size_t g = base + rel0 + i;
+    if (n.kind == K_LIST || n.kind == K_MAP) { n.a += O; if (n.kind == K_MAP && n.b) n.b += O; }
+    if (n.kind == K_STRING || n.kind == K_REGEX) { n.a = str_id(n.a, n.count); n.b = n.a; }
+    if (n.key_off != NONE) { n.key_off = str_id(n.key_off, n.key_len); n.key_hash = n.key_off; }
+    if (n.parent != NONE) n.parent += O;
+    b.nodes[g] = n;
+    b.line[g] = P.line[pbase + i]; b.col[g] = P.col[pbase + i];
+    b.kline[g] = P.kline[pbase + i]; b.kcol[g] = P.kcol[pbase + i];
+  }
+  const uint32_t aroot = O + P.roots[pd];
+  const DNode Ar = b.nodes[base + aroot];
+  // 2. the merged root, then its entries: self's, then other's (shallow copies: their subtrees stay)
+  const uint32_t R = O + np, E = R + 1, n = Ar.count + Bn.count;
+  b.grow_zeroed(base + E + n);
+  {
+    DNode& r = b.nodes[base + R];
+    r.kind = Ar.kind; r.count = n; r.a = E; r.b = 0; r.key_off = NONE; r.key_len = 0; r.key_hash = 0; r.parent = NONE;
+    b.line[base + R] = b.line[base + aroot]; b.col[base + R] = b.col[base + aroot];   // self's location
+  }
+  for (uint32_t j = 0; j < n; j++) {
+    const bool mine = j < Ar.count;
+    const uint64_t src = base + (mine ? Ar.a + j : Bn.a + (j - Ar.count));
+    const uint64_t g = base + E + j;
+    b.nodes[g] = b.nodes[src];
+    b.line[g] = b.line[src]; b.col[g] = b.col[src];
+    if (Ar.kind == K_MAP) {
+      b.nodes[g].parent = R;
+      if (mine) { b.kline[g] = b.kline[src]; b.kcol[g] = b.kcol[src]; }
+      else {
+        // map.keys.push(String((path.extend_str(&key), key))): other's root path + "/key" at other's location
+        b.kline[g] = b.line[base + broot] | kKeyPathExt; b.kcol[g] = b.col[base + broot];
+      }
+    } else {
+      b.kline[g] = 0; b.kcol[g] = 0;
+    }
+  }
+  if (Ar.kind == K_LIST) {
+    // vec.extend: the elements keep their own paths (their index in the list they came from), so
+    // each side's copies hang under a detached list node whose first child is the side's first copy
+    const uint32_t V = E + n;
+    b.grow_zeroed(base + V + 2);
+    for (uint32_t k = 0; k < 2; k++) {
+      DNode& v = b.nodes[base + V + k];
+      v.kind = K_LIST; v.count = k ? Bn.count : Ar.count; v.a = k ? E + Ar.count : E; v.parent = NONE;
+      v.key_off = NONE; v.key_len = 0; v.key_hash = 0;
+    }
+    for (uint32_t j = 0; j < n; j++) b.nodes[base + E + j].parent = j < Ar.count ? V : V + 1;
+  } else if (Ar.b) {
+    // self keeps a key block (a repeated key): the merged keys are self's keys, then other's
+    const uint32_t na = b.nodes[base + Ar.b].count, nk = na + Bn.count, K = E + n;
+    b.grow_zeroed(base + K + nk);
+    for (uint32_t j = 0; j < nk; j++) {
+      const uint64_t g = base + K + j;
+      const uint64_t src = j < na ? base + Ar.b + j : base + E + Ar.count + (j - na);
+      DNode k = b.nodes[src];
+      DNode& kn = b.nodes[g];
+      kn = DNode{};
+      kn.kind = K_NULL; kn.count = nk; kn.parent = R;
+      kn.key_off = k.key_off; kn.key_len = k.key_len; kn.key_hash = k.key_hash;
+      b.kline[g] = b.kline[src]; b.kcol[g] = b.kcol[src];
+    }
+    b.nodes[base + R].b = K;
+  }
+  b.roots[d] = R;
+  return true;
+}
+
 // test hook: 1 when the fast path accepts `text` and builds exactly the libyaml path's arena,
 // 0 when they differ, -1 when the fast path declines (or libyaml fails)
 int loader_selfcheck(const char* text, size_t len) {

@@ -86,4 +86,16 @@ int loader_selfcheck(const char* text, size_t len);
 bool load_document(DocBatch& b, const char* text, size_t len, const std::string& name,
                    LoadMode mode, LoadError& err);
 
+// kline flag of a map entry: the entry's key PathAwareValue has the map's path + "/key" at the
+// location kept in kline/kcol (keys PathAwareValue::merge pushes, path_value.rs:905-907), not the
+// map's path at the key's own mark (path_value.rs:459-466)
+constexpr uint32_t kKeyPathExt = 0x80000000u;
+
+// `cfn-guard validate -i`: PathAwareValue::merge (path_value.rs:889-919) of `self` = document `pd`
+// of P (the input parameters) with `other` = document d of b, which must be b's last document.
+// The merged value is built in place after d's nodes (d's own nodes are not touched) and becomes d's
+// root (b.roots[d]).  Returns false with err = MultipleValues / IncompatibleError (the reference's
+// messages) and b unchanged.
+bool merge_into_last(DocBatch& b, size_t d, const DocBatch& P, size_t pd, LoadError& err);
+
 }  // namespace gg

@@ -148,18 +148,20 @@ struct R {
   // key PV paths: libyaml loader -> the map's path at the key mark (path_value.rs:467-470);
   // serde loader / rule literals -> map path + "/key" at the map's (0,0) location (:391-395)
   bool key_serde(uint32_t ref) const { return (ref & LIT_BIT) || docs.serde; }
+  // a key PathAwareValue::merge pushed (input parameters): map path + "/key" at kline's location
+  bool key_ext(uint32_t ref) const { return !(ref & LIT_BIT) && (B(ref).kline[G(ref)] & kKeyPathExt) != 0; }
   uint32_t parent_of(uint32_t ref) const { return B(ref).nodes[G(ref)].parent; }
   std::string path(uint32_t ref) const {
     if (is_syn(ref)) { const uint32_t src = syn_of(ref).node; return src == NONE ? std::string() : path(src); }
     if (!is_key(ref)) return B(ref).path(base_of(ref), I(ref));
     std::string mp = B(ref).path(base_of(ref), parent_of(ref));
-    if (key_serde(ref)) { const DNode& e = B(ref).nodes[G(ref)]; return mp + "/" + B(ref).bytes.substr(e.key_off, e.key_len); }
+    if (key_serde(ref) || key_ext(ref)) { const DNode& e = B(ref).nodes[G(ref)]; return mp + "/" + B(ref).bytes.substr(e.key_off, e.key_len); }
     return mp;
   }
   uint32_t line(uint32_t ref) const {
     if (is_syn(ref)) { const uint32_t src = syn_of(ref).node; return src == NONE ? 0 : line(src); }
     if (!is_key(ref)) return B(ref).line[G(ref)];
-    return key_serde(ref) ? 0 : B(ref).kline[G(ref)];
+    return key_serde(ref) ? 0 : B(ref).kline[G(ref)] & ~kKeyPathExt;
   }
   uint32_t col(uint32_t ref) const {
     if (is_syn(ref)) { const uint32_t src = syn_of(ref).node; return src == NONE ? 0 : col(src); }
@@ -267,7 +269,11 @@ struct R {
           if (j) keys += ", ";
           // libyaml mode -> parent path at the key mark; serde mode -> path/key at L0,C0
           if (serde || lit) keys += "String((" + dbg_path(mp + "/" + k, 0, 0) + ", " + rust_debug_str(k) + "))";
-          else keys += "String((" + dbg_path(mp, B(c).kline[G(c)], B(c).kcol[G(c)]) + ", " + rust_debug_str(k) + "))";
+          else {
+            const uint32_t kl = B(c).kline[G(c)];
+            keys += "String((" + dbg_path((kl & kKeyPathExt) ? mp + "/" + k : mp, kl & ~kKeyPathExt, B(c).kcol[G(c)]) + ", " +
+                    rust_debug_str(k) + "))";
+          }
         }
         for (uint32_t j = 0; j < n.count; j++) {
           uint32_t c = child(ref, j);
@@ -948,6 +954,16 @@ std::string error_display(const std::string& kind, const std::string& msg) {
   if (kind == "NotComparable") return "Comparing incoming context with literals or dynamic results wasn't possible `" + msg + "`";
   if (kind == "YamlError") return "Error parsing incoming YAML context " + msg;
   if (kind == "JsonError") return "Error parsing incoming JSON context " + msg;
+  // the rest of errors.rs:11-54's Display strings
+  if (kind == "MultipleValues") return "Conflicting rule or variable assignments inside the same scope `" + msg + "`";
+  if (kind == "MissingVariable") return "Variable assignment could not be resolved in rule file or incoming context `" + msg + "`";
+  if (kind == "MissingProperty") return "Could not evaluate clause for a rule with missing property for incoming context `" + msg + "`";
+  if (kind == "RetrievalError") return "Could not retrieve data from incoming context. Error = `" + msg + "`";
+  if (kind == "IncompatibleRetrievalError") return "Types or variable assignments have incompatible types to retrieve `" + msg + "`";
+  if (kind == "FileNotFoundError") return "The path `" + msg + "` does not exist";
+  if (kind == "FormatError") return "Formatting error when writing " + msg;
+  if (kind == "IoError") return "I/O error when reading " + msg;
+  if (kind == "RegexError") return "Regex expression parse error for rules file " + msg;
   return msg;
 }
 

@@ -55,6 +55,17 @@ def lib():
                                                   ctypes.POINTER(ValidateInput), ctypes.c_size_t, ctypes.c_int32,
                                                   ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ExternError)]
     L.cfn_guard_validate_batch_format.restype = ctypes.c_void_p
+    L.cfn_guard_validate_batch_params.argtypes = [ctypes.POINTER(ValidateInput), ctypes.c_size_t,
+                                                  ctypes.POINTER(ValidateInput), ctypes.c_size_t,
+                                                  ctypes.POINTER(ValidateInput), ctypes.c_size_t, ctypes.c_int32,
+                                                  ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ExternError)]
+    L.cfn_guard_validate_batch_params.restype = ctypes.c_void_p
+    L.gg_session_set_params.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_size_t),
+                                        ctypes.POINTER(ctypes.c_char_p), ctypes.c_size_t, ctypes.POINTER(ExternError)]
+    L.gg_session_set_params.restype = ctypes.c_int32
+    L.gg_session_report_range.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_size_t, ctypes.c_size_t,
+                                          ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ExternError)]
+    L.gg_session_report_range.restype = ctypes.c_void_p
     L.gg_session_report_format.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32),
                                            ctypes.POINTER(ExternError)]
     L.gg_session_report_format.restype = ctypes.c_void_p
@@ -218,16 +229,18 @@ def run_checks(data, data_name, rules, rules_name, verbose=False):
 OUTPUT_FORMATS = {"json": 0, "yaml": 1, "sarif": 2, "junit": 3}
 
 
-def validate_structured(rules, data, output="json"):
+def validate_structured(rules, data, output="json", params=None):
     """rules: [(name, text)], data: [(name, text)] -> (stdout text, exit_code) for
-    `cfn-guard validate --structured -o <output> -S none`.
-    Raises GuardError for an evaluation error (the CLI prints it to stderr, exit -1)."""
+    `cfn-guard validate --structured -o <output> -S none [-i <params>...]`; params: [(name, text)] in
+    the CLI's walk order.  Raises GuardError for an evaluation error (the CLI prints it to stderr, exit -1)."""
     R = (ValidateInput * max(1, len(rules)))(*[ValidateInput(_b(t), _b(n)) for n, t in rules])
     D = (ValidateInput * max(1, len(data)))(*[ValidateInput(_b(t), _b(n)) for n, t in data])
+    params = params or []
+    P = (ValidateInput * max(1, len(params)))(*[ValidateInput(_b(t), _b(n)) for n, t in params])
     code = ctypes.c_int32(0)
     err = ExternError()
-    p = lib().cfn_guard_validate_batch_format(D, len(data), R, len(rules), OUTPUT_FORMATS[output], ctypes.byref(code),
-                                              ctypes.byref(err))
+    p = lib().cfn_guard_validate_batch_params(D, len(data), R, len(rules), P, len(params), OUTPUT_FORMATS[output],
+                                              ctypes.byref(code), ctypes.byref(err))
     if err.code != 0:
         _raise(err)
     return _take_string(p), code.value
@@ -282,6 +295,18 @@ class Session:
         if err.code != 0:
             _raise(err)
 
+    def set_params(self, params):
+        """input parameters [(name, text)] merged into every document added afterwards (validate -i)"""
+        n = len(params)
+        bufs = [_b(t) for _, t in params]
+        T = (ctypes.c_char_p * max(1, n))(*bufs)
+        Ls = (ctypes.c_size_t * max(1, n))(*[len(b) for b in bufs])
+        N = (ctypes.c_char_p * max(1, n))(*[_b(x) for x, _ in params])
+        err = ExternError()
+        lib().gg_session_set_params(self.s, T, Ls, N, n, ctypes.byref(err))
+        if err.code != 0:
+            _raise(err)
+
     def add_docs_device(self, texts, names=None):
         """Parses and interns strict-JSON documents on the MI355X (empty session only).  Returns the
         loader statistics, or None when a document is outside the device subset (nothing loaded)."""
@@ -319,6 +344,16 @@ class Session:
         code = ctypes.c_int32(0)
         err = ExternError()
         p = lib().gg_session_report_format(self.s, OUTPUT_FORMATS[output], ctypes.byref(code), ctypes.byref(err))
+        if err.code != 0:
+            _raise(err)
+        return _take_string(p), code.value
+
+    def report_range(self, output="json", first=0, count=None):
+        """the structured report of documents [first, first + count) alone (a rank's shard)"""
+        code = ctypes.c_int32(0)
+        err = ExternError()
+        n = ctypes.c_size_t(-1).value if count is None else count
+        p = lib().gg_session_report_range(self.s, OUTPUT_FORMATS[output], first, n, ctypes.byref(code), ctypes.byref(err))
         if err.code != 0:
             _raise(err)
         return _take_string(p), code.value

@@ -68,25 +68,39 @@ _SEVERITY = {0: 0, 5: 1, 19: 2, -1: 3}
 _BY_SEVERITY = {v: k for k, v in _SEVERITY.items()}
 
 
-def reduce_exit_code(code, dist, device="cpu"):
+def collective_device(dist, device=None):
+    """The device a collective's tensors live on: the caller's choice, else the current GPU under
+    the nccl (RCCL) backend -- which accepts device tensors only -- and the CPU under gloo."""
+    import torch
+    if device is not None:
+        return torch.device(device)
+    if dist is not None and dist.is_initialized() and dist.get_backend() == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def reduce_exit_code(code, dist, device=None):
     """The job's exit code from every rank's (all_reduce MAX over the precedence above)."""
     import torch
     if code not in _SEVERITY:
         raise ValueError("unknown structured exit code %r" % (code,))
     if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
         return code
+    device = collective_device(dist, device)
     t = torch.tensor([_SEVERITY[code]], dtype=torch.int64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return _BY_SEVERITY[int(t.item())]
 
 
-def gather_bytes(payload, dist, device="cpu"):
+def gather_bytes(payload, dist, device=None):
     """Every rank's `payload` (bytes) in rank order on rank 0; None on the other ranks.  The byte
     counts are all-gathered (8 B per rank); then each rank sends its bytes to rank 0 alone, so a
-    rank holds only its own report and rank 0 the job's (no world-sized padded buffers)."""
+    rank holds only its own report and rank 0 the job's (no world-sized padded buffers).  Under
+    RCCL the buffers are device tensors (collective_device); under gloo host tensors."""
     import torch
     if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
         return [payload]
+    device = collective_device(dist, device)
     world, rank = dist.get_world_size(), dist.get_rank()
     n = torch.tensor([len(payload)], dtype=torch.int64, device=device)
     sizes = [torch.zeros(1, dtype=torch.int64, device=device) for _ in range(world)]
@@ -177,7 +191,7 @@ def _merge_junit(parts):
         decl, name, tests, failures, errors, time, "".join(bodies))
 
 
-def gather_report(local_text, local_code, dist, output="json", device="cpu"):
+def gather_report(local_text, local_code, dist, output="json", device=None):
     """Rank 0: (merged structured report, job exit code); other ranks: (None, job exit code)."""
     code = reduce_exit_code(local_code, dist, device)
     parts = gather_bytes(local_text.encode(), dist, device)

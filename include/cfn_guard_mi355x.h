@@ -55,6 +55,17 @@ char *cfn_guard_validate_batch(const validate_input_t *docs, size_t n_docs, cons
 char *cfn_guard_validate_batch_format(const validate_input_t *docs, size_t n_docs, const validate_input_t *rules,
                                       size_t n_rules, int32_t output_format, int32_t *exit_code, extern_err_t *err);
 
+/* cfn_guard_validate_batch_format with input parameters: `validate --structured -i <params>...`
+ * (commands/validate.rs:317-350; reporters/validate/structured.rs:51-65).  params: the parameter
+ * files in the order the CLI walks its -i arguments (files and sorted directory listings); they are
+ * merged in that order with PathAwareValue::merge (path_value.rs:889-919) and the result is merged
+ * into every data file.  A conflict between parameter files is the reference's MultipleValues (9) /
+ * IncompatibleError (11) abort; between the parameters and a data file the reference unwraps the
+ * merge and panics: code -1, message "called `Result::unwrap()` on an `Err` value: ...". */
+char *cfn_guard_validate_batch_params(const validate_input_t *docs, size_t n_docs, const validate_input_t *rules,
+                                      size_t n_rules, const validate_input_t *params, size_t n_params,
+                                      int32_t output_format, int32_t *exit_code, extern_err_t *err);
+
 /* `cfn-guard test -r <rules> -t <spec files> [-o json|yaml|junit]` (commands/test.rs,
  * reporters/test/generic.rs and structured.rs): one rules file x n_specs test-spec files
  * (YAML / JSON `Vec<TestSpec>`); output_format CFN_GUARD_OUTPUT_TEXT (the default text report),
@@ -71,10 +82,18 @@ int32_t gg_session_add_rules(gg_session *s, const char *text, const char *name, 
 /* mode 0: libyaml loader (CLI path, marks); mode 1: serde loader (FFI path) */
 int32_t gg_session_add_docs(gg_session *s, const char *const *texts, const size_t *lens, const char *const *names,
                             size_t n, int32_t mode, int32_t nthreads, extern_err_t *err);
+/* input parameters (validate -i) merged into every document added after this call; texts are
+ * loaded like the CLI's data files (libyaml loader) and merged in order; 0, or the error code */
+int32_t gg_session_set_params(gg_session *s, const char *const *texts, const size_t *lens, const char *const *names,
+                              size_t n, extern_err_t *err);
 int32_t gg_session_upload(gg_session *s, extern_err_t *err);
 int32_t gg_session_eval(gg_session *s, int32_t iters, double *ms_out, extern_err_t *err);
 char *gg_session_report(gg_session *s, int32_t *exit_code, extern_err_t *err);
 char *gg_session_report_format(gg_session *s, int32_t output_format, int32_t *exit_code, extern_err_t *err);
+/* the structured report of documents [first, first + count) alone (count SIZE_MAX: to the end): what a
+ * run over just those documents writes -- one rank's shard of a multi-GPU job */
+char *gg_session_report_range(gg_session *s, int32_t output_format, size_t first, size_t count, int32_t *exit_code,
+                              extern_err_t *err);
 int64_t gg_session_stat(gg_session *s, int32_t what);
 /* Diagnostic: save an evaluation's results (tiles, rule statuses, records) / load them into a session
  * holding the same rules files and documents (no GPU needed to render its reports). */

@@ -474,3 +474,27 @@ def from_value(value, path="", line=0, col=0) -> PV:
             mv.values[key] = from_value(e, path + "/" + key, line, col)
         return PV(MAP, path, line, col, mv)
     return PV(kind, path, line, col, payload)
+
+
+# ---------------------------------------------------------------------------
+# PathAwareValue::merge (path_value.rs:889-919), used by `validate -i` (validate.rs:317-350,
+# structured.rs:51-65)
+# ---------------------------------------------------------------------------
+def merge(this: PV, other: PV) -> PV:
+    """``self.merge(other)`` on a copy of ``this`` (the caller's value is left unchanged, as the
+    reference merges ``data.clone()``)."""
+    if this.kind == LIST and other.kind == LIST:
+        return PV(LIST, this.path, this.line, this.col, list(this.val) + list(other.val))
+    if this.kind == MAP and other.kind == MAP:
+        mv = MapValue()
+        mv.keys = list(this.val.keys)
+        mv.values = dict(this.val.values)
+        for key, value in other.val.values.items():
+            if key in mv.values:
+                raise GuardError("MultipleValues", "Key %s, already exists in map" % key)
+            mv.values[key] = value
+            # map.keys.push(String((path.extend_str(&key), key))): other's path + "/key", other's location
+            mv.keys.append(PV(STRING, other.path + "/" + key, other.line, other.col, key))
+        return PV(MAP, this.path, this.line, this.col, mv)
+    raise GuardError("IncompatibleError", "Types are not compatible for merges %s, %s"
+                     % (this.type_info(), other.type_info()))

@@ -323,10 +323,11 @@ def eval_file_report(rules_file, doc, data_name):
     return status, simplified_json_from_root(rec)
 
 
-def validate_structured(rules, data, parsed_docs=None, output="json", raise_errors=False):
-    """``cfn-guard validate --structured -o {json|yaml|sarif|junit} -S none`` over in-memory inputs.
+def validate_structured(rules, data, parsed_docs=None, output="json", raise_errors=False, params=None):
+    """``cfn-guard validate --structured -o {json|yaml|sarif|junit} -S none [-i ...]`` over in-memory inputs.
 
-    rules: list of (rules_file_name, text); data: list of (data_name, text).
+    rules: list of (rules_file_name, text); data: list of (data_name, text); params: input
+    parameter files (name, text) in the CLI's walk order (validate.rs:317-350).
     Returns (stdout_text, exit_code, stderr_text).  Evaluation errors abort the run with
     no stdout, exit code -1 (main.rs:35-42); raise_errors=True re-raises the GuardError instead
     (its kind gives the guard-ffi code, errors.rs:12-38)."""
@@ -344,6 +345,23 @@ def validate_structured(rules, data, parsed_docs=None, output="json", raise_erro
             parsed_rules.append((rf, name))
     try:
         docs = parsed_docs if parsed_docs is not None else [(n, load_document(t, n)) for n, t in data]
+        if params:
+            # validate.rs:317-350: every parameter file loaded like a data file, merged in order
+            # (`primary.merge(path_value)?`: an error aborts)
+            from .pv import merge as pv_merge, rust_debug_str
+            primary = None
+            for n, t in params:
+                pv = load_document(t, n)
+                primary = pv if primary is None else pv_merge(primary, pv)
+            # structured.rs:51-65: `data.clone().merge(file.path_value.clone()).unwrap()` -- a panic
+            merged = []
+            for n, doc in docs:
+                try:
+                    merged.append((n, pv_merge(primary, doc)))
+                except GuardError as e:
+                    raise GuardError("Panic", "called `Result::unwrap()` on an `Err` value: %s(%s)"
+                                     % (e.kind, rust_debug_str(e.msg)))
+            docs = merged
         from . import formats
         records, suites = [], []
         for dname, doc in docs:

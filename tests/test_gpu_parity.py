@@ -375,3 +375,91 @@ def test_unreachable_filter_predecessor_panics_like_the_reference():
     with pytest.raises(guard_amd.GuardError) as ei:
         guard_amd.validate_structured(rules, data)
     assert ei.value.code == -1 and ei.value.message == "internal error: entered unreachable code"
+
+
+PARAMS_DIR = os.path.join(G, "params")
+
+
+def _pfile(rel):
+    return (os.path.basename(rel), open(os.path.join(PARAMS_DIR, rel)).read())
+
+
+# guard/tests/validate.rs:421-473 (test_combinations_of_rules_data_and_input_params_files): -i
+# arguments -> the exit code; a directory argument is its sorted supported files (walk_dir)
+PARAM_CASES = [
+    (["input-parameters-dir/db_params.yaml"], 19),
+    (["input-parameters-dir/db_params.yaml", "input-parameters-dir/db_metadata.yaml"], 0),
+    (["input-parameters-dir/db_metadata.yaml", "input-parameters-dir/db_params.yaml"], 0),   # "input-parameters-dir/"
+    (["malformed-template.yaml"], -1),
+    (["blank-template.yaml"], -1),
+    (["blank-template.yaml", "input-parameters-dir/db_params.yaml"], -1),
+]
+
+
+def test_input_parameters_reference_cases():
+    """validate -i (validate.rs:317-350, structured.rs:51-65, path_value.rs:889-919): the six cases of
+    guard/tests/validate.rs:421-473 give the reference's exit codes, with byte parity vs the oracle
+    in every format and the same abort (code + message) where the run aborts"""
+    rules = [_pfile("db_param_port_rule.guard")]
+    data = [_pfile("db_resource.yaml")]
+    for files, want in PARAM_CASES:
+        params = [_pfile(f) for f in files]
+        for fmt in ("json", "yaml", "sarif", "junit"):
+            exp, ecode, err = oracle_validate(rules, data, output=fmt, params=params)
+            assert ecode == want, (files, fmt)
+            if want == -1:
+                with pytest.raises(guard_amd.GuardError) as ei:
+                    guard_amd.validate_structured(rules, data, output=fmt, params=params)
+                assert err == "Error occurred " + ei.value.message, files
+                continue
+            out, code = guard_amd.validate_structured(rules, data, output=fmt, params=params)
+            assert (code, out) == (ecode, exp), (files, fmt)
+
+
+def test_input_parameters_merge_semantics_vs_oracle():
+    """merged roots: self's (the parameters') location, self's keys then other's keys at other's
+    path + "/key" and location (path_value.rs:905-907) -- seen through root captures and R7 / Display
+    of the merged root; a repeated key in a parameter file (key block kept through the merge); list
+    roots concatenate with every element keeping its own path.  Every format, lane and wave mode."""
+    rules = [_pfile("params_keys.guard")]
+    data = [_pfile("db_resource.yaml")]
+    for files in (["input-parameters-dir/db_params.yaml", "input-parameters-dir/db_metadata.yaml"], ["dup_params.yaml"]):
+        params = [_pfile(f) for f in files]
+        for fmt in ("json", "yaml", "sarif", "junit"):
+            exp, ecode, _ = oracle_validate(rules, data, output=fmt, params=params)
+            out, code = guard_amd.validate_structured(rules, data, output=fmt, params=params)
+            assert (code, out) == (ecode, exp), (files, fmt)
+        outs = []
+        for mode in (0, 1):
+            s = guard_amd.Session()
+            s.configure(mode, 0)
+            s.add_rules(rules[0][1], rules[0][0])
+            s.set_params(params)
+            s.add_docs([data[0][1]] * 70, ["db-%d.yaml" % i for i in range(70)])
+            s.eval(1)
+            outs.append(s.report())
+            s.close()
+        assert outs[0] == outs[1]
+    lrules = [("l.guard", "this[*] > 5\nthis[3] == 1\n")]
+    ldata = [("l.yaml", "- 1\n- 2\n")]
+    lparams = [("p.yaml", "- 7\n- 3\n")]
+    exp, ecode, _ = oracle_validate(lrules, ldata, params=lparams)
+    out, code = guard_amd.validate_structured(lrules, ldata, params=lparams)
+    assert (code, out) == (ecode, exp)
+
+
+def test_input_parameters_conflicts_abort_like_the_reference():
+    """between parameter files a merge error propagates (MultipleValues 9 / IncompatibleError 11);
+    between the parameters and a data file the reference unwraps the merge and panics (code -1)"""
+    rules = [_pfile("db_param_port_rule.guard")]
+    data = [_pfile("db_resource.yaml")]
+    cases = [([("p.yaml", "Resources: {}\n")], -1),
+             ([("p.yaml", "- 1\n")], -1),
+             ([("p.yaml", "a: 1\n"), ("q.yaml", "a: 2\n")], 9),
+             ([("p.yaml", "a: 1\n"), ("q.yaml", "- 2\n")], 11)]
+    for params, code in cases:
+        _, ecode, err = oracle_validate(rules, data, params=params)
+        assert ecode == -1
+        with pytest.raises(guard_amd.GuardError) as ei:
+            guard_amd.validate_structured(rules, data, params=params)
+        assert ei.value.code == code and err == "Error occurred " + ei.value.message, params
