@@ -245,7 +245,12 @@ struct Compiler {
     if (op != OP_EQ || nt || neg || rk != RHS_LITERAL) return 0;
     const PQuery& q = queries[pc.a];
     if (q.n != 1 || parts[q.first].kind != P_KEY) return 0;
-    if (!(pc.b & LIT_BIT) || P.lit.nodes[pc.b & ~LIT_BIT].kind != K_STRING) return 0;
+    if (!(pc.b & LIT_BIT)) return 0;
+    // `<key> == '<string>'`, or `<key> == /<regex>/` with a DFA-compilable regex (the device runs the
+    // DFA over the value instead of the generic filter path; an unsupported regex must raise when it
+    // is reached, so it stays on the generic path)
+    const DNode& lit = P.lit.nodes[pc.b & ~LIT_BIT];
+    if (lit.kind != K_STRING && !(lit.kind == K_REGEX && lit.b < P.regex.size() && !P.regex[lit.b].unsupported)) return 0;
     if (C.n == 1) return cid + 1;
     for (uint32_t i = 1; i < C.n; i++) {
       const PRange2 Di = disjs[disj_refs[C.first + i]];

@@ -23,10 +23,17 @@ if PACK == "micro":
     FILES = [(k + ".guard", v) for k, v in CASES.items()]
 else:
     FILES = rulepack.rule_pack(PACK)
+corpus = None
+if PACK == "cfg5":
+    import synth  # noqa: E402
+    corpus = synth.config_corpus(ndocs, start=0)
 for name, text in FILES:
     s = guard_amd.Session()
     s.add_rules(text, name)
-    s.add_synthetic(0, ndocs, threads=16)
+    if corpus is not None:
+        s.add_docs(corpus, ["snapshot-%d.json" % i for i in range(ndocs)], threads=16)
+    else:
+        s.add_synthetic(0, ndocs, threads=16)
     s.upload()
     ms = s.eval(1)
     st = s.kernel_stats()
