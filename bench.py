@@ -153,9 +153,9 @@ def main():
     ap.add_argument("--docs", type=int, default=0, help="documents per GPU (default: 1M templates; cfg5 303031 "
                                                          "snapshots = 10M configuration items)")
     ap.add_argument("--no-e2e", action="store_true")
-    ap.add_argument("--e2e-report-docs", type=int, default=50_000,
-                    help="documents whose structured report is rendered for e2e (0: all); the report time is "
-                         "scaled to the whole job")
+    ap.add_argument("--e2e-report-docs", type=int, default=0,
+                    help="documents whose structured report is rendered for e2e (0: all, the default); a sample's "
+                         "report time is scaled to the whole job")
     ap.add_argument("--resources", type=int, default=50)
     ap.add_argument("--threads", type=int, default=0, help="host loader threads (default: CPU share)")
     ap.add_argument("--loader", choices=("host", "device"), default="host",
@@ -298,6 +298,7 @@ def main():
         rdocs = min(ndocs, args.e2e_report_docs) if args.e2e_report_docs else ndocs
         log("e2e: structured report of %d of %d documents" % (rdocs, ndocs))
         t0 = time.time()
+        os.environ.setdefault("GG_PROGRESS", "1")   # a block line per 65536 documents (a long render keeps writing)
         rep_bytes, rep_code = sess.report_bytes("json", rdocs)
         t_report_sample = time.time() - t0
         # the synthetic documents are alike: the whole report costs ndocs / rdocs times the sample
@@ -312,7 +313,7 @@ def main():
                "pcie_inclusive_value": round(ntiles / (t_upload + t_eval), 1),
                "note": "one job: host load (incl. synthetic text generation%s) + upload + one evaluation with "
                        "statuses/records fetched + structured JSON report rendered on the host and discarded "
-                       "(rendered for report_docs_rendered documents, report_s scaled to all)"
+                       "(rendered for report_docs_rendered documents; report_s scaled to all when that is fewer)"
                        % (", %.1f s of Python generation excluded" % t_gen if args.workload == "cfg5" else "")}
 
     total_units = ntiles * world * args.steps

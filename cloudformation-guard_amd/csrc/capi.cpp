@@ -993,38 +993,18 @@ int32_t status_of(const std::string& s) { return s == "PASS" ? (int32_t)ST_PASS 
 
 }  // namespace
 
-/* `cfn-guard test -r <rules> -t <spec files>`: every spec's inputs evaluated on the MI355X in one
- * batch, each test case a document whose root is its `input` subtree. */
-char* cfn_guard_test(validate_input_t rules, const validate_input_t* specs, size_t n_specs, int32_t output_format,
-                     int32_t* exit_code, extern_err_t* err) {
-  set_err(err, 0, "");
-  if (exit_code) *exit_code = 0;
-  if (output_format != OUT_TEXT && output_format != OUT_JSON && output_format != OUT_YAML && output_format != OUT_JUNIT) {
-    set_err(err, 18, "IllegalArguments: test reports are text, json, yaml or junit");
-    if (exit_code) *exit_code = -1;
-    return nullptr;
-  }
-  try {
-    std::string why;
-    if (!ensure_device(why)) { set_err(err, -1, why); if (exit_code) *exit_code = -1; return nullptr; }
-    gg_session s;
-    const std::string rname = rules.file_name ? rules.file_name : "";
-    std::string perr;
-    const char* rtext = rules.content ? rules.content : "";
-    if (!add_rules(&s, rtext, rname, perr)) {
-      // test.rs:300-303 (text): exit code 1; 338-350 (structured TestResult::Err): the report, and
-      // handle_structured_single_report's exit_code stays SUCCESS_STATUS_CODE on that branch
-      if (exit_code) *exit_code = output_format == OUT_TEXT ? 1 : 0;
-      if (output_format == OUT_TEXT) return dup_str("Parse Error on ruleset file " + error_display("ParseError", perr) + "\n");
-      std::vector<TestSpecFile> ef(1);
-      ef[0].error = error_display("ParseError", perr);
-      int32_t code = 0;
-      std::string out = test_report(output_format, rname, ef, code);
-      return dup_str(out);
-    }
-    // a rules file with no rules (Ok(None)): nothing is written, exit code 0 (test.rs:315, 366)
-    if (s.progs.empty()) return dup_str("");
-    std::vector<TestSpecFile> files(n_specs);
+namespace {
+// One rules file's `cfn-guard test` run on the MI355X (StructuredTestReporter::evaluate /
+// GenericReporter::report, reporters/test/*.rs): every spec's test cases in one batch, each test
+// case a document whose root is its `input` subtree.  Returns 1 with the spec files' results, 2 for
+// a rules file with no rules (Ok(None)), 3 for an unparsable one (perr), 0 for an aborting error (err set).
+int run_test_file(const std::string& rname, const char* rtext, const validate_input_t* specs, size_t n_specs,
+                  std::vector<TestSpecFile>& files, std::string& perr, extern_err_t* err) {
+  gg_session s;
+  if (!add_rules(&s, rtext, rname, perr)) return 3;
+  if (s.progs.empty()) return 2;
+  auto body = [&]() -> bool {
+    files.assign(n_specs, TestSpecFile());
     std::vector<std::vector<SpecCase>> cases(n_specs);
     std::vector<std::pair<size_t, size_t>> tile_of;   // (spec, case) of each evaluated document
     DocBatch& D = s.docs;
@@ -1068,8 +1048,7 @@ char* cfn_guard_test(validate_input_t rules, const validate_input_t* specs, size
           ReportError re;
           tile_error(D, (uint32_t)d, *P, to, re);
           set_err(err, ffi_code(re.kind), error_display(re.kind, re.msg));
-          if (exit_code) *exit_code = -1;
-          return nullptr;
+          return false;
         }
         // get_by_rules (reporters/test/mod.rs:7-18): top-level rule records grouped by name
         std::vector<std::string> order;
@@ -1088,8 +1067,7 @@ char* cfn_guard_test(validate_input_t rules, const validate_input_t* specs, size
             rr.expected = status_of(it->second);
             if (rr.expected < 0) {
               set_err(err, 5, error_display("ParseError", "Unable to parse status " + it->second));
-              if (exit_code) *exit_code = -1;
-              return nullptr;
+              return false;
             }
             // get_status_result (reporters/test/mod.rs:20-54)
             uint32_t all_skipped = 0;
@@ -1105,10 +1083,105 @@ char* cfn_guard_test(validate_input_t rules, const validate_input_t* specs, size
       }
       files[k].cases.push_back(std::move(tc));
     }
+    return true;
+  };
+  return body() ? 1 : 0;
+}
+}  // namespace
+
+/* `cfn-guard test -r <rules> -t <spec files>` (test.rs:285-380). */
+char* cfn_guard_test(validate_input_t rules, const validate_input_t* specs, size_t n_specs, int32_t output_format,
+                     int32_t* exit_code, extern_err_t* err) {
+  set_err(err, 0, "");
+  if (exit_code) *exit_code = 0;
+  if (output_format != OUT_TEXT && output_format != OUT_JSON && output_format != OUT_YAML && output_format != OUT_JUNIT) {
+    set_err(err, 18, "IllegalArguments: test reports are text, json, yaml or junit");
+    if (exit_code) *exit_code = -1;
+    return nullptr;
+  }
+  try {
+    std::string why;
+    if (!ensure_device(why)) { set_err(err, -1, why); if (exit_code) *exit_code = -1; return nullptr; }
+    const std::string rname = rules.file_name ? rules.file_name : "";
+    std::string perr;
+    std::vector<TestSpecFile> files;
+    const int r = run_test_file(rname, rules.content ? rules.content : "", specs, n_specs, files, perr, err);
+    if (r == 0) { if (exit_code) *exit_code = -1; return nullptr; }
+    if (r == 3) {
+      // test.rs:300-303 (text): exit code 1; 338-350 (structured TestResult::Err): the report, and
+      // handle_structured_single_report's exit_code stays SUCCESS_STATUS_CODE on that branch
+      if (exit_code) *exit_code = output_format == OUT_TEXT ? 1 : 0;
+      if (output_format == OUT_TEXT) return dup_str("Parse Error on ruleset file " + error_display("ParseError", perr) + "\n");
+      std::vector<TestSpecFile> ef(1);
+      ef[0].error = error_display("ParseError", perr);
+      int32_t code = 0;
+      return dup_str(test_report(output_format, rname, ef, code));
+    }
+    // a rules file with no rules (Ok(None)): nothing is written, exit code 0 (test.rs:315, 366)
+    if (r == 2) return dup_str("");
     int32_t code = 0;
     std::string out = test_report(output_format, rname, files, code);
     if (exit_code) *exit_code = code;
     return dup_str(out);
+  } catch (std::exception& e) {
+    set_err(err, -1, e.what());
+    if (exit_code) *exit_code = -1;
+    return nullptr;
+  }
+}
+
+/* `cfn-guard test -d <dir>` (test.rs:143-165): rules file i with its spec_counts[i] spec files, which
+ * follow each other in `specs`.  Text: handle_plaintext_directory (test.rs:221-283); json / yaml /
+ * junit: handle_structured_directory_report (test.rs:383-456). */
+char* cfn_guard_test_dir(const validate_input_t* rules, size_t n_rules, const validate_input_t* specs,
+                         const size_t* spec_counts, int32_t output_format, int32_t* exit_code, extern_err_t* err) {
+  set_err(err, 0, "");
+  if (exit_code) *exit_code = 0;
+  if (output_format != OUT_TEXT && output_format != OUT_JSON && output_format != OUT_YAML && output_format != OUT_JUNIT) {
+    set_err(err, 18, "IllegalArguments: test reports are text, json, yaml or junit");
+    if (exit_code) *exit_code = -1;
+    return nullptr;
+  }
+  try {
+    std::string why;
+    if (!ensure_device(why)) { set_err(err, -1, why); if (exit_code) *exit_code = -1; return nullptr; }
+    std::string text;
+    std::vector<TestResultIn> results;
+    int32_t code = 0;
+    size_t at = 0;
+    for (size_t i = 0; i < n_rules; i++) {
+      const std::string rname = rules[i].file_name ? rules[i].file_name : "";
+      const size_t ns = spec_counts ? spec_counts[i] : 0;
+      const validate_input_t* sp = specs + at;
+      at += ns;
+      if (!ns) {
+        // structured: skipped silently (test.rs:395-397); text: a notice (:229-237)
+        if (output_format == OUT_TEXT) text += "Guard File " + rname + " did not have any tests associated, skipping.\n---\n";
+        continue;
+      }
+      if (output_format == OUT_TEXT) text += "Testing Guard File " + rname + "\n";
+      std::string perr;
+      TestResultIn tr;
+      tr.rules_name = rname;
+      const int r = run_test_file(rname, rules[i].content ? rules[i].content : "", sp, ns, tr.files, perr, err);
+      if (r == 0) { if (exit_code) *exit_code = -1; return nullptr; }
+      if (output_format == OUT_TEXT) {
+        if (r == 3) { text += "Parse Error on ruleset file " + error_display("ParseError", perr) + "\n"; code = 7; }
+        else if (r == 1) {
+          int32_t c = 0;
+          text += test_report(OUT_TEXT, rname, tr.files, c);
+          if (code == 0) code = c;
+        }
+        text += "---\n";
+        continue;
+      }
+      if (r == 2) continue;   // Ok(None): no TestResult
+      if (r == 3) tr.parse_error = error_display("ParseError", perr);
+      results.push_back(std::move(tr));
+    }
+    if (output_format != OUT_TEXT) text = test_report_list(output_format, results, code, false);
+    if (exit_code) *exit_code = code;
+    return dup_str(text);
   } catch (std::exception& e) {
     set_err(err, -1, e.what());
     if (exit_code) *exit_code = -1;
@@ -1190,15 +1263,15 @@ int64_t gg_session_report_bytes(gg_session* s, int32_t output_format, size_t max
     int64_t bytes = 0;
     std::string out;
     size_t json_parts = 0;   // JSON: the whole report is "[\n" + every block's parts joined by ",\n" + "\n]"
+    std::vector<TextBuf> parts;   // reused across blocks, as a writer streaming to a file reuses its buffers
     for (size_t d0 = 0; d0 < nd; d0 += kBlock) {
       const size_t n = std::min(kBlock, nd - d0);
       ReportError re;
       bool ok;
       if (output_format == OUT_JSON) {
-        std::vector<TextBuf> parts;
         ok = report_batch_json_parts(s->docs, progs, d0, n, tile, report_threads(), parts, re);
         for (auto& p : parts) bytes += (int64_t)p.size();
-        json_parts += parts.size();
+        json_parts += json_parts_count(parts);
       } else {
         ok = report_batch(s->docs, progs, d0, n, tile, output_format, report_threads(), out, re);
         bytes += (int64_t)out.size();
@@ -1254,10 +1327,12 @@ int32_t gg_session_add_docs(gg_session* s, const char* const* texts, const size_
   const DocBatch* params = s->params.get();
   auto work = [&](int t) {
     size_t lo = n * t / nthreads, hi = n * (t + 1) / nthreads;
+    DocBatch B;   // thread-local while it grows (no shared cache lines with the neighbours' headers)
     for (size_t i = lo; i < hi; i++) {
-      if (!load_document(parts[t], texts[i], lens[i], names ? names[i] : std::string(), (LoadMode)mode, errs[t]) ||
-          !merge_params_last(parts[t], params, errs[t])) { failed[t] = (int)i; return; }
+      if (!load_document(B, texts[i], lens[i], names ? names[i] : std::string(), (LoadMode)mode, errs[t]) ||
+          !merge_params_last(B, params, errs[t])) { failed[t] = (int)i; break; }
     }
+    parts[t] = std::move(B);
   };
   try {
     parallel_run((size_t)nthreads, work);
@@ -1421,7 +1496,8 @@ int32_t gg_session_add_synthetic(gg_session* s, uint64_t first, size_t n, int32_
     auto work = [&](int t) {
       size_t lo = n * t / nthreads, hi = n * (t + 1) / nthreads;
       std::string text;
-      DocBatch& B = parts[t];
+      DocBatch B;   // thread-local while it grows (no shared cache lines with the neighbours' headers)
+      struct Back { DocBatch& b; DocBatch& slot; ~Back() { slot = std::move(b); } } back{B, parts[t]};
       for (size_t i = lo; i < hi; i++) {
         cfn_synth_doc(first + i, n_resources, text);
         if (!load_document(B, text.data(), text.size(), "synthetic-" + std::to_string(first + i) + ".json",

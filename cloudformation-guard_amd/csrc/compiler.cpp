@@ -216,22 +216,70 @@ struct Compiler {
       for (uint32_t j = 0; j < n.count; j++) if (lit_has_regex(n.a + j)) return true;
     return false;
   }
-  // access clause over plain navigation steps with no EMPTY (raises on scalars) and no regex or
-  // query/function operand: its evaluation can only produce statuses and records
-  bool error_free_clause(uint32_t cid) const {
+  // A literal whose regexes (if any) all compile to DFAs: comparing against it cannot raise.
+  bool lit_dfa_only(uint32_t ref) const {
+    const DNode& n = P.lit.nodes[ref & ~LIT_BIT];
+    if (n.kind == K_REGEX) return n.b < P.regex.size() && !P.regex[n.b].unsupported;
+    if (n.kind == K_LIST || n.kind == K_MAP)
+      for (uint32_t j = 0; j < n.count; j++) if (!lit_dfa_only(n.a + j)) return false;
+    return true;
+  }
+  // `%v` whose resolution cannot raise: defined by root-block lets only (no block let or rule
+  // parameter anywhere shares the name, so every scope chain reaches the root's), every one of them
+  // a literal or a query that cannot raise.  A capture-only name does not qualify (MissingVariable
+  // when nothing was captured).
+  bool safe_root_var(uint32_t var, int depth) const {
+    bool defined = false;
+    for (size_t b = 0; b < blocks.size(); b++)
+      for (uint32_t i = 0; i < blocks[b].nlets; i++) {
+        const PLet& l = lets[blocks[b].first_let + i];
+        if (l.var != var) continue;
+        if (b != P.hdr.root_block) return false;
+        if (l.kind == L_FUNC) return false;
+        if (l.kind == L_LITERAL && !lit_dfa_only(l.id)) return false;
+        if (l.kind == L_QUERY && !error_free_query(l.id, depth)) return false;
+        defined = true;
+      }
+    for (uint32_t v : param_vars) if (v == var) return false;
+    return defined;
+  }
+  // a query of navigation steps, root-variable heads and filters that cannot raise (no `%var` key
+  // interpolation, no named capture -- captures change the root scope)
+  bool error_free_query(uint32_t qid, int depth) const {
+    if (depth > 4) return false;
+    const PQuery& q = queries[qid];
+    for (uint32_t i = 0; i < q.n; i++) {
+      const PPart& pp = parts[q.first + i];
+      bool ok = pp.kind == P_THIS || pp.kind == P_KEY || pp.kind == P_KEY_INDEX || pp.kind == P_INDEX ||
+                ((pp.kind == P_ALL_VALUES || pp.kind == P_ALL_INDICES) && pp.a == NONE);
+      if (!ok && i == 0 && pp.kind == P_VAR_HEAD) ok = safe_root_var(pp.a, depth + 1);
+      if (!ok && pp.kind == P_FILTER && pp.b == NONE) ok = error_free_conj(pp.a, depth + 1);
+      if (!ok) return false;
+    }
+    return true;
+  }
+  bool error_free_conj(uint32_t cj, int depth) const {
+    if (depth > 4) return false;
+    const PRange2 C = conjs[cj];
+    for (uint32_t i = 0; i < C.n; i++) {
+      const PRange2 Di = disjs[disj_refs[C.first + i]];
+      for (uint32_t j = 0; j < Di.n; j++) if (!error_free_clause(clause_refs[Di.first + j], depth)) return false;
+    }
+    return true;
+  }
+  // access clause with no EMPTY (raises on scalars), whose operands are literals with DFA-compilable
+  // regexes or queries that cannot raise: its evaluation can only produce statuses and records
+  bool error_free_clause(uint32_t cid, int depth = 0) const {
     const PClause& pc = clauses[cid];
     if (pc.kind != C_ACCESS) return false;
     uint32_t op = pc.flags & 15u, rk = (pc.flags >> 8) & 15u;
     if (op == OP_EMPTY) return false;
-    if (op < OP_EXISTS && (rk != RHS_LITERAL || !(pc.b & LIT_BIT) || lit_has_regex(pc.b))) return false;
-    const PQuery& q = queries[pc.a];
-    for (uint32_t i = 0; i < q.n; i++) {
-      const PPart& pp = parts[q.first + i];
-      bool plain = pp.kind == P_THIS || pp.kind == P_KEY || pp.kind == P_KEY_INDEX || pp.kind == P_INDEX ||
-                   ((pp.kind == P_ALL_VALUES || pp.kind == P_ALL_INDICES) && pp.a == NONE);
-      if (!plain) return false;
+    if (op < OP_EXISTS) {
+      if (rk == RHS_LITERAL) { if (!(pc.b & LIT_BIT) || !lit_dfa_only(pc.b)) return false; }
+      else if (rk == RHS_QUERY) { if (!error_free_query(pc.b, depth + 1)) return false; }
+      else return false;
     }
-    return true;
+    return error_free_query(pc.a, depth + 1);
   }
   uint32_t fast_filter_clause(uint32_t cj) {
     const PRange2 C = conjs[cj];
@@ -290,7 +338,7 @@ struct Compiler {
         case QueryPart::AllIndices: pp.kind = P_ALL_INDICES; pp.a = qp.has_name ? var(qp.key) : NONE; break;
         case QueryPart::Filter:
           pp.kind = P_FILTER; pp.a = conj(*qp.filter); pp.b = qp.has_name ? var(qp.key) : NONE;
-          pp.c = fast_filter_clause(pp.a);
+          pp.c = 0;   // fast_filter_clause, once the whole file is compiled (assemble: lets seen)
           break;
         case QueryPart::MapKeyFilter: {
           // MapKeyFilterClause (exprs.rs:183-187): rhs literal | query (rooted at the map) | function
@@ -539,6 +587,8 @@ struct Compiler {
   }
 
   void assemble() {
+    for (auto& pp : parts)
+      if (pp.kind == P_FILTER) pp.c = fast_filter_clause(pp.a);
     mark_root_vars();
     std::vector<uint32_t> blob(sizeof(ProgHeader) / 4 + 2, 0);
     ProgHeader& h = P.hdr;

@@ -8,6 +8,8 @@
 // The YAML event stream comes from libyaml 0.2.5 (the reference links unsafe-libyaml 0.2.11,
 // a transpile of the same C library).
 #pragma once
+#include <sys/mman.h>
+
 #include <memory>
 #include <new>
 #include <string>
@@ -18,6 +20,20 @@
 
 namespace gg {
 
+// Large host buffers (arena columns: tens of GB at 1M templates; report text: ~150 KB per template)
+// are fresh memory the first time they are written, and first-touch page faults on 4 KB pages
+// serialise in the kernel: on the MI355X box 16 threads fault fresh memory in at ~15 GB/s, against
+// ~200 GB/s with transparent huge pages (tools/prof/fault_bench.c; THP is in `madvise` mode there).
+// Buffers from kHugeMin up are mmap'd and marked MADV_HUGEPAGE before anything touches them.
+constexpr size_t kHugeMin = 4u << 20;
+inline void* huge_alloc(size_t bytes) {
+  void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  if (p == MAP_FAILED) throw std::bad_alloc();
+  madvise(p, bytes, MADV_HUGEPAGE);
+  return p;
+}
+inline void huge_free(void* p, size_t bytes) { if (p) munmap(p, bytes); }
+
 // Allocator whose value-less construct() default-initialises: resize() of the arena columns (trivial
 // element types, every element written right after) skips the zero fill.  At 1M templates the
 // columns are ~29 GB, so zero-filling them before the copy doubled the loader's memory traffic.
@@ -27,6 +43,15 @@ struct default_init_allocator : std::allocator<T> {
   using std::allocator<T>::allocator;
   template <class U> void construct(U* p) noexcept { ::new ((void*)p) U; }
   template <class U, class... A> void construct(U* p, A&&... a) { ::new ((void*)p) U(std::forward<A>(a)...); }
+  // huge-page backed from kHugeMin bytes up (see huge_alloc)
+  T* allocate(size_t n) {
+    const size_t b = n * sizeof(T);
+    return b >= kHugeMin ? (T*)huge_alloc(b) : std::allocator<T>::allocate(n);
+  }
+  void deallocate(T* p, size_t n) {
+    const size_t b = n * sizeof(T);
+    if (b >= kHugeMin) huge_free(p, b); else std::allocator<T>::deallocate(p, n);
+  }
 };
 template <class T>
 using column = std::vector<T, default_init_allocator<T>>;

@@ -1502,15 +1502,20 @@ bool report_batch_json_parts(const DocBatch& docs, const std::vector<const Progr
                              std::vector<TextBuf>& parts, ReportError& err) {
   const size_t nf = progs.size();
   const size_t T = std::max<size_t>(1, std::min<size_t>(nthreads, (ndocs + 255) / 256));
-  parts.clear();
+  // the callers' part buffers are reused (a block loop keeps their pages: no fresh-memory faults)
   parts.resize(T);
+  for (auto& p : parts) p.clear();
   std::vector<ReportError> errs(T);
   std::vector<size_t> err_doc(T, SIZE_MAX);
   auto work = [&](size_t t) {
     const size_t d0 = first + ndocs * t / T, d1 = first + ndocs * (t + 1) / T;
     std::vector<TileResult> trs(nf);
     std::vector<const TileResult*> tp(nf);
-    TextBuf& o = parts[t];
+    // the part is written through a thread-local TextBuf and handed back at the end: the parts'
+    // headers sit side by side in `parts`, and a length update per append on a shared cache line
+    // made the writers slow each other down (16 threads ran at 2.4x one, tools/gpu_writer_scaling.sh)
+    TextBuf o(std::move(parts[t]));
+    struct Back { TextBuf& o; TextBuf& slot; ~Back() { slot = std::move(o); } } back{o, parts[t]};
     for (size_t d = d0; d < d1; d++) {
       for (size_t f = 0; f < nf; f++) { trs[f] = tile(d, f); tp[f] = &trs[f]; }
       if (d > d0) o += ",\n";
@@ -1523,15 +1528,20 @@ bool report_batch_json_parts(const DocBatch& docs, const std::vector<const Progr
   };
   parallel_run(T, work);
   for (size_t t = 0; t < T; t++) if (err_doc[t] != SIZE_MAX) { err = errs[t]; return false; }
-  std::vector<TextBuf> kept;
-  for (auto& p : parts) if (!p.empty()) kept.push_back(std::move(p));
-  parts.swap(kept);
   return true;
 }
 
+// parts may be empty (a thread with no documents): they contribute nothing
+size_t json_parts_count(const std::vector<TextBuf>& parts) {
+  size_t k = 0;
+  for (auto& p : parts) if (!p.empty()) k++;
+  return k;
+}
+
 size_t json_parts_size(const std::vector<TextBuf>& parts) {
-  if (parts.empty()) return 2;   // "[]"
-  size_t n = 4 + 2 * (parts.size() - 1);   // "[\n" ... "\n]", ",\n" between parts
+  const size_t k = json_parts_count(parts);
+  if (!k) return 2;   // "[]"
+  size_t n = 4 + 2 * (k - 1);   // "[\n" ... "\n]", ",\n" between parts
   for (auto& p : parts) n += p.size();
   return n;
 }
@@ -1540,17 +1550,24 @@ char* json_parts_join(const std::vector<TextBuf>& parts) {
   const size_t n = json_parts_size(parts);
   char* buf = (char*)malloc(n + 1);
   if (!buf) throw std::bad_alloc();
-  if (parts.empty()) { memcpy(buf, "[]", 3); return buf; }
-  std::vector<size_t> off(parts.size());
+  std::vector<const TextBuf*> ne;
+  for (auto& p : parts) if (!p.empty()) ne.push_back(&p);
+  if (ne.empty()) { memcpy(buf, "[]", 3); return buf; }
+  // a large result is one mmap'd chunk of its own: huge pages before the copy first-touches it
+  if (n >= kHugeMin) {
+    const uintptr_t a = ((uintptr_t)buf + (2u << 20) - 1) & ~(uintptr_t)((2u << 20) - 1);
+    if (a < (uintptr_t)buf + n) madvise((void*)a, (uintptr_t)buf + n - a, MADV_HUGEPAGE);
+  }
+  std::vector<size_t> off(ne.size());
   size_t o = 2;
-  for (size_t k = 0; k < parts.size(); k++) { off[k] = o; o += parts[k].size() + 2; }
+  for (size_t k = 0; k < ne.size(); k++) { off[k] = o; o += ne[k]->size() + 2; }
   memcpy(buf, "[\n", 2);
   // each part (and the separator after it) copied by its own thread: one pass over the output
   auto copy = [&](size_t k) {
-    memcpy(buf + off[k], parts[k].data(), parts[k].size());
-    memcpy(buf + off[k] + parts[k].size(), k + 1 < parts.size() ? ",\n" : "\n]", 2);
+    memcpy(buf + off[k], ne[k]->data(), ne[k]->size());
+    memcpy(buf + off[k] + ne[k]->size(), k + 1 < ne.size() ? ",\n" : "\n]", 2);
   };
-  parallel_run(parts.size(), copy);
+  parallel_run(ne.size(), copy);
   buf[n] = 0;
   return buf;
 }
@@ -1639,30 +1656,46 @@ std::string test_report(int32_t fmt, const std::string& rules_name, const std::v
     return out;
   }
   // StructuredTestReporter (reporters/test/structured.rs) + handle_structured_single_report (test.rs:326-380)
-  for (auto& f : files) {
-    if (f.error.empty()) continue;
-    exit_code = 1;
-    if (fmt == OUT_JUNIT) {
-      const std::string rn = xml_escape(rules_name);
-      return "<?xml version=\"1.0\" encoding=\"UTF-8\"?>\n<testsuites name=\"cfn-guard test report\" tests=\"1\" failures=\"0\" "
-             "errors=\"1\" time=\"0\">\n    <testsuite name=\"" + rn + "\" errors=\"1\" failures=\"0\" time=\"0\">\n"
-             "        <testcase name=\"" + rn + "\" time=\"0\" status=\"error\">\n            <error>" + xml_escape(f.error) +
-             "</error>\n        </testcase>\n    </testsuite>\n</testsuites>\n";
-    }
-    J e = J::obj(); e.add("rule_file", J::str(rules_name)); e.add("error", J::str(f.error));
-    if (fmt == OUT_YAML) { YamlOut y; y.document(e); return y.buf; }
-    std::string out; pretty(e, 0, out); return out;
+  TestResultIn one;
+  one.rules_name = rules_name;
+  one.files = files;
+  return test_report_list(fmt, std::vector<TestResultIn>{one}, exit_code, true);
+}
+
+namespace {
+// one TestResult (reporters/test/structured.rs:33-67): Ok {rule_file, test_cases} or Err {rule_file,
+// error}; its exit code, its serde object and its JUnit suite (build_test_suite, :69-104)
+J test_result(const TestResultIn& in, int32_t& code, std::string& suite, size_t& tests, size_t& failures, size_t& errors) {
+  static const char* kStatus[] = {"PASS", "FAIL", "SKIP"};
+  auto statuses = [&](const std::vector<uint32_t>& v) {
+    std::string o;
+    for (size_t i = 0; i < v.size(); i++) o += (i ? ", " : "") + std::string(kStatus[v[i]]);
+    return o;
+  };
+  code = 0;
+  const std::string rn = xml_escape(in.rules_name);
+  std::string error = in.parse_error;
+  if (error.empty())
+    for (auto& f : in.files) if (!f.error.empty()) { error = f.error; break; }   // evaluate() returns at the first
+  if (!error.empty()) {
+    code = 1;
+    suite = "    <testsuite name=\"" + rn + "\" errors=\"1\" failures=\"0\" time=\"0\">\n"
+            "        <testcase name=\"" + rn + "\" time=\"0\" status=\"error\">\n            <error>" + xml_escape(error) +
+            "</error>\n        </testcase>\n    </testsuite>\n";
+    tests += 1; errors += 1;
+    J e = J::obj(); e.add("rule_file", J::str(in.rules_name)); e.add("error", J::str(error));
+    return e;
   }
   J cases = J::arr();
   std::string junit;
-  size_t njunit = 0, failures = 0;
-  for (auto& f : files) {
+  size_t nfail = 0;
+  for (auto& f : in.files) {
     for (auto& tc : f.cases) {
       J passed = J::arr(), failed = J::arr(), skipped = J::arr();
       std::string jp, jf;
       const std::string tid = xml_escape(tc.has_name ? tc.name : std::string());
       for (auto& r : tc.rules) {
-        if (r.expected < 0) { J s = J::obj(); s.add("name", J::str(r.rule)); skipped.push(std::move(s)); continue; }
+        if (r.expected < 0) { J sk = J::obj(); sk.add("name", J::str(r.rule)); skipped.push(std::move(sk)); continue; }
         if (r.matched >= 0) {
           J p = J::obj(); p.add("name", J::str(r.rule)); p.add("evaluated", J::str(kStatus[r.matched]));
           passed.push(std::move(p));
@@ -1675,11 +1708,11 @@ std::string test_report(int32_t fmt, const std::string& rules_name, const std::v
           jf += "        <testcase id=\"" + tid + "\" name=\"" + xml_escape(r.rule) + "\" time=\"0\">\n            <failure>" +
                 xml_escape(std::string("Expected = ") + kStatus[r.expected] + ", Evaluated = [" + statuses(r.evaluated) + "]") +
                 "</failure>\n        </testcase>\n";
-          failures++;
+          nfail++;
         }
-        njunit++;
+        tests++;
       }
-      if (!failed.a.empty()) exit_code = 7;
+      if (!failed.a.empty()) code = 7;
       junit += jp + jf;   // build_junit_test_cases: passed rules, then failed rules
       J c = J::obj();
       c.add("name", J::str(tc.has_name ? tc.name : std::string()));
@@ -1689,16 +1722,45 @@ std::string test_report(int32_t fmt, const std::string& rules_name, const std::v
       cases.push(std::move(c));
     }
   }
-  if (fmt == OUT_JUNIT)
-    return "<?xml version=\"1.0\" encoding=\"UTF-8\"?>\n<testsuites name=\"cfn-guard test report\" tests=\"" + std::to_string(njunit) +
-           "\" failures=\"" + std::to_string(failures) + "\" errors=\"0\" time=\"0\">\n    <testsuite name=\"" + xml_escape(rules_name) +
-           "\" errors=\"0\" failures=\"" + std::to_string(failures) + "\" time=\"0\">\n" + junit + "    </testsuite>\n</testsuites>\n";
+  failures += nfail;
+  suite = "    <testsuite name=\"" + rn + "\" errors=\"0\" failures=\"" + std::to_string(nfail) + "\" time=\"0\">\n" + junit +
+          "    </testsuite>\n";
   J res = J::obj();
-  res.add("rule_file", J::str(rules_name));
+  res.add("rule_file", J::str(in.rules_name));
   res.add("test_cases", std::move(cases));
-  if (fmt == OUT_YAML) { YamlOut y; y.document(res); return y.buf; }
+  return res;
+}
+}  // namespace
+
+// `cfn-guard test` structured output of one TestResult (single: handle_structured_single_report,
+// test.rs:326-380) or of a Vec<TestResult> (handle_structured_directory_report, test.rs:383-456);
+// exit code: the TestResults' codes folded with get_exit_code (test.rs:459-472)
+std::string test_report_list(int32_t fmt, const std::vector<TestResultIn>& results, int32_t& exit_code, bool single) {
+  exit_code = 0;
+  J arr = J::arr();
+  std::string suites;
+  size_t tests = 0, failures = 0, errors = 0;
+  for (auto& r : results) {
+    int32_t code = 0;
+    std::string suite;
+    J o = test_result(r, code, suite, tests, failures, errors);
+    suites += suite;
+    // get_exit_code: SUCCESS takes the result's; TEST_ERROR stays; TEST_FAILURE yields to TEST_ERROR
+    if (exit_code == 0) exit_code = code;
+    else if (exit_code == 7 && code == 1) exit_code = 1;
+    arr.push(std::move(o));
+  }
+  if (fmt == OUT_JUNIT)
+    return "<?xml version=\"1.0\" encoding=\"UTF-8\"?>\n<testsuites name=\"cfn-guard test report\" tests=\"" + std::to_string(tests) +
+           "\" failures=\"" + std::to_string(failures) + "\" errors=\"" + std::to_string(errors) + "\" time=\"0\">\n" + suites +
+           "</testsuites>\n";
+  if (fmt == OUT_YAML) {
+    YamlOut y;
+    if (single) y.document(arr.a[0]); else y.document(arr);
+    return y.buf;
+  }
   std::string out;
-  pretty(res, 0, out);
+  pretty(single ? arr.a[0] : arr, 0, out);
   return out;
 }
 

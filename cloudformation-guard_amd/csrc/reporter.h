@@ -102,6 +102,14 @@ struct TestSpecFile {
 };
 std::string test_report(int32_t fmt, const std::string& rules_name, const std::vector<TestSpecFile>& files,
                         int32_t& exit_code);
+// one rules file's TestResult: its spec files' results, or parse_error (the rules file did not parse)
+struct TestResultIn {
+  std::string rules_name;
+  std::vector<TestSpecFile> files;
+  std::string parse_error;
+};
+// structured (json / yaml / junit) report of one TestResult (single) or of a Vec<TestResult>
+std::string test_report_list(int32_t fmt, const std::vector<TestResultIn>& results, int32_t& exit_code, bool single);
 
 class ReportWriter {
  public:
@@ -140,13 +148,34 @@ struct TextBuf {
   TextBuf& operator=(const TextBuf&) = delete;
   TextBuf(TextBuf&& o) noexcept : p(o.p), n(o.n), cap(o.cap) { o.p = nullptr; o.n = o.cap = 0; }
   TextBuf& operator=(TextBuf&& o) noexcept { std::swap(p, o.p); std::swap(n, o.n); std::swap(cap, o.cap); return *this; }
-  ~TextBuf() { free(p); }
+  ~TextBuf() { release(); }
+  // storage: malloc below kHugeMin, then huge-page backed mmap regions (doc_loader.h huge_alloc) grown
+  // by mremap, which moves the pages without copying them
+  void release() {
+    if (cap >= kHugeMin) huge_free(p, cap); else free(p);
+    p = nullptr; n = cap = 0;
+  }
   void reserve(size_t k) {
     if (k <= cap) return;
     size_t nc = cap * 2 > k ? cap * 2 : k;
     if (nc < 4096) nc = 4096;
-    char* q = (char*)realloc(p, nc);
-    if (!q) throw std::bad_alloc();
+    char* q;
+    if (nc < kHugeMin) {
+      q = (char*)realloc(p, nc);
+      if (!q) throw std::bad_alloc();
+    } else {
+      nc = (nc + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
+      if (cap >= kHugeMin) {
+        void* r = mremap(p, cap, nc, MREMAP_MAYMOVE);
+        if (r == MAP_FAILED) throw std::bad_alloc();
+        q = (char*)r;
+        madvise(q + cap, nc - cap, MADV_HUGEPAGE);
+      } else {
+        q = (char*)huge_alloc(nc);
+        if (n) memcpy(q, p, n);
+        free(p);
+      }
+    }
     p = q; cap = nc;
   }
   // kSlack bytes past the end are always allocated, so short copies may store whole 8 / 16-byte
@@ -200,6 +229,7 @@ bool report_batch_json_parts(const DocBatch& docs, const std::vector<const Progr
                              const std::function<TileResult(size_t doc, size_t file)>& tile, unsigned nthreads,
                              std::vector<TextBuf>& parts, ReportError& err);
 size_t json_parts_size(const std::vector<TextBuf>& parts);
+size_t json_parts_count(const std::vector<TextBuf>& parts);   // non-empty parts
 char* json_parts_join(const std::vector<TextBuf>& parts);
 
 }  // namespace gg

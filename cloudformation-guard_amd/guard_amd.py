@@ -66,6 +66,10 @@ def lib():
     L.gg_session_report_range.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_size_t, ctypes.c_size_t,
                                           ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ExternError)]
     L.gg_session_report_range.restype = ctypes.c_void_p
+    L.cfn_guard_test_dir.argtypes = [ctypes.POINTER(ValidateInput), ctypes.c_size_t, ctypes.POINTER(ValidateInput),
+                                     ctypes.POINTER(ctypes.c_size_t), ctypes.c_int32, ctypes.POINTER(ctypes.c_int32),
+                                     ctypes.POINTER(ExternError)]
+    L.cfn_guard_test_dir.restype = ctypes.c_void_p
     L.gg_session_report_format.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32),
                                            ctypes.POINTER(ExternError)]
     L.gg_session_report_format.restype = ctypes.c_void_p
@@ -256,6 +260,21 @@ def run_test(rules_text, rules_name, specs, output="text"):
     err = ExternError()
     p = lib().cfn_guard_test(ValidateInput(_b(rules_text), _b(rules_name)), S, len(specs), TEST_OUTPUT_FORMATS[output],
                              ctypes.byref(code), ctypes.byref(err))
+    if err.code != 0:
+        _raise(err)
+    return _take_string(p), code.value
+
+
+def run_test_dir(pairs, output="text"):
+    """`cfn-guard test -d` over [(rules_name, rules_text, [(spec_path, spec_text), ...]), ...] in the
+    directory's order -> (report text, exit code)."""
+    R = (ValidateInput * max(1, len(pairs)))(*[ValidateInput(_b(t), _b(n)) for n, t, _ in pairs])
+    flat = [sp for _, _, sps in pairs for sp in sps]
+    S = (ValidateInput * max(1, len(flat)))(*[ValidateInput(_b(t), _b(n)) for n, t in flat])
+    C = (ctypes.c_size_t * max(1, len(pairs)))(*[len(sps) for _, _, sps in pairs])
+    code = ctypes.c_int32(0)
+    err = ExternError()
+    p = lib().cfn_guard_test_dir(R, len(pairs), S, C, TEST_OUTPUT_FORMATS[output], ctypes.byref(code), ctypes.byref(err))
     if err.code != 0:
         _raise(err)
     return _take_string(p), code.value

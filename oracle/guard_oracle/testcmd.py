@@ -132,13 +132,15 @@ def _generic(rf, specs):
     return "".join(out), code
 
 
-def _structured(rf, rules_name, specs, output):
+def _result(rf, rules_name, specs):
+    """One TestResult (reporters/test/structured.rs:33-67): StructuredTestReporter::evaluate returns
+    Err at the first spec file that does not load.  Returns (serde object, exit code, JUnit suite)."""
     cases_out, junit_cases, failures, code = [], [], 0, SUCCESS
     for path, text in specs:
         try:
             cases = _load_specs(text, path)
         except GuardError as e:
-            return _structured_error(rules_name, e.display(), output)
+            return _err_result(rules_name, e.display())
         for name, inp, expected in cases:
             exp = dict(expected)
             by = _by_rules(rf, inp)
@@ -163,36 +165,102 @@ def _structured(rf, rules_name, specs, output):
                 code = TEST_FAILURE
             cases_out.append(OMap([("name", tname), ("passed_rules", passed), ("failed_rules", failed),
                                    ("skipped_rules", skipped)]))
-    result = OMap([("rule_file", rules_name), ("test_cases", cases_out)])
-    if output == "json":
-        return to_json_pretty(result), code
-    if output == "yaml":
-        return to_yaml(result), code
-    lines = ['<?xml version="1.0" encoding="UTF-8"?>',
-             '<testsuites name="cfn-guard test report" tests="%d" failures="%d" errors="0" time="0">' % (len(junit_cases), failures),
-             '    <testsuite name="%s" errors="0" failures="%d" time="0">' % (_xml_escape(rules_name), failures)]
+    suite = ['    <testsuite name="%s" errors="0" failures="%d" time="0">' % (_xml_escape(rules_name), failures)]
     for tid, rname, msg in junit_cases:
         if msg is None:
-            lines.append('        <testcase id="%s" name="%s" time="0" status="pass"/>' % (_xml_escape(tid), _xml_escape(rname)))
+            suite.append('        <testcase id="%s" name="%s" time="0" status="pass"/>' % (_xml_escape(tid), _xml_escape(rname)))
         else:
-            lines.append('        <testcase id="%s" name="%s" time="0">' % (_xml_escape(tid), _xml_escape(rname)))
-            lines.append('            <failure>%s</failure>' % _xml_escape(msg))
-            lines.append('        </testcase>')
-    lines += ['    </testsuite>', '</testsuites>']
-    return "\n".join(lines) + "\n", code
+            suite.append('        <testcase id="%s" name="%s" time="0">' % (_xml_escape(tid), _xml_escape(rname)))
+            suite.append('            <failure>%s</failure>' % _xml_escape(msg))
+            suite.append('        </testcase>')
+    suite.append('    </testsuite>')
+    return OMap([("rule_file", rules_name), ("test_cases", cases_out)]), code, (suite, len(junit_cases), failures, 0)
+
+
+def _err_result(rules_name, error):
+    """TestResult::Err (build_test_suite: one error test case)"""
+    suite = ['    <testsuite name="%s" errors="1" failures="0" time="0">' % _xml_escape(rules_name),
+             '        <testcase name="%s" time="0" status="error">' % _xml_escape(rules_name),
+             '            <error>%s</error>' % _xml_escape(error),
+             '        </testcase>', '    </testsuite>']
+    return OMap([("rule_file", rules_name), ("error", error)]), TEST_ERROR, (suite, 1, 0, 1)
+
+
+def _render(results, output, single):
+    """serde_json pretty / serde_yaml of one TestResult or a Vec<TestResult>; JunitReport::from
+    (reporters/mod.rs:35-63) sums the suites' tests, failures and errors"""
+    if output == "json":
+        return to_json_pretty(results[0][0] if single else [r[0] for r in results])
+    if output == "yaml":
+        return to_yaml(results[0][0] if single else [r[0] for r in results])
+    tests = sum(r[2][1] for r in results)
+    failures = sum(r[2][2] for r in results)
+    errors = sum(r[2][3] for r in results)
+    lines = ['<?xml version="1.0" encoding="UTF-8"?>',
+             '<testsuites name="cfn-guard test report" tests="%d" failures="%d" errors="%d" time="0">' % (tests, failures, errors)]
+    for r in results:
+        lines += r[2][0]
+    lines.append('</testsuites>')
+    return "\n".join(lines) + "\n"
+
+
+def _structured(rf, rules_name, specs, output):
+    res = _result(rf, rules_name, specs)
+    return _render([res], output, True), res[1]
 
 
 def _structured_error(rules_name, error, output, code=TEST_ERROR):
     """TestResult::Err report; `code`: TEST_ERROR for a spec file that does not load (structured.rs:57-59
     get_exit_code), SUCCESS for an unparsable rules file (test.rs:338-350)"""
-    result = OMap([("rule_file", rules_name), ("error", error)])
-    if output == "json":
-        return to_json_pretty(result), code
-    if output == "yaml":
-        return to_yaml(result), code
-    return ("\n".join(['<?xml version="1.0" encoding="UTF-8"?>',
-                       '<testsuites name="cfn-guard test report" tests="1" failures="0" errors="1" time="0">',
-                       '    <testsuite name="%s" errors="1" failures="0" time="0">' % _xml_escape(rules_name),
-                       '        <testcase name="%s" time="0" status="error">' % _xml_escape(rules_name),
-                       '            <error>%s</error>' % _xml_escape(error),
-                       '        </testcase>', '    </testsuite>', '</testsuites>']) + "\n", code)
+    return _render([_err_result(rules_name, error)], output, True), code
+
+
+def _fold_code(code, test_code):
+    """get_exit_code (test.rs:459-472)"""
+    if code == SUCCESS:
+        return test_code
+    if code == TEST_ERROR:
+        return code
+    return TEST_ERROR if test_code == TEST_ERROR else TEST_FAILURE
+
+
+def run_test_dir(pairs, output="text"):
+    """``cfn-guard test -d`` (test.rs:143-165) over [(rules_name, rules_text, [(spec_path, text)])] in the
+    directory's order: handle_plaintext_directory (text, :221-283) or
+    handle_structured_directory_report (:383-456).  Returns (stdout text, exit code)."""
+    if output == "text":
+        out, code = [], SUCCESS
+        for rules_name, rules_text, specs in pairs:
+            if not specs:
+                out.append("Guard File %s did not have any tests associated, skipping.\n---\n" % rules_name)
+                continue
+            out.append("Testing Guard File %s\n" % rules_name)
+            try:
+                rf = parse_rules(rules_text, rules_name)
+            except GuardError as e:
+                out.append("Parse Error on ruleset file %s\n" % e.display())
+                code = TEST_FAILURE
+                out.append("---\n")
+                continue
+            if rf is not None:
+                text, c = _generic(rf, specs)
+                out.append(text)
+                code = c if code == SUCCESS else code
+            out.append("---\n")
+        return "".join(out), code
+    results, code = [], SUCCESS
+    for rules_name, rules_text, specs in pairs:
+        if not specs:
+            continue
+        try:
+            rf = parse_rules(rules_text, rules_name)
+        except GuardError as e:
+            results.append(_err_result(rules_name, e.display()))
+            code = TEST_ERROR
+            continue
+        if rf is None:
+            continue
+        res = _result(rf, rules_name, specs)
+        code = _fold_code(code, res[1])
+        results.append(res)
+    return _render(results, output, False), code

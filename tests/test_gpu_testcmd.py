@@ -43,3 +43,34 @@ def test_reference_example_specs_vs_oracle():
             exp = oracle_test(rtext, rname, [(spec, spec_json)], fmt)
             got = guard_amd.run_test(rtext, rname, [(spec, spec_json)], fmt)
             assert got == exp, (rname, spec, fmt)
+
+
+def test_test_command_directory_and_shorthand_goldens():
+    """cfn_guard_test_dir: guard/tests/test_command.rs:297-313 (the dir's rules files with their tests,
+    structured_directory_report_{json,yaml,junit}.out) and cfn_guard_test on :135-150 (shorthand:
+    expectations for another rule, test_data_file_with_shorthand_reference.out); exit 0"""
+    from test_oracle_golden import directory_pairs
+    for fmt in ("json", "yaml", "junit"):
+        out, code = guard_amd.run_test_dir(directory_pairs(), fmt)
+        assert code == 0 and out == open(os.path.join(T, "structured_directory_report_%s.out" % fmt)).read(), fmt
+    for sp in ("json", "yaml"):
+        spec = "s3_bucket_logging_enabled_tests." + sp
+        out, code = guard_amd.run_test(_rules(), RN, [("resources/test-command/data-dir/" + spec, open(os.path.join(T, spec)).read())])
+        assert code == 0 and out == open(os.path.join(T, "test_data_file_with_shorthand_reference.out")).read(), sp
+
+
+def test_test_command_directory_vs_oracle():
+    """directory mode in every format against the oracle, with a rules file without tests, an
+    unparsable rules file (TEST_ERROR in structured mode, TEST_FAILURE in text mode, test.rs:255-259,
+    416-423), a rules file with no rules and a failing expectation"""
+    from guard_oracle.testcmd import run_test_dir as oracle_dir
+    from test_oracle_golden import directory_pairs
+    pairs = directory_pairs()
+    spec = pairs[0][2]
+    extra = [("none.guard", "rule r { Resources exists }", []),
+             ("bad.guard", "rule r { Resources.x == << m >>\n}", spec),
+             ("empty.guard", "# nothing\n", spec),
+             ("fails.guard", "rule S3_BUCKET_LOGGING_ENABLED { Resources.* exists }", spec)]
+    for combo in (pairs, pairs + extra, extra[::-1] + pairs):
+        for fmt in ("text", "json", "yaml", "junit"):
+            assert guard_amd.run_test_dir(combo, fmt) == oracle_dir(combo, fmt), ([c[0] for c in combo], fmt)

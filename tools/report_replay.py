@@ -24,9 +24,14 @@ if mode == "save":
     print("saved", path)
 else:
     s.load_results(path)
-    t = time.time()
-    n, code = s.report_bytes(fmt)
-    dt = time.time() - t
-    print("%s: %d bytes in %.3f s = %.3f GB/s (threads %s), exit %d" % (fmt, n, dt, n / dt / 1e9,
-                                                                        os.environ.get("GG_REPORT_THREADS", "auto"), code))
+    reps = int(os.environ.get("REPS", "1"))
+    for _ in range(reps):
+        c0 = os.times()
+        t = time.time()
+        n, code = s.report_bytes(fmt)
+        dt = time.time() - t
+        c1 = os.times()
+        print("%s: %d bytes in %.3f s = %.3f GB/s (threads %s), exit %d; cpu user %.2f s sys %.2f s" % (
+            fmt, n, dt, n / dt / 1e9, os.environ.get("GG_REPORT_THREADS", "auto"), code,
+            c1.user - c0.user, c1.system - c0.system))
 s.close()
