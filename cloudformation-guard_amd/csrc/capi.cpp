@@ -999,113 +999,140 @@ namespace {
 // case a document whose root is its `input` subtree.  Returns 1 with the spec files' results, 2 for
 // a rules file with no rules (Ok(None)), 3 for an unparsable one (perr), 0 for an aborting error (err set).
 int run_test_file(const std::string& rname, const char* rtext, const validate_input_t* specs, size_t n_specs,
-                  std::vector<TestSpecFile>& files, std::string& perr, extern_err_t* err) {
+                  std::vector<TestSpecFile>& files, std::string& perr, extern_err_t* err, bool verbose = false) {
   gg_session s;
   if (!add_rules(&s, rtext, rname, perr)) return 3;
   if (s.progs.empty()) return 2;
-  auto body = [&]() -> bool {
-    files.assign(n_specs, TestSpecFile());
-    std::vector<std::vector<SpecCase>> cases(n_specs);
-    std::vector<std::pair<size_t, size_t>> tile_of;   // (spec, case) of each evaluated document
-    DocBatch& D = s.docs;
-    for (size_t k = 0; k < n_specs; k++) {
-      const char* t = specs[k].content ? specs[k].content : "";
-      const std::string path = specs[k].file_name ? specs[k].file_name : "";
-      LoadError le;
-      std::string shape;
-      const size_t at = D.ndocs();
-      bool ok = load_document(D, t, strlen(t), path, LOAD_SERDE, le);
-      if (ok && !read_spec(D, at, cases[k], shape)) { ok = false; le.msg = shape; }
-      if (!ok) {
-        files[k].error = error_display("ParseError", "Unable to process data in file " + path + ", Error " + le.msg + ",");
-        if (D.ndocs() > at) { D.roots.pop_back(); D.base.pop_back(); D.names.pop_back(); }
-        continue;
-      }
-      // the spec document itself is not evaluated: one document per test case, rooted at its input
-      const uint64_t base = D.base[at];
-      D.roots.pop_back(); D.base.pop_back(); D.names.pop_back();
-      for (size_t c = 0; c < cases[k].size(); c++) {
-        D.roots.push_back(cases[k][c].input);
-        D.base.push_back(base);
-        D.names.push_back(path);
-        tile_of.push_back({k, c});
-      }
+  if (verbose) { s.mode = 1; s.verbose = true; }   // every event recorded (the verbose wave kernel)
+  files.assign(n_specs, TestSpecFile());
+  std::vector<std::vector<SpecCase>> cases(n_specs);
+  std::vector<std::pair<size_t, size_t>> tile_of;   // (spec, case) of each evaluated document
+  DocBatch& D = s.docs;
+  for (size_t k = 0; k < n_specs; k++) {
+    const char* t = specs[k].content ? specs[k].content : "";
+    const std::string path = specs[k].file_name ? specs[k].file_name : "";
+    LoadError le;
+    std::string shape;
+    const size_t at = D.ndocs();
+    bool ok = load_document(D, t, strlen(t), path, LOAD_SERDE, le);
+    if (ok && !read_spec(D, at, cases[k], shape)) { ok = false; le.msg = shape; }
+    if (!ok) {
+      files[k].error = error_display("ParseError", "Unable to process data in file " + path + ", Error " + le.msg + ",");
+      if (D.ndocs() > at) { D.roots.pop_back(); D.base.pop_back(); D.names.pop_back(); }
+      continue;
     }
-    if (!s.progs.empty() && D.ndocs()) {
-      session_upload(&s);
-      session_run(&s, true);
+    // the spec document itself is not evaluated: one document per test case, rooted at its input,
+    // whose paths start at that input (PathAwareValue::try_from(spec.input), generic.rs:75)
+    const uint64_t base = D.base[at];
+    D.roots.pop_back(); D.base.pop_back(); D.names.pop_back();
+    for (size_t c = 0; c < cases[k].size(); c++) D.nodes[base + cases[k][c].input].parent = NONE;
+    for (size_t c = 0; c < cases[k].size(); c++) {
+      D.roots.push_back(cases[k][c].input);
+      D.base.push_back(base);
+      D.names.push_back(path);
+      tile_of.push_back({k, c});
     }
-    const Program* P = s.progs.empty() ? nullptr : &s.progs[0]->prog;
-    for (size_t d = 0; d < tile_of.size(); d++) {
-      const size_t k = tile_of[d].first, c = tile_of[d].second;
-      const SpecCase& sc = cases[k][c];
-      TestCaseResult tc;
-      tc.has_name = sc.has_name;
-      tc.name = sc.name;
-      if (P) {
-        const TileOut& to = s.tiles[d];
-        if (to.err) {   // an evaluation error aborts the command (eval_rules_file(..)?)
-          ReportError re;
-          tile_error(D, (uint32_t)d, *P, to, re);
-          set_err(err, ffi_code(re.kind), error_display(re.kind, re.msg));
-          return false;
-        }
-        // get_by_rules (reporters/test/mod.rs:7-18): top-level rule records grouped by name
-        std::vector<std::string> order;
-        std::vector<std::vector<uint32_t>> got;
-        for (uint32_t r = 0; r < P->n_rules; r++) {
-          const std::string& nm = P->rule_names[P->rule_names.size() - P->n_rules + r];
-          size_t g = std::find(order.begin(), order.end(), nm) - order.begin();
-          if (g == order.size()) { order.push_back(nm); got.emplace_back(); }
-          got[g].push_back(s.rule_status[d * s.max_top + r]);
-        }
-        for (size_t g = 0; g < order.size(); g++) {
-          TestRuleResult rr;
-          rr.rule = order[g];
-          auto it = std::find_if(sc.expected.begin(), sc.expected.end(), [&](const std::pair<std::string, std::string>& e) { return e.first == order[g]; });
-          if (it != sc.expected.end()) {
-            rr.expected = status_of(it->second);
-            if (rr.expected < 0) {
-              set_err(err, 5, error_display("ParseError", "Unable to parse status " + it->second));
-              return false;
-            }
-            // get_status_result (reporters/test/mod.rs:20-54)
-            uint32_t all_skipped = 0;
-            for (uint32_t st : got[g]) {
-              if (rr.expected == (int32_t)ST_SKIP) { if (st == ST_SKIP) all_skipped++; }
-              else if ((int32_t)st == rr.expected) { rr.matched = rr.expected; break; }
-              rr.evaluated.push_back(st);
-            }
-            if (rr.matched < 0 && rr.expected == (int32_t)ST_SKIP && all_skipped == got[g].size()) rr.matched = ST_SKIP;
+  }
+  if (!s.progs.empty() && D.ndocs()) {
+    session_upload(&s);
+    session_run(&s, true);
+  }
+  const Program* P = s.progs.empty() ? nullptr : &s.progs[0]->prog;
+  for (size_t d = 0; d < tile_of.size(); d++) {
+    const size_t k = tile_of[d].first, c = tile_of[d].second;
+    const SpecCase& sc = cases[k][c];
+    TestCaseResult tc;
+    tc.has_name = sc.has_name;
+    tc.name = sc.name;
+    if (P) {
+      const TileOut& to = s.tiles[d];
+      if (to.err) {   // an evaluation error aborts the command (eval_rules_file(..)?)
+        ReportError re;
+        tile_error(D, (uint32_t)d, *P, to, re);
+        set_err(err, ffi_code(re.kind), error_display(re.kind, re.msg));
+        return 0;
+      }
+      // get_by_rules (reporters/test/mod.rs:7-18): top-level rule records grouped by name
+      std::vector<std::string> order;
+      std::vector<std::vector<uint32_t>> got;
+      for (uint32_t r = 0; r < P->n_rules; r++) {
+        const std::string& nm = P->rule_names[P->rule_names.size() - P->n_rules + r];
+        size_t g = std::find(order.begin(), order.end(), nm) - order.begin();
+        if (g == order.size()) { order.push_back(nm); got.emplace_back(); }
+        got[g].push_back(s.rule_status[d * s.max_top + r]);
+      }
+      for (size_t g = 0; g < order.size(); g++) {
+        TestRuleResult rr;
+        rr.rule = order[g];
+        auto it = std::find_if(sc.expected.begin(), sc.expected.end(), [&](const std::pair<std::string, std::string>& e) { return e.first == order[g]; });
+        if (it != sc.expected.end()) {
+          rr.expected = status_of(it->second);
+          if (rr.expected < 0) {
+            set_err(err, 5, error_display("ParseError", "Unable to parse status " + it->second));
+            return 0;
           }
-          tc.rules.push_back(std::move(rr));
+          // get_status_result (reporters/test/mod.rs:20-54)
+          uint32_t all_skipped = 0;
+          for (uint32_t st : got[g]) {
+            if (rr.expected == (int32_t)ST_SKIP) { if (st == ST_SKIP) all_skipped++; }
+            else if ((int32_t)st == rr.expected) { rr.matched = rr.expected; break; }
+            rr.evaluated.push_back(st);
+          }
+          if (rr.matched < 0 && rr.expected == (int32_t)ST_SKIP && all_skipped == got[g].size()) rr.matched = ST_SKIP;
+        }
+        tc.rules.push_back(std::move(rr));
+      }
+      if (verbose) {
+        ReportError re;
+        TileResult tr = tile_view(s.tiles.data(), s.rule_status.data(), s.max_top, s.recs.data(), d);
+        if (!verbose_text(D, (uint32_t)d, *P, tr, "", tc.tree, re)) {   // eval_rules_file(.., None): File(, ..)
+          set_err(err, ffi_code(re.kind), error_display(re.kind, re.msg));
+          return 0;
         }
       }
-      files[k].cases.push_back(std::move(tc));
     }
-    return true;
-  };
-  return body() ? 1 : 0;
+    files[k].cases.push_back(std::move(tc));
+  }
+  return 1;
+}
+}  // namespace
+
+namespace {
+// test.rs:134-141: --verbose with a structured output, SARIF, unknown formats -> IllegalArguments
+bool test_args_ok(int32_t output_format, bool verbose, int32_t* exit_code, extern_err_t* err) {
+  if (output_format != OUT_TEXT && output_format != OUT_JSON && output_format != OUT_YAML && output_format != OUT_JUNIT) {
+    set_err(err, 18, output_format == OUT_SARIF ? "Cannot provide an output_type of SARIF, SARIF reporter is unsupported."
+                                                 : "IllegalArguments: test reports are text, json, yaml or junit");
+    if (exit_code) *exit_code = -1;
+    return false;
+  }
+  if (verbose && output_format != OUT_TEXT) {
+    set_err(err, 18, "Cannot provide an output_type of JSON, YAML, or JUnit while the verbose flag is set");
+    if (exit_code) *exit_code = -1;
+    return false;
+  }
+  return true;
 }
 }  // namespace
 
 /* `cfn-guard test -r <rules> -t <spec files>` (test.rs:285-380). */
 char* cfn_guard_test(validate_input_t rules, const validate_input_t* specs, size_t n_specs, int32_t output_format,
                      int32_t* exit_code, extern_err_t* err) {
+  return cfn_guard_test_ex(rules, specs, n_specs, output_format, false, exit_code, err);
+}
+
+char* cfn_guard_test_ex(validate_input_t rules, const validate_input_t* specs, size_t n_specs, int32_t output_format,
+                        bool verbose, int32_t* exit_code, extern_err_t* err) {
   set_err(err, 0, "");
   if (exit_code) *exit_code = 0;
-  if (output_format != OUT_TEXT && output_format != OUT_JSON && output_format != OUT_YAML && output_format != OUT_JUNIT) {
-    set_err(err, 18, "IllegalArguments: test reports are text, json, yaml or junit");
-    if (exit_code) *exit_code = -1;
-    return nullptr;
-  }
+  if (!test_args_ok(output_format, verbose, exit_code, err)) return nullptr;
   try {
     std::string why;
     if (!ensure_device(why)) { set_err(err, -1, why); if (exit_code) *exit_code = -1; return nullptr; }
     const std::string rname = rules.file_name ? rules.file_name : "";
     std::string perr;
     std::vector<TestSpecFile> files;
-    const int r = run_test_file(rname, rules.content ? rules.content : "", specs, n_specs, files, perr, err);
+    const int r = run_test_file(rname, rules.content ? rules.content : "", specs, n_specs, files, perr, err, verbose);
     if (r == 0) { if (exit_code) *exit_code = -1; return nullptr; }
     if (r == 3) {
       // test.rs:300-303 (text): exit code 1; 338-350 (structured TestResult::Err): the report, and
@@ -1134,14 +1161,11 @@ char* cfn_guard_test(validate_input_t rules, const validate_input_t* specs, size
  * follow each other in `specs`.  Text: handle_plaintext_directory (test.rs:221-283); json / yaml /
  * junit: handle_structured_directory_report (test.rs:383-456). */
 char* cfn_guard_test_dir(const validate_input_t* rules, size_t n_rules, const validate_input_t* specs,
-                         const size_t* spec_counts, int32_t output_format, int32_t* exit_code, extern_err_t* err) {
+                         const size_t* spec_counts, int32_t output_format, bool verbose, int32_t* exit_code,
+                         extern_err_t* err) {
   set_err(err, 0, "");
   if (exit_code) *exit_code = 0;
-  if (output_format != OUT_TEXT && output_format != OUT_JSON && output_format != OUT_YAML && output_format != OUT_JUNIT) {
-    set_err(err, 18, "IllegalArguments: test reports are text, json, yaml or junit");
-    if (exit_code) *exit_code = -1;
-    return nullptr;
-  }
+  if (!test_args_ok(output_format, verbose, exit_code, err)) return nullptr;
   try {
     std::string why;
     if (!ensure_device(why)) { set_err(err, -1, why); if (exit_code) *exit_code = -1; return nullptr; }
@@ -1163,7 +1187,7 @@ char* cfn_guard_test_dir(const validate_input_t* rules, size_t n_rules, const va
       std::string perr;
       TestResultIn tr;
       tr.rules_name = rname;
-      const int r = run_test_file(rname, rules[i].content ? rules[i].content : "", sp, ns, tr.files, perr, err);
+      const int r = run_test_file(rname, rules[i].content ? rules[i].content : "", sp, ns, tr.files, perr, err, verbose);
       if (r == 0) { if (exit_code) *exit_code = -1; return nullptr; }
       if (output_format == OUT_TEXT) {
         if (r == 3) { text += "Parse Error on ruleset file " + error_display("ParseError", perr) + "\n"; code = 7; }

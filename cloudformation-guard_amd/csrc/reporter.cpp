@@ -1648,6 +1648,7 @@ std::string test_report(int32_t fmt, const std::string& rules_name, const std::v
           auto& dst = r.matched >= 0 ? pass : failv;
           if (std::find(dst.begin(), dst.end(), line) == dst.end()) dst.push_back(line);   // IndexSet
         }
+        out += tc.tree;   // --verbose (generic.rs:116-118): after the rules' lines, before the report
         if (!failv.empty()) { exit_code = 7; out += "  FAIL Rules:\n"; for (auto& l : failv) out += "    " + l + "\n"; }
         if (!pass.empty()) { out += "  PASS Rules:\n"; for (auto& l : pass) out += "    " + l + "\n"; }
         out += "\n";
@@ -1777,11 +1778,25 @@ J block_check(bool alo, uint32_t st) {
 J tagged(const char* k, J v) { J o = J::obj(); o.add(k, std::move(v)); return o; }
 
 // one open event of the verbose tree
+// one line of the verbose tree as text (EventRecord Display, display.rs:314-323) and its children
+struct TNode {
+  std::string line;
+  std::vector<TNode> kids;
+};
+
 struct VNode {
   uint32_t type = 0, id = NONE;
   std::string ctx;
   J children = J::arr();
+  std::vector<TNode> tk;
 };
+
+// display_comparison (display.rs:9-11) over CmpOperator's Display (values.rs:58-79)
+std::string cmp_text(uint32_t op, bool neg) {
+  static const char* names[] = {"EQUALS", "IN", "GREATER THAN", "LESS THAN", "LESS THAN EQUALS", "GREATER THAN EQUALS",
+                                "EXISTS", "EMPTY", "IS STRING", "IS LIST", "IS MAP", "IS BOOL", "IS INT", "IS FLOAT", "IS NULL"};
+  return std::string(neg ? "not" : "") + " " + (op < 15 ? names[op] : "?");
+}
 
 struct VerboseBuilder {
   const R& r;
@@ -1794,7 +1809,16 @@ struct VerboseBuilder {
   const std::string& ctx_d(uint32_t cid) const { return r.prog.ctx[pc(cid).d]; }
   std::string when_ctx(uint32_t cid) const { return (pc(cid).flags & 1u) ? "RuleClause" : "GuardConditionClause"; }
 
-  void attach(std::string ctx, J container, J children) {
+  // text: also build the Display tree (`cfn-guard test --verbose`, validate --verbose)
+  bool text = false;
+  TNode troot;
+
+  void attach(std::string ctx, J container, J children, std::string disp = std::string(), std::vector<TNode> tk = {}) {
+    if (text) {
+      TNode t{disp + "[Context=" + ctx + "]", std::move(tk)};
+      if (stack.empty()) troot = std::move(t);
+      else stack.back().tk.push_back(std::move(t));
+    }
     J e = J::obj();
     e.add("context", J::str(ctx));
     e.add("container", std::move(container));
@@ -1802,7 +1826,40 @@ struct VerboseBuilder {
     if (stack.empty()) { root = std::move(e); have_root = true; }
     else stack.back().children.push(std::move(e));
   }
-  void leaf(std::string ctx, J check) { attach(std::move(ctx), tagged("ClauseValueCheck", std::move(check)), J::arr()); }
+  void leaf(std::string ctx, J check, std::string disp = std::string()) {
+    attach(std::move(ctx), tagged("ClauseValueCheck", std::move(check)), J::arr(), std::move(disp));
+  }
+
+  // QueryResult Display (display.rs:109-126); keep_literal as the serde form of the same record
+  std::string qr_text(const QR& q, bool keep_literal) const {
+    const uint32_t k = q.meta & 3u;
+    if (k == QR_UNRESOLVED) return "(unresolved, " + r.unresolved_display(q) + ")";
+    if (keep_literal && k == QR_LITERAL) return "literal, " + r.pav_display(q);
+    return "(resolved, " + r.pav_display(q) + ")";
+  }
+  static std::string st_text(uint32_t st) { return st == ST_PASS ? "PASS" : st == ST_FAIL ? "FAIL" : "SKIP"; }
+
+  // RecordType Display (display.rs:200-311) of a closing container
+  std::string close_disp(const Rec& rc) const {
+    const std::string st = st_text(rc.y & 0xFFu);
+    switch (rc.x) {
+      case EV_FILE: return "File(" + data_name + ", Status=" + st + ")";
+      case EV_RULE: return "Rule(" + r.prog.rule_names[rc.clause] + ", Status=" + st + ")";
+      case EV_RULE_COND: return "Rule/When(Status=" + st + ")";
+      case EV_DISJ: return "Disjunction(Status = " + st + ")";
+      case EV_GAC: return "GuardClauseBlock(Status = " + st + ")";
+      case EV_NAMED:
+        if ((rc.y & 0xFFu) == ST_PASS) return "GuardClauseValueCheck(Status=PASS)";
+        return "GuardClauseDependentRule(Rule=" + r.prog.ctx[pc(rc.clause).f] + ", Status=FAIL)";
+      case EV_BLOCK: return "GuardValueBlockCheck(Status = " + st + ")";
+      case EV_WHEN: return "WhenConditionalBlock(Status = " + st + ")";
+      case EV_WHEN_COND: return "WhenCondition(Status = " + st + ")";
+      case EV_TYPE: return "Type(" + r.prog.ctx[pc(rc.clause).f] + ", Status=" + st + ")";
+      case EV_TYPE_COND: return "TypeBlock/When Status=" + st + ")";
+      case EV_TYPE_VAL: return "TypeBlock/Block Status=" + st + ")";
+      default: return "Filter/ConjunctionsBlock(Status=" + st + ")";
+    }
+  }
 
   // eval_conjunction_clauses' context: format!("{}#disjunction", type_name::<T>()) (eval.rs:1980), T
   // the clause type the enclosing container evaluates
@@ -1884,10 +1941,10 @@ struct VerboseBuilder {
           if (stack.empty() || stack.back().type != rc.x) throw Fatal{"IncompatibleError", "MI355X path: unbalanced verbose event records"};
           VNode n = std::move(stack.back());
           stack.pop_back();
-          attach(std::move(n.ctx), close_container(rc), std::move(n.children));
+          attach(std::move(n.ctx), close_container(rc), std::move(n.children), text ? close_disp(rc) : std::string(), std::move(n.tk));
           break;
         }
-        case REC_SUCCESS: leaf(mk ? std::string() : ctx_d(rc.clause), J::str("Success")); break;
+        case REC_SUCCESS: leaf(mk ? std::string() : ctx_d(rc.clause), J::str("Success"), "GuardClauseValueCheck(Status=PASS)"); break;
         case REC_CMP: {
           const uint32_t op = mk ? (rc.y & 15u) : (pc(rc.clause).flags & 15u);
           const bool neg = mk ? ((rc.y >> 4) & 1u) : ((pc(rc.clause).flags >> 4) & 1u);
@@ -1898,18 +1955,28 @@ struct VerboseBuilder {
           m.add("message", rc.x ? J::str(r.nc_reason(rc)) : J::null());
           m.add("custom_message", mk ? J::null() : r.custom_opt(pc(rc.clause)));
           m.add("status", status_json(ST_FAIL));
-          leaf(mk ? std::string() : ctx_d(rc.clause), tagged("Comparison", std::move(m)));
+          std::string disp;
+          if (text)
+            disp = "GuardClauseBinaryCheck(Status=FAIL, Comparison=" + cmp_text(op, neg) + ", from=" + qr_text(rc.from, false) +
+                   ", to=" + (rc.to.meta == 0xFFFFFFFFu ? std::string() : qr_text(rc.to, false)) + ")";
+          leaf(mk ? std::string() : ctx_d(rc.clause), tagged("Comparison", std::move(m)), std::move(disp));
           break;
         }
         case REC_IN: {
           const uint32_t op = mk ? (rc.y & 15u) : (pc(rc.clause).flags & 15u);
           const bool neg = mk ? ((rc.y >> 4) & 1u) : ((pc(rc.clause).flags >> 4) & 1u);
           J to = J::arr();
+          std::string tos;   // SliceDisplay (exprs.rs:286-303) of the to values
           uint32_t got = 0;
+          auto add_to = [&](const QR& q) {
+            to.push(r.qr_json(q, false));
+            if (text) tos += (got ? "." : "") + qr_text(q, false);
+            got++;
+          };
           while (got < rc.x && i + 1 < recs.size() && recs[i + 1].kind == REC_LIST) {
             const Rec& l = recs[++i];
-            to.push(r.qr_json(l.from, false)); got++;
-            if (got < rc.x) { to.push(r.qr_json(l.to, false)); got++; }
+            add_to(l.from);
+            if (got < rc.x) add_to(l.to);
           }
           J m = J::obj();
           m.add("comparison", r.comparison(op, neg));
@@ -1918,7 +1985,14 @@ struct VerboseBuilder {
           m.add("message", J::null());
           m.add("custom_message", mk ? J::null() : r.custom_opt(pc(rc.clause)));
           m.add("status", status_json(ST_FAIL));
-          leaf(mk ? std::string() : ctx_d(rc.clause), tagged("InComparison", std::move(m)));
+          std::string disp;
+          if (text) {
+            std::string fixed;
+            for (size_t k = 0; k < tos.size(); k++) { if (tos[k] == '.' && k + 1 < tos.size() && tos[k + 1] == '[') continue; fixed.push_back(tos[k]); }
+            disp = "GuardClauseInBinaryCheck(Status=FAIL, Comparison=" + cmp_text(op, neg) + ", from=" + qr_text(rc.from, false) +
+                   ", to=" + fixed + ")";
+          }
+          leaf(mk ? std::string() : ctx_d(rc.clause), tagged("InComparison", std::move(m)), std::move(disp));
           break;
         }
         case REC_UNARY: {
@@ -1931,20 +2005,30 @@ struct VerboseBuilder {
           J u = J::obj();
           u.add("value", std::move(v));
           u.add("comparison", r.comparison(p.flags & 15u, (p.flags >> 4) & 1u));
-          leaf(ctx_d(rc.clause), tagged("Unary", std::move(u)));
+          std::string disp;
+          if (text)
+            disp = "GuardClauseUnaryCheck(Status=FAIL, Comparison=" + cmp_text(p.flags & 15u, (p.flags >> 4) & 1u) +
+                   ", Value-At=" + qr_text(rc.from, true) + ")";
+          leaf(ctx_d(rc.clause), tagged("Unary", std::move(u)), std::move(disp));
           break;
         }
-        case REC_NOVALUE_EMPTY: leaf(ctx_d(rc.clause), tagged("NoValueForEmptyCheck", r.custom_opt(pc(rc.clause)))); break;
+        case REC_NOVALUE_EMPTY:
+          leaf(ctx_d(rc.clause), tagged("NoValueForEmptyCheck", r.custom_opt(pc(rc.clause))),
+               "GuardClause(Status=FAIL, Empty, " + r.custom(pc(rc.clause)) + ")");
+          break;
         case REC_MISSING_BLOCK_VALUE: {
           // eval.rs:1343-1358: message "Query <query> did not resolve to correct value, reason <reason>"
           const PClause& p = pc(rc.clause);
+          const std::string msg = "Query " + slice_display(r.prog.queries[p.a], 0) + " did not resolve to correct value, reason " +
+                                  r.reason(rc.from);
           J v = J::obj();
           v.add("from", r.qr_json(rc.from, false));
-          v.add("message", J::str("Query " + slice_display(r.prog.queries[p.a], 0) + " did not resolve to correct value, reason " +
-                                  r.reason(rc.from)));
+          v.add("message", J::str(msg));
           v.add("custom_message", J::null());
           v.add("status", status_json(ST_FAIL));
-          leaf(r.prog.ctx[p.f], tagged("MissingBlockValue", std::move(v)));
+          // display.rs:148-161: the unresolved value's traversed_to path (pointer only)
+          const std::string tt = (rc.from.meta & 3u) == QR_UNRESOLVED ? r.path(rc.from.node) : std::string();
+          leaf(r.prog.ctx[p.f], tagged("MissingBlockValue", std::move(v)), "GuardBlockValueMissing(Status=FAIL, Reason=" + msg + ", " + tt + ")");
           break;
         }
         default: break;   // report-only records (rule / disjunction brackets) and REC_LIST (consumed above)
@@ -1964,6 +2048,31 @@ bool verbose_tree(const DocBatch& docs, uint32_t doc, const Program& prog, const
     VerboseBuilder b{r, data_name, {}, J(), false};
     b.run(tile.recs);
     pretty(b.root, 0, out);
+    return true;
+  } catch (Fatal& f) {
+    err.set = true; err.kind = f.kind; err.msg = f.msg;
+    return false;
+  }
+}
+
+namespace {
+// pprint_tree (commands/validate.rs:666-683)
+void pprint_tree(const TNode& n, const std::string& prefix, bool last, std::string& out) {
+  out += prefix; out += last ? "`- " : "|- "; out += n.line; out += '\n';
+  const std::string child = prefix + (last ? "   " : "|  ");
+  for (size_t i = 0; i < n.kids.size(); i++) pprint_tree(n.kids[i], child, i + 1 == n.kids.size(), out);
+}
+}  // namespace
+
+bool verbose_text(const DocBatch& docs, uint32_t doc, const Program& prog, const TileResult& tile, const std::string& data_name,
+                  std::string& out, ReportError& err) {
+  try {
+    if (tile.out.err) { tile_error(docs, doc, prog, tile.out, err); return false; }
+    R r{docs, prog, docs.serde, docs.base[doc], &tile.aux};
+    VerboseBuilder b{r, data_name, {}, J(), false};
+    b.text = true;
+    b.run(tile.recs);
+    pprint_tree(b.troot, "", true, out);
     return true;
   } catch (Fatal& f) {
     err.set = true; err.kind = f.kind; err.msg = f.msg;

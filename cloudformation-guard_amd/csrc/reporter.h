@@ -91,10 +91,16 @@ struct TestRuleResult {
   int32_t matched = -1;               // get_status_result: the matched status, -1 = FAIL
   std::vector<uint32_t> evaluated;    // statuses seen before the match (FAIL: all of them)
 };
+// print_verbose_tree (commands/validate.rs:685-687) of a verbose-kernel tile: the EventRecord tree
+// as Display lines (display.rs:128-328)
+bool verbose_text(const DocBatch& docs, uint32_t doc, const Program& prog, const TileResult& tile, const std::string& data_name,
+                  std::string& out, ReportError& err);
+
 struct TestCaseResult {
   bool has_name = false;
   std::string name;
   std::vector<TestRuleResult> rules;
+  std::string tree;                   // --verbose: the case's EventRecord tree as text (verbose_text)
 };
 struct TestSpecFile {
   std::string error;                  // non-empty: the spec file did not parse (Error Display)

@@ -67,8 +67,11 @@ def lib():
                                           ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ExternError)]
     L.gg_session_report_range.restype = ctypes.c_void_p
     L.cfn_guard_test_dir.argtypes = [ctypes.POINTER(ValidateInput), ctypes.c_size_t, ctypes.POINTER(ValidateInput),
-                                     ctypes.POINTER(ctypes.c_size_t), ctypes.c_int32, ctypes.POINTER(ctypes.c_int32),
-                                     ctypes.POINTER(ExternError)]
+                                     ctypes.POINTER(ctypes.c_size_t), ctypes.c_int32, ctypes.c_bool,
+                                     ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ExternError)]
+    L.cfn_guard_test_ex.argtypes = [ValidateInput, ctypes.POINTER(ValidateInput), ctypes.c_size_t, ctypes.c_int32,
+                                    ctypes.c_bool, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ExternError)]
+    L.cfn_guard_test_ex.restype = ctypes.c_void_p
     L.cfn_guard_test_dir.restype = ctypes.c_void_p
     L.gg_session_report_format.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32),
                                            ctypes.POINTER(ExternError)]
@@ -253,19 +256,19 @@ def validate_structured(rules, data, output="json", params=None):
 TEST_OUTPUT_FORMATS = {"text": 4, "json": 0, "yaml": 1, "junit": 3}
 
 
-def run_test(rules_text, rules_name, specs, output="text"):
-    """`cfn-guard test` over one rules file and spec files [(path, text)] -> (report text, exit code)."""
+def run_test(rules_text, rules_name, specs, output="text", verbose=False):
+    """`cfn-guard test [--verbose]` over one rules file and spec files [(path, text)] -> (report text, exit code)."""
     S = (ValidateInput * max(1, len(specs)))(*[ValidateInput(_b(t), _b(n)) for n, t in specs])
     code = ctypes.c_int32(0)
     err = ExternError()
-    p = lib().cfn_guard_test(ValidateInput(_b(rules_text), _b(rules_name)), S, len(specs), TEST_OUTPUT_FORMATS[output],
-                             ctypes.byref(code), ctypes.byref(err))
+    p = lib().cfn_guard_test_ex(ValidateInput(_b(rules_text), _b(rules_name)), S, len(specs), TEST_OUTPUT_FORMATS[output],
+                                verbose, ctypes.byref(code), ctypes.byref(err))
     if err.code != 0:
         _raise(err)
     return _take_string(p), code.value
 
 
-def run_test_dir(pairs, output="text"):
+def run_test_dir(pairs, output="text", verbose=False):
     """`cfn-guard test -d` over [(rules_name, rules_text, [(spec_path, spec_text), ...]), ...] in the
     directory's order -> (report text, exit code)."""
     R = (ValidateInput * max(1, len(pairs)))(*[ValidateInput(_b(t), _b(n)) for n, t, _ in pairs])
@@ -274,7 +277,8 @@ def run_test_dir(pairs, output="text"):
     C = (ctypes.c_size_t * max(1, len(pairs)))(*[len(sps) for _, _, sps in pairs])
     code = ctypes.c_int32(0)
     err = ExternError()
-    p = lib().cfn_guard_test_dir(R, len(pairs), S, C, TEST_OUTPUT_FORMATS[output], ctypes.byref(code), ctypes.byref(err))
+    p = lib().cfn_guard_test_dir(R, len(pairs), S, C, TEST_OUTPUT_FORMATS[output], verbose, ctypes.byref(code),
+                                 ctypes.byref(err))
     if err.code != 0:
         _raise(err)
     return _take_string(p), code.value

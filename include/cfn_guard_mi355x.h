@@ -73,14 +73,21 @@ char *cfn_guard_validate_batch_params(const validate_input_t *docs, size_t n_doc
 #define CFN_GUARD_OUTPUT_TEXT 4
 char *cfn_guard_test(validate_input_t rules, const validate_input_t *specs, size_t n_specs, int32_t output_format,
                      int32_t *exit_code, extern_err_t *err);
+/* cfn_guard_test with `--verbose` (text only): each test case's EventRecord tree printed as
+ * print_verbose_tree does (commands/validate.rs:666-687, reporters/test/generic.rs:116-118); verbose
+ * with a structured format is the reference's IllegalArguments (18, test.rs:134-137). */
+char *cfn_guard_test_ex(validate_input_t rules, const validate_input_t *specs, size_t n_specs, int32_t output_format,
+                        bool verbose, int32_t *exit_code, extern_err_t *err);
 
 /* `cfn-guard test -d <dir> [-o json|yaml|junit]` (commands/test.rs:143-165): n_rules rules files, rules
  * file i with the spec_counts[i] test-spec files that follow each other in `specs` (the directory's
  * pairing of a rules file with its tests, done by the caller as OrderedTestDirectory does).  Text:
  * "Testing Guard File ..." sections (test.rs:221-283); json / yaml / junit: one Vec<TestResult>
- * (test.rs:383-456).  *exit_code as cfn_guard_test, folded over the rules files. */
+ * (test.rs:383-456); verbose (text only) as cfn_guard_test_ex.  *exit_code as cfn_guard_test, folded
+ * over the rules files. */
 char *cfn_guard_test_dir(const validate_input_t *rules, size_t n_rules, const validate_input_t *specs,
-                         const size_t *spec_counts, int32_t output_format, int32_t *exit_code, extern_err_t *err);
+                         const size_t *spec_counts, int32_t output_format, bool verbose, int32_t *exit_code,
+                         extern_err_t *err);
 
 /* ---- session API (documents resident in HBM across evaluations; used by bench.py/tests) ---- */
 typedef struct gg_session gg_session;

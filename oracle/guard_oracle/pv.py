@@ -210,6 +210,11 @@ def display(v: PV) -> str:
     return "Path=%s Value=%s" % (v.path_display(), value_only(v))
 
 
+def display_path_only(v: PV) -> str:
+    """`self_path().0` -- the JSON pointer alone (display.rs:157-160)"""
+    return v.path
+
+
 # ---------------------------------------------------------------------------
 # Rust Debug (derived)
 # ---------------------------------------------------------------------------

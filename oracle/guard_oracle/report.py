@@ -461,6 +461,100 @@ def _container_json(c):
     return OMap([(k, _clause_check_json(c[1]))])
 
 
+# ---------------------------------------------------------------------------
+# verbose EventRecord tree as text: Display of EventRecord / RecordType / ClauseCheck (display.rs:
+# 128-328) drawn by pprint_tree (commands/validate.rs:666-687) -- `cfn-guard test --verbose`
+# (reporters/test/generic.rs:116-118) and `validate --verbose`
+# ---------------------------------------------------------------------------
+_CMP_DISPLAY = {"Eq": "EQUALS", "In": "IN", "Gt": "GREATER THAN", "Lt": "LESS THAN", "Ge": "GREATER THAN EQUALS",
+                "Le": "LESS THAN EQUALS", "Exists": "EXISTS", "Empty": "EMPTY", "IsString": "IS STRING",
+                "IsBool": "IS BOOL", "IsInt": "IS INT", "IsList": "IS LIST", "IsMap": "IS MAP", "IsNull": "IS NULL",
+                "IsFloat": "IS FLOAT"}
+
+
+def _cmp_text(c):
+    """display_comparison (display.rs:9-11): format!("{} {}", if not {"not"} else {""}, cmp)"""
+    op, neg = c
+    return "%s %s" % ("not" if neg else "", _CMP_DISPLAY[op])
+
+
+def _qr_text(q):
+    """QueryResult Display (display.rs:109-126)"""
+    k, v = q
+    if k == "L":
+        return "literal, %s" % P.display(v)
+    if k == "R":
+        return "(resolved, %s)" % P.display(v)
+    return "(unresolved, %s)" % P.display(v.traversed_to)
+
+
+def _slice_text(items):
+    """SliceDisplay (exprs.rs:286-303): items joined by "." with ".[" -> "[" """
+    return ".".join(items).replace(".[", "[")
+
+
+def _container_text(c):
+    k = c[0]
+    if k == "FileCheck":
+        return "File(%s, Status=%s)" % (c[1], c[2])
+    if k == "RuleCheck":
+        return "Rule(%s, Status=%s)" % (c[1], c[2])
+    if k == "RuleCondition":
+        return "Rule/When(Status=%s)" % c[1]
+    if k == "TypeCheck":
+        return "Type(%s, Status=%s)" % (c[2], c[1])
+    if k == "TypeCondition":
+        return "TypeBlock/When Status=%s)" % c[1]
+    if k == "TypeBlock":
+        return "TypeBlock/Block Status=%s)" % c[1]
+    if k == "Filter":
+        return "Filter/ConjunctionsBlock(Status=%s)" % c[1]
+    if k == "WhenCheck":
+        return "WhenConditionalBlock(Status = %s)" % c[1]
+    if k == "WhenCondition":
+        return "WhenCondition(Status = %s)" % c[1]
+    if k == "Disjunction":
+        return "Disjunction(Status = %s)" % c[1]
+    if k == "BlockGuardCheck":
+        return "GuardValueBlockCheck(Status = %s)" % c[1]
+    if k == "GuardClauseBlockCheck":
+        return "GuardClauseBlock(Status = %s)" % c[1]
+    cc = c[1]
+    ck = cc[0]
+    if ck == "Success":
+        return "GuardClauseValueCheck(Status=PASS)"
+    m = cc[1]
+    if ck == "NoValueForEmptyCheck":
+        return "GuardClause(Status=FAIL, Empty, %s)" % (m or "")
+    if ck == "MissingBlockValue":
+        f = m["from"]
+        tt = P.display_path_only(f[1].traversed_to) if f[0] == "U" else ""
+        return "GuardBlockValueMissing(Status=FAIL, Reason=%s, %s)" % (m["message"] or "", tt)
+    if ck == "DependentRule":
+        return "GuardClauseDependentRule(Rule=%s, Status=FAIL)" % m["rule"]
+    if ck == "Unary":
+        return "GuardClauseUnaryCheck(Status=FAIL, Comparison=%s, Value-At=%s)" % (_cmp_text(m["comparison"]), _qr_text(m["from"]))
+    if ck == "Comparison":
+        return "GuardClauseBinaryCheck(Status=%s, Comparison=%s, from=%s, to=%s)" % (
+            m["status"], _cmp_text(m["comparison"]), _qr_text(m["from"]), _qr_text(m["to"]) if m["to"] is not None else "")
+    return "GuardClauseInBinaryCheck(Status=%s, Comparison=%s, from=%s, to=%s)" % (
+        m["status"], _cmp_text(m["comparison"]), _qr_text(m["from"]), _slice_text([_qr_text(t) for t in m["to"]]))
+
+
+def event_text(ev):
+    """print_verbose_tree: pprint_tree(root, "", true) -- one line per record,
+    prefix + ("`- " | "|- ") + "{container}[Context={context}]" """
+    out = []
+
+    def walk(e, prefix, last):
+        out.append("%s%s%s[Context=%s]\n" % (prefix, "`- " if last else "|- ", _container_text(e.container), e.context))
+        child_prefix = prefix + ("   " if last else "|  ")
+        for i, ch in enumerate(e.children):
+            walk(ch, child_prefix, i == len(e.children) - 1)
+    walk(ev, "", True)
+    return "".join(out)
+
+
 def event_json(ev):
     """EventRecord {context, container, children} (eval_context.rs:990-997)"""
     return OMap([("context", ev.context), ("container", _container_json(ev.container)),

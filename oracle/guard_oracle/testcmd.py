@@ -15,8 +15,8 @@ from . import evaluator as E
 from .formats import _xml_escape, to_yaml
 from .loader import load_serde_yaml_tree, serde_tree_to_pv, load_serde_json
 from .parser import parse_rules
-from .pv import LIST, MAP, STRING
-from .report import OMap, to_json_pretty
+from .pv import LIST, MAP, STRING, PV, MapValue
+from .report import OMap, event_text, to_json_pretty
 
 TEST_ERROR, TEST_FAILURE, SUCCESS = 1, 7, 0
 
@@ -42,8 +42,23 @@ def _load_specs(text, path):
             raise GuardError("ParseError", "Unable to process data in file %s, Error missing field" % path)
         rules = exp.val.values["rules"]
         expected = [(k, v.val) for k, v in rules.val.values.items()] if rules.kind == MAP else []
-        out.append((None if name is None or name.kind != STRING else name.val, vals["input"], expected))
+        # PathAwareValue::try_from(spec.input) (reporters/test/generic.rs:75): the input is its own
+        # root -- paths relative to it, not to the spec file
+        out.append((None if name is None or name.kind != STRING else name.val, _reroot(vals["input"], len(vals["input"].path)), expected))
     return out
+
+
+def _reroot(v, cut):
+    """a copy of serde-loaded value `v` with `cut` leading path characters removed (locations are 0)"""
+    k = v.kind
+    if k == LIST:
+        return PV(LIST, v.path[cut:], 0, 0, [_reroot(e, cut) for e in v.val])
+    if k == MAP:
+        mv = MapValue()
+        mv.keys = [PV(STRING, kp.path[cut:], 0, 0, kp.val) for kp in v.val.keys]
+        mv.values = {key: _reroot(e, cut) for key, e in v.val.values.items()}
+        return PV(MAP, v.path[cut:], 0, 0, mv)
+    return PV(k, v.path[cut:], 0, 0, v.val)
 
 
 def _status(s):
@@ -52,9 +67,11 @@ def _status(s):
     return s
 
 
-def _by_rules(rf, inp):
+def _by_rules(rf, inp, tree=None):
     root = E.RootScope(rf, inp)
     E.eval_rules_file(rf, root, None)
+    if tree is not None:
+        tree.append(root.recorder.final_event)
     by = {}
     for ch in root.recorder.final_event.children:
         if ch.container and ch.container[0] == "RuleCheck":
@@ -77,8 +94,12 @@ def get_status_result(expected, got):
     return None, statuses
 
 
-def run_test(rules_text, rules_name, specs, output="text"):
-    """specs: [(path, text)].  Returns (stdout text, exit code)."""
+def run_test(rules_text, rules_name, specs, output="text", verbose=False):
+    """specs: [(path, text)].  Returns (stdout text, exit code).  verbose: each test case's
+    EventRecord tree as text (reporters/test/generic.rs:116-118); with a structured output the
+    reference refuses the flags (test.rs:134-137, IllegalArguments)."""
+    if verbose and output != "text":
+        raise GuardError("IllegalArguments", "Cannot provide an output_type of JSON, YAML, or JUnit while the verbose flag is set")
     try:
         rf = parse_rules(rules_text, rules_name)
     except GuardError as e:
@@ -91,11 +112,11 @@ def run_test(rules_text, rules_name, specs, output="text"):
         # Ok(None): nothing written, SUCCESS_STATUS_CODE (test.rs:315, 366)
         return "", SUCCESS
     if output == "text":
-        return _generic(rf, specs)
+        return _generic(rf, specs, verbose)
     return _structured(rf, rules_name, specs, output)
 
 
-def _generic(rf, specs):
+def _generic(rf, specs, verbose=False):
     out, code, counter = [], SUCCESS, 1
     for path, text in specs:
         try:
@@ -109,7 +130,8 @@ def _generic(rf, specs):
             if name is not None:
                 out.append("Name: %s\n" % name)
             exp = dict(expected)
-            by = _by_rules(rf, inp)
+            tree = []
+            by = _by_rules(rf, inp, tree)
             res = {}
             for rule, got in by.items():
                 if rule not in exp:
@@ -121,6 +143,8 @@ def _generic(rf, specs):
                     res.setdefault("PASS", []).append("%s: Expected = %s" % (rule, m))
                 else:
                     res.setdefault("FAIL", []).append("%s: Expected = %s, Evaluated = [%s]" % (rule, e, ", ".join(st)))
+            if verbose:
+                out.append(event_text(tree[0]))
             if "FAIL" in res:
                 code = TEST_FAILURE
             for k in sorted(res):
@@ -224,10 +248,12 @@ def _fold_code(code, test_code):
     return TEST_ERROR if test_code == TEST_ERROR else TEST_FAILURE
 
 
-def run_test_dir(pairs, output="text"):
+def run_test_dir(pairs, output="text", verbose=False):
     """``cfn-guard test -d`` (test.rs:143-165) over [(rules_name, rules_text, [(spec_path, text)])] in the
     directory's order: handle_plaintext_directory (text, :221-283) or
     handle_structured_directory_report (:383-456).  Returns (stdout text, exit code)."""
+    if verbose and output != "text":
+        raise GuardError("IllegalArguments", "Cannot provide an output_type of JSON, YAML, or JUnit while the verbose flag is set")
     if output == "text":
         out, code = [], SUCCESS
         for rules_name, rules_text, specs in pairs:
@@ -243,7 +269,7 @@ def run_test_dir(pairs, output="text"):
                 out.append("---\n")
                 continue
             if rf is not None:
-                text, c = _generic(rf, specs)
+                text, c = _generic(rf, specs, verbose)
                 out.append(text)
                 code = c if code == SUCCESS else code
             out.append("---\n")

@@ -227,8 +227,10 @@ def test_reference_validate_resources_vs_oracle():
         for fmt in ("json", "yaml", "sarif", "junit"):
             exp, ecode, err = oracle_validate(rules, data, output=fmt)
             if ecode == -1:
-                with pytest.raises(guard_amd.GuardError):
+                with pytest.raises(guard_amd.GuardError) as ei:
                     guard_amd.validate_structured(rules, data, output=fmt)
+                # same abort: the Display the CLI prints after "Error occurred " (main.rs:36-41)
+                assert err.endswith("Error occurred " + ei.value.message), (c["source"], fmt)
                 continue
             out, code = guard_amd.validate_structured(rules, data, output=fmt)
             assert (code, out) == (ecode, exp), (c["source"], fmt)

@@ -74,3 +74,34 @@ def test_test_command_directory_vs_oracle():
     for combo in (pairs, pairs + extra, extra[::-1] + pairs):
         for fmt in ("text", "json", "yaml", "junit"):
             assert guard_amd.run_test_dir(combo, fmt) == oracle_dir(combo, fmt), ([c[0] for c in combo], fmt)
+
+
+def test_test_command_verbose_goldens():
+    """cfn_guard_test_ex / cfn_guard_test_dir with verbose: the verbose wave kernel's event stream drawn
+    as print_verbose_tree (test_command.rs:223-257 goldens); structured formats refuse the flag (18)"""
+    from test_oracle_golden import directory_pairs
+    for sp in ("json", "yaml"):
+        spec = "s3_bucket_server_side_encryption_enabled." + sp
+        out, code = guard_amd.run_test(_rules(), RN, [("resources/test-command/data-dir/" + spec, open(os.path.join(T, spec)).read())],
+                                       "text", verbose=True)
+        assert code == 0 and out == open(os.path.join(T, "test_data_file_verbose.out")).read(), sp
+    out, code = guard_amd.run_test_dir(directory_pairs(), "text", verbose=True)
+    assert code == 0 and out == open(os.path.join(T, "test_data_dir_verbose.out")).read()
+    with pytest.raises(guard_amd.GuardError) as ei:
+        guard_amd.run_test(_rules(), RN, [("s.yaml", "[]")], "json", verbose=True)
+    assert ei.value.code == 18
+
+
+def test_test_command_verbose_vs_oracle():
+    """every reference example spec (tests/golden/expectations.json) through `test --verbose`: the text
+    EventRecord trees (every container and value-check kind the packs reach) equal the oracle's"""
+    cases = json.load(open(os.path.join(G, "expectations.json")))
+    groups = {}
+    for c in cases:
+        groups.setdefault((c["rules_name"], c["spec"]), (c["rules_text"], []))[1].append(c)
+    for (rname, spec), (rtext, cs) in sorted(groups.items()):
+        spec_json = json.dumps([{"name": "case %d" % c["case"], "input": json.loads(c["input_json"]),
+                                 "expectations": {"rules": c["expected"]}} for c in cs])
+        exp = oracle_test(rtext, rname, [(spec, spec_json)], "text", verbose=True)
+        got = guard_amd.run_test(rtext, rname, [(spec, spec_json)], "text", verbose=True)
+        assert got == exp, (rname, spec)
