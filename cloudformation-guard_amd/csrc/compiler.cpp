@@ -224,64 +224,81 @@ struct Compiler {
       for (uint32_t j = 0; j < n.count; j++) if (!lit_dfa_only(n.a + j)) return false;
     return true;
   }
-  // `%v` whose resolution cannot raise: defined by root-block lets only (no block let or rule
-  // parameter anywhere shares the name, so every scope chain reaches the root's), every one of them
-  // a literal or a query that cannot raise.  A capture-only name does not qualify (MissingVariable
-  // when nothing was captured).
-  bool safe_root_var(uint32_t var, int depth) const {
+  // `%v` whose resolution cannot raise:
+  //  * in block `blk` (a let query's own block): v is one of blk's lets -- the lazy evaluation of a
+  //    block let runs in that block's scope (BlockScope::resolve_variable, eval_context.rs:1564-1590),
+  //    and filters and value scopes in between define no variables -- and that let cannot raise;
+  //  * otherwise: v is defined by root-block lets only (no block let or rule parameter anywhere shares
+  //    the name, so every scope chain reaches the root's), every one a literal or a query that cannot
+  //    raise.  A capture-only name does not qualify (MissingVariable when nothing was captured).
+  bool let_error_free(const PLet& l, uint32_t blk, int depth) const {
+    if (l.kind == L_FUNC) return false;
+    if (l.kind == L_LITERAL) return lit_dfa_only(l.id);
+    return error_free_query(l.id, depth, blk);
+  }
+  bool safe_var(uint32_t var, uint32_t blk, int depth) const {
+    if (blk != NONE) {
+      bool found = false;
+      for (uint32_t i = 0; i < blocks[blk].nlets; i++) {
+        const PLet& l = lets[blocks[blk].first_let + i];
+        if (l.var != var) continue;
+        if (!let_error_free(l, blk, depth)) return false;
+        found = true;
+      }
+      if (found) return true;
+    }
     bool defined = false;
     for (size_t b = 0; b < blocks.size(); b++)
       for (uint32_t i = 0; i < blocks[b].nlets; i++) {
         const PLet& l = lets[blocks[b].first_let + i];
         if (l.var != var) continue;
         if (b != P.hdr.root_block) return false;
-        if (l.kind == L_FUNC) return false;
-        if (l.kind == L_LITERAL && !lit_dfa_only(l.id)) return false;
-        if (l.kind == L_QUERY && !error_free_query(l.id, depth)) return false;
+        if (!let_error_free(l, P.hdr.root_block, depth)) return false;
         defined = true;
       }
     for (uint32_t v : param_vars) if (v == var) return false;
     return defined;
   }
-  // a query of navigation steps, root-variable heads and filters that cannot raise (no `%var` key
-  // interpolation, no named capture -- captures change the root scope)
-  bool error_free_query(uint32_t qid, int depth) const {
-    if (depth > 4) return false;
+  // a query of navigation steps, variable heads (safe_var) and filters that cannot raise (no `%var`
+  // key interpolation, no named capture -- captures change the root scope); `blk`: the block whose
+  // scope evaluates it (a let query), or NONE
+  bool error_free_query(uint32_t qid, int depth, uint32_t blk = NONE) const {
+    if (depth > 16) return false;
     const PQuery& q = queries[qid];
     for (uint32_t i = 0; i < q.n; i++) {
       const PPart& pp = parts[q.first + i];
       bool ok = pp.kind == P_THIS || pp.kind == P_KEY || pp.kind == P_KEY_INDEX || pp.kind == P_INDEX ||
                 ((pp.kind == P_ALL_VALUES || pp.kind == P_ALL_INDICES) && pp.a == NONE);
-      if (!ok && i == 0 && pp.kind == P_VAR_HEAD) ok = safe_root_var(pp.a, depth + 1);
-      if (!ok && pp.kind == P_FILTER && pp.b == NONE) ok = error_free_conj(pp.a, depth + 1);
+      if (!ok && i == 0 && pp.kind == P_VAR_HEAD) ok = safe_var(pp.a, blk, depth + 1);
+      if (!ok && pp.kind == P_FILTER && pp.b == NONE) ok = error_free_conj(pp.a, depth + 1, blk);
       if (!ok) return false;
     }
     return true;
   }
-  bool error_free_conj(uint32_t cj, int depth) const {
-    if (depth > 4) return false;
+  bool error_free_conj(uint32_t cj, int depth, uint32_t blk = NONE) const {
+    if (depth > 16) return false;
     const PRange2 C = conjs[cj];
     for (uint32_t i = 0; i < C.n; i++) {
       const PRange2 Di = disjs[disj_refs[C.first + i]];
-      for (uint32_t j = 0; j < Di.n; j++) if (!error_free_clause(clause_refs[Di.first + j], depth)) return false;
+      for (uint32_t j = 0; j < Di.n; j++) if (!error_free_clause(clause_refs[Di.first + j], depth, blk)) return false;
     }
     return true;
   }
   // access clause with no EMPTY (raises on scalars), whose operands are literals with DFA-compilable
   // regexes or queries that cannot raise: its evaluation can only produce statuses and records
-  bool error_free_clause(uint32_t cid, int depth = 0) const {
+  bool error_free_clause(uint32_t cid, int depth = 0, uint32_t blk = NONE) const {
     const PClause& pc = clauses[cid];
     if (pc.kind != C_ACCESS) return false;
     uint32_t op = pc.flags & 15u, rk = (pc.flags >> 8) & 15u;
     if (op == OP_EMPTY) return false;
     if (op < OP_EXISTS) {
       if (rk == RHS_LITERAL) { if (!(pc.b & LIT_BIT) || !lit_dfa_only(pc.b)) return false; }
-      else if (rk == RHS_QUERY) { if (!error_free_query(pc.b, depth + 1)) return false; }
+      else if (rk == RHS_QUERY) { if (!error_free_query(pc.b, depth + 1, blk)) return false; }
       else return false;
     }
-    return error_free_query(pc.a, depth + 1);
+    return error_free_query(pc.a, depth + 1, blk);
   }
-  uint32_t fast_filter_clause(uint32_t cj) {
+  uint32_t fast_filter_clause(uint32_t cj, uint32_t blk = NONE) {
     const PRange2 C = conjs[cj];
     if (C.n < 1) return 0;
     const PRange2 D = disjs[disj_refs[C.first]];
@@ -302,7 +319,7 @@ struct Compiler {
     if (C.n == 1) return cid + 1;
     for (uint32_t i = 1; i < C.n; i++) {
       const PRange2 Di = disjs[disj_refs[C.first + i]];
-      for (uint32_t j = 0; j < Di.n; j++) if (!error_free_clause(clause_refs[Di.first + j])) return 0;
+      for (uint32_t j = 0; j < Di.n; j++) if (!error_free_clause(clause_refs[Di.first + j], 0, blk)) return 0;
     }
     return (cid + 1) | 0x80000000u;
   }
@@ -587,8 +604,18 @@ struct Compiler {
   }
 
   void assemble() {
-    for (auto& pp : parts)
-      if (pp.kind == P_FILTER) pp.c = fast_filter_clause(pp.a);
+    // a let's query is evaluated in its block's scope: its filters may lean on that block's lets
+    std::vector<uint32_t> query_block(queries.size(), NONE);
+    for (size_t b = 0; b < blocks.size(); b++)
+      for (uint32_t i = 0; i < blocks[b].nlets; i++) {
+        const PLet& l = lets[blocks[b].first_let + i];
+        if (l.kind == L_QUERY && l.id < queries.size()) query_block[l.id] = (uint32_t)b;
+      }
+    for (size_t q = 0; q < queries.size(); q++)
+      for (uint32_t i = 0; i < queries[q].n; i++) {
+        PPart& pp = parts[queries[q].first + i];
+        if (pp.kind == P_FILTER) pp.c = fast_filter_clause(pp.a, query_block[q]);
+      }
     mark_root_vars();
     std::vector<uint32_t> blob(sizeof(ProgHeader) / 4 + 2, 0);
     ProgHeader& h = P.hdr;
