@@ -219,6 +219,7 @@ struct DeviceBufs {
   DBuf<uint32_t> d_order;       // lane-mode document order (shape-sorted batches), empty = identity
   DBuf<uint32_t> d_tix;
   DBuf<DevProg> d_progs;
+  DBuf<uint32_t> d_rx_memo;     // regex is_match memo over the string pool (DevProg::rx_memo)
   DBuf<uint8_t> d_heaps;        // wave mode: one heap per wave slot
   DBuf<uint8_t> d_lane_heaps;   // lane mode: one heap per lane
   DBuf<uint32_t> d_retry;       // tiles handed from lane mode to wave mode
@@ -239,7 +240,7 @@ struct DeviceBufs {
   }
   size_t bytes() const {
     return d_nodes.bytes() + d_klen.bytes() + d_bytes.bytes() + d_roots.bytes() + d_base.bytes() + d_res_map.bytes() +
-           d_tix_off.bytes() + d_tix.bytes() + d_progs.bytes() + d_heaps.bytes() + d_lane_heaps.bytes() + d_retry.bytes() +
+           d_tix_off.bytes() + d_tix.bytes() + d_progs.bytes() + d_rx_memo.bytes() + d_heaps.bytes() + d_lane_heaps.bytes() + d_retry.bytes() +
            d_big_heaps.bytes() + d_retry2.bytes() + d_tiles.bytes() + d_rule_status.bytes() + d_recs.bytes() +
            d_counters.bytes() + d_counts.bytes() + d_stats.bytes();
   }
@@ -464,8 +465,22 @@ void session_upload(gg_session* s) {
   std::vector<DevProg> dps;
   s->max_top = 1;
   StringIds ids;
+  // regex is_match memo: 2 bits per 16-B pool slot per regex, zeroed once per upload (the pool and
+  // the programs are fixed for the session's life)
+  const uint32_t memo_words = (uint32_t)std::min<size_t>(s->docs.bytes.size() / 256 + 1, 0xFFFFFFFFull);
+  size_t memo_total = 0;
+  for (auto& p : s->progs) memo_total += (size_t)p->prog.hdr.n_regex * memo_words;
+  const bool memo_on = memo_total && (!getenv("GG_RX_MEMO") || atoi(getenv("GG_RX_MEMO")) != 0);
+  if (memo_on) {
+    s->dv->d_rx_memo.alloc(memo_total);
+    HIPCHK(hipMemsetAsync(s->dv->d_rx_memo.p, 0, memo_total * 4, st));
+  }
+  size_t memo_off = 0;
   for (auto& p : s->progs) {
     p->upload(st, s->docs, ids);
+    p->dp.rx_memo = memo_on && p->prog.hdr.n_regex ? s->dv->d_rx_memo.p + memo_off : nullptr;
+    p->dp.memo_words = memo_words;
+    if (memo_on) memo_off += (size_t)p->prog.hdr.n_regex * memo_words;
     dps.push_back(p->dp);
     s->max_top = std::max<uint32_t>(s->max_top, p->dp.n_top);
   }

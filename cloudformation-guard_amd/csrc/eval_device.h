@@ -39,6 +39,11 @@ struct DevProg {
   uint32_t lds_words;     // words the kernels stage in LDS: the whole blob when it fits the window,
                           // else everything before the regex DFA tables
   uint32_t dfa_lds;       // set by stage_program: the DFA tables were staged (dfa points into LDS)
+  // is_match memo (eval_core.inc regex_match_ref): per regex of this program, 2 bits per 16-B slot of
+  // the document string pool (0 unknown, 1 no match, 2 match) -- a regex's answer is a function of
+  // the interned string alone, and a corpus repeats its strings across documents.  Null: no memo.
+  uint32_t* rx_memo;
+  uint32_t memo_words;    // words per regex
 };
 
 struct DevBatch {
