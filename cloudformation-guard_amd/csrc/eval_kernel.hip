@@ -115,6 +115,7 @@ __device__ __attribute__((always_inline)) inline void tile_begin(CtxT& c, const 
 #ifdef GG_STATS
   for (int i = 0; i < 8; i++) { c.st[i] = 0; c.tdep[i] = 0; }
   for (int i = 0; i < 9; i++) c.tst[i] = 0;
+  for (int i = 0; i < 14; i++) c.fc[i] = 0;
   c.tst[8] = __builtin_amdgcn_s_memtime();
 #endif
 }
@@ -125,6 +126,7 @@ __device__ __attribute__((always_inline)) inline void tile_stats(CtxT& c, const 
   atomicAdd(&A.stats[8], 1ull);
   c.tst[8] = __builtin_amdgcn_s_memtime() - c.tst[8];
   for (int i = 0; i < 9; i++) atomicAdd(&A.stats[9 + i], c.tst[i]);
+  for (int i = 0; i < 14; i++) atomicAdd(&A.stats[18 + i], (unsigned long long)c.fc[i]);
 #endif
 }
 

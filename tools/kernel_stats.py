@@ -14,6 +14,10 @@ NAMES = ["node_reads", "heap_accesses", "query_calls", "clause_evals", "frames",
 # inclusive shader-clock cycles per tile (outermost entry of each category; lanes of a wave share time)
 TIMES = ["eval_rule", "query_retrieval", "binary_operation", "unary_operation", "rec_push", "filter_test",
          "resolve_variable", "push_frame", "tile_total"]
+# entries of the noinline evaluator functions per tile (stats slots 18..31; eval_core.inc FCALL)
+FCALLS = ["eval_conj", "eval_rule", "eval_block_clause", "eval_type_block", "eval_param_call", "eval_misc_call",
+          "query_retrieval", "walk_run", "compare_op", "resolve_variable", "resolve_function", "map_key_filter",
+          "key_var_step", "filter_test"]
 ndocs = int(sys.argv[1]) if len(sys.argv) > 1 else 20000
 out = {}
 PACK = os.environ.get("PACK", "cfg2")
@@ -41,5 +45,7 @@ for name, text in FILES:
     out[name] = {"kernel_ms": round(min(ms), 3), "tiles": st[8]}
     out[name].update({k: round(st[i] / tiles, 1) for i, k in enumerate(NAMES)})
     out[name]["cycles_per_tile"] = {k: round(st[9 + i] / tiles) for i, k in enumerate(TIMES)}
+    if len(st) >= 32:
+        out[name]["calls_per_tile"] = {k: round(st[18 + i] / tiles, 2) for i, k in enumerate(FCALLS)}
     s.close()
 print(json.dumps(out, indent=1))

@@ -6,7 +6,7 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/pmc
+O=$R/gpurun_out/pmc_${WORKLOAD:-cfg2}
 mkdir -p $O
 for ctr in FETCH_SIZE WRITE_SIZE ${EXTRA_PMC:-}; do
   timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d $O/$ctr -o run -- \
