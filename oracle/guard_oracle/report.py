@@ -24,15 +24,31 @@ class OMap:
         self.items = items
 
 
+class PavJ(OMap):
+    """a serialized PathAwareValue that keeps the value itself (the console reporters read its
+    location and ValueOnlyDisplay, commands/reporters/validate/cfn.rs)"""
+    __slots__ = ("pv",)
+
+    def __init__(self, items, pv):
+        OMap.__init__(self, items)
+        self.pv = pv
+
+
+class UrJ(PavJ):
+    __slots__ = ("ur",)
+
+
 def _ur_json(ur):
-    return OMap([("traversed_to", P.serialize(ur.traversed_to)),
-                 ("remaining_query", ur.remaining_query),
-                 ("reason", ur.reason)])
+    o = UrJ([("traversed_to", P.serialize(ur.traversed_to)),
+             ("remaining_query", ur.remaining_query),
+             ("reason", ur.reason)], ur.traversed_to)
+    o.ur = ur
+    return o
 
 
 def _pav_json(v):
     s = P.serialize(v)
-    return OMap([("path", s["path"]), ("value", s["value"])])
+    return PavJ([("path", s["path"]), ("value", s["value"])], v)
 
 
 class Msgs(OMap):
