@@ -955,6 +955,145 @@ char* cfn_guard_validate_batch_params(const validate_input_t* docs, size_t n_doc
   }
 }
 
+// ---------------------------------------------------------------- validate (console) ---
+// `cfn-guard validate [-r]+ [-d]+ [-i]* [-o single-line-summary|json|yaml] [-S ...] [--verbose]
+// [--print-json]` without --structured (commands/validate.rs:253-487, 552-596, 690-758).  Every pair is
+// evaluated twice on the device -- the throughput kernels (the FileReport the CFN / Terraform reporters
+// and -o json / yaml read) and the verbose kernel (the EventRecord tree the summary table, the generic
+// reporter, --verbose and --print-json read) -- then reported rules file by rules file, data file by
+// data file.  An evaluation error ends the output where the reference's `?` does.
+char* cfn_guard_validate_console(const validate_input_t* docs, size_t n_docs, const validate_input_t* rules,
+                                 size_t n_rules, const validate_input_t* params, size_t n_params, uint32_t show_summary,
+                                 int32_t output_format, uint32_t flags, int32_t* exit_code, char** err_text,
+                                 extern_err_t* err) {
+  set_err(err, 0, "");
+  if (err_text) *err_text = nullptr;
+  if (exit_code) *exit_code = 0;
+  // validate_construct (validate.rs:203-232): junit / sarif need --structured
+  if (output_format != OUT_TEXT && output_format != OUT_JSON && output_format != OUT_YAML) {
+    set_err(err, 18, error_display("IllegalArguments", "the structured flag must be set when output is set to junit or sarif"));
+    if (exit_code) *exit_code = -1;
+    return nullptr;
+  }
+  std::string out, errs;
+  auto finish = [&](int32_t code) -> char* {
+    if (exit_code) *exit_code = code;
+    if (err_text && !errs.empty()) *err_text = dup_str(errs);
+    return dup_str(out);
+  };
+  try {
+    std::string why;
+    if (!ensure_device(why)) { set_err(err, -1, why); if (exit_code) *exit_code = -1; return nullptr; }
+    gg_session s;
+    // data files first (validate.rs:274-315), then the parameter files (317-350): a failure aborts
+    // before anything is evaluated
+    std::vector<std::string> texts;
+    for (size_t i = 0; i < n_docs; i++) {
+      LoadError le;
+      const char* t = docs[i].content ? docs[i].content : "";
+      if (!load_document(s.docs, t, strlen(t), docs[i].file_name ? docs[i].file_name : "", LOAD_LIBYAML, le)) {
+        set_err(err, ffi_code(le.kind), error_display(le.kind, le.msg));
+        if (exit_code) *exit_code = -1;
+        return nullptr;
+      }
+      texts.emplace_back(t);
+    }
+    LoadError pe;
+    if (!load_params(params, n_params, s.params, pe)) {
+      set_err(err, ffi_code(pe.kind), error_display(pe.kind, pe.msg));
+      if (exit_code) *exit_code = -1;
+      return nullptr;
+    }
+    // evaluate_against_data_input merges per data file (`data.clone().merge(file)?`): the first data file
+    // whose merge fails ends the run there, in the first rules file that is evaluated
+    size_t ndocs = s.docs.ndocs();
+    LoadError merge_err;
+    bool merge_failed = false;
+    if (s.params) {
+      DocBatch merged;
+      for (size_t d = 0; d < s.docs.ndocs() && !merge_failed; d++) {
+        // re-append document d alone, then merge the parameters into it
+        DocBatch one;
+        LoadError le;
+        const char* t = texts[d].c_str();
+        load_document(one, t, texts[d].size(), s.docs.names[d], LOAD_LIBYAML, le);
+        merge_batch(merged, one);
+        if (!merge_into_last(merged, merged.ndocs() - 1, *s.params, 0, merge_err)) { merge_failed = true; ndocs = d; }
+      }
+      if (merge_failed) { merged.roots.pop_back(); merged.base.pop_back(); merged.names.pop_back(); }
+      s.docs = std::move(merged);
+    }
+    // rules files in order: a parse error goes to stderr with exit code 5 (evaluate_rule, 563-572)
+    std::vector<int> entry;   // program index, -1 parse error, -2 empty rules file
+    for (size_t i = 0; i < n_rules; i++) {
+      const std::string name = rules[i].file_name ? rules[i].file_name : "";
+      const std::string text = rules[i].content ? rules[i].content : "";
+      RulesFile rf;
+      bool empty = false;
+      std::string perr;
+      bool ok = parse_rules_file(text, name, rf, empty, perr);
+      if (ok && !empty) {
+        auto gp = std::make_unique<GpuProgram>();
+        ok = compile_program(rf, name, gp->prog, perr);
+        if (ok) { entry.push_back((int)s.progs.size()); s.progs.push_back(std::move(gp)); continue; }
+      }
+      if (!ok) {
+        errs += "Parsing error handling rule file = " + name + ", Error = " + error_display("ParseError", perr) + "\n---\n";
+        entry.push_back(-1);
+      } else {
+        entry.push_back(-2);
+      }
+    }
+    const size_t nf = s.progs.size();
+    std::vector<TileOut> tiles;
+    std::vector<uint8_t> rstat;
+    std::vector<Rec> recs;
+    if (nf && s.docs.ndocs()) {
+      session_upload(&s);
+      session_run(&s, true);
+      tiles.swap(s.tiles); rstat.swap(s.rule_status); recs.swap(s.recs);
+      s.mode = 1; s.verbose = true;   // the same batch again through the verbose kernel
+      session_run(&s, true);
+    }
+    ConsoleOptions opt;
+    opt.summary = show_summary;
+    opt.format = output_format;
+    opt.verbose = (flags & 1u) != 0;
+    opt.print_json = (flags & 2u) != 0;
+    int32_t code = 0;
+    bool first_eval = true;
+    for (int e : entry) {
+      if (e == -1) { code = 5; continue; }
+      if (e == -2) continue;
+      bool fail = false;
+      for (size_t d = 0; d < ndocs; d++) {
+        const size_t t = d * nf + (size_t)e;
+        TileResult tr = tile_view(tiles.data(), rstat.data(), s.max_top, recs.data(), t);
+        TileResult vr = tile_view(s.tiles.data(), s.rule_status.data(), s.max_top, s.recs.data(), t);
+        ReportError re;
+        if (!console_report(s.docs, (uint32_t)d, texts[d], s.progs[e]->prog, tr, vr, opt, out, re)) {
+          set_err(err, ffi_code(re.kind), error_display(re.kind, re.msg));
+          errs += "Error occurred " + error_display(re.kind, re.msg);
+          return finish(-1);
+        }
+        if (tr.out.status == ST_FAIL) fail = true;
+      }
+      if (merge_failed && first_eval) {
+        set_err(err, ffi_code(merge_err.kind), error_display(merge_err.kind, merge_err.msg));
+        errs += "Error occurred " + error_display(merge_err.kind, merge_err.msg);
+        return finish(-1);
+      }
+      first_eval = false;
+      if (fail) code = 19;
+    }
+    return finish(code);
+  } catch (std::exception& e) {
+    set_err(err, -1, e.what());
+    if (exit_code) *exit_code = -1;
+    return nullptr;
+  }
+}
+
 // ---------------------------------------------------------------- cfn-guard test ---
 namespace {
 

@@ -162,6 +162,24 @@ inline std::string rust_debug_str(const char* p, size_t n) {
 }
 inline std::string rust_debug_str(const std::string& s) { return rust_debug_str(s.data(), s.size()); }
 
+// char::is_whitespace (Unicode White_Space)
+inline bool rust_is_whitespace(uint32_t c) {
+  return (c >= 0x09 && c <= 0x0D) || c == 0x20 || c == 0x85 || c == 0xA0 || c == 0x1680 || (c >= 0x2000 && c <= 0x200A) ||
+         c == 0x2028 || c == 0x2029 || c == 0x202F || c == 0x205F || c == 0x3000;
+}
+// str::trim: leading and trailing Unicode whitespace removed
+inline std::string rust_trim(const std::string& s) {
+  const unsigned char* p = (const unsigned char*)s.data();
+  size_t i = 0, b = 0, e = 0;
+  bool seen = false;
+  while (i < s.size()) {
+    const size_t at = i;
+    const uint32_t c = utf8_next(p, s.size(), i);
+    if (!rust_is_whitespace(c)) { if (!seen) { b = at; seen = true; } e = i; }
+  }
+  return seen ? s.substr(b, e - b) : std::string();
+}
+
 inline uint32_t fnv1a(const char* p, size_t n) {
   uint32_t h = 2166136261u;
   for (size_t i = 0; i < n; i++) { h ^= (unsigned char)p[i]; h *= 16777619u; }

@@ -11,7 +11,9 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <set>
+#include <unordered_map>
 #include <stdexcept>
 
 #include "host_format.h"
@@ -33,6 +35,10 @@ struct J {
   std::vector<J> a;
   std::vector<std::pair<std::string, J>> o;
   int64_t loc_line = -1, loc_col = -1;   // Messages.location (skip_serializing; read by the SARIF writer)
+  // a serialized PathAwareValue / UnResolved keeps the value it came from (the console reporters read
+  // its location and ValueOnlyDisplay)
+  QR q{};
+  bool hasq = false;
   static J null() { return J(); }
   static J str(const std::string& v) { J j; j.t = Str; j.s = v; return j; }
   static J raw(const std::string& v) { J j; j.t = Raw; j.s = v; return j; }
@@ -304,6 +310,7 @@ struct R {
   int64_t synth_val(const QR& q) const { return (int64_t)(((uint64_t)q.aux << 32) | q.uref); }
   J pav_json(const QR& q) const {
     J o = J::obj();
+    o.q = q; o.hasq = true;
     o.add("path", J::str(q_path(q)));
     o.add("value", is_synth(q) ? J::raw(std::to_string(synth_val(q))) : value_json(q.node));
     return o;
@@ -387,9 +394,13 @@ struct R {
            ", reason: " + (why.empty() ? std::string("None") : "Some(" + rust_debug_str(why) + ")") + " })";
   }
   std::string remaining(const QR& q) const { return prog.query_remaining(q.uref >> 12, q.uref & 0xFFF); }
+  // self_path().1.line and ValueOnlyDisplay of the value a QR carries (an unresolved one's traversed_to)
+  uint32_t q_line(const QR& q) const { return q.node == NONE ? 0 : line(q.node); }
+  std::string q_value_only(const QR& q) const { return is_synth(q) ? std::to_string(synth_val(q)) : value_only(q.node); }
 
   J unresolved_json(const QR& q) const {
     J o = J::obj();
+    o.q = q; o.hasq = true;
     J t = J::obj();
     t.add("path", J::str(path(q.node)));
     t.add("value", value_json(q.node));
@@ -2087,5 +2098,7 @@ bool report_document(const DocBatch& docs, uint32_t doc, const std::vector<const
   out.append(t.data(), t.size());
   return true;
 }
+
+#include "console_report.inc"
 
 }  // namespace gg

@@ -96,6 +96,20 @@ struct TestRuleResult {
 bool verbose_text(const DocBatch& docs, uint32_t doc, const Program& prog, const TileResult& tile, const std::string& data_name,
                   std::string& out, ReportError& err);
 
+// `cfn-guard validate` without --structured (commands/validate.rs:690-758): one (data file, rules file)
+// pair's console output -- the summary table (-S), the CFN / Terraform / generic single-line reporter
+// (-o single-line-summary) or the pair's FileReport (-o json / yaml), then --verbose's EventRecord tree
+// and --print-json.  `tile` is the throughput kernel's tile of the pair, `vtile` the verbose kernel's;
+// `text` the data file's source (the CFN reporter prints code around failing values).
+struct ConsoleOptions {
+  uint32_t summary = 2;            // SummaryType bits: 1 PASS, 2 FAIL, 4 SKIP (0: -S none)
+  int32_t format = OUT_TEXT;       // OUT_TEXT (single-line-summary), OUT_JSON or OUT_YAML
+  bool verbose = false, print_json = false;
+};
+bool console_report(const DocBatch& docs, uint32_t doc, const std::string& text, const Program& prog,
+                    const TileResult& tile, const TileResult& vtile, const ConsoleOptions& opt, std::string& out,
+                    ReportError& err);
+
 struct TestCaseResult {
   bool has_name = false;
   std::string name;

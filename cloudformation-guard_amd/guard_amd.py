@@ -60,6 +60,12 @@ def lib():
                                                   ctypes.POINTER(ValidateInput), ctypes.c_size_t, ctypes.c_int32,
                                                   ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ExternError)]
     L.cfn_guard_validate_batch_params.restype = ctypes.c_void_p
+    L.cfn_guard_validate_console.argtypes = [ctypes.POINTER(ValidateInput), ctypes.c_size_t,
+                                             ctypes.POINTER(ValidateInput), ctypes.c_size_t,
+                                             ctypes.POINTER(ValidateInput), ctypes.c_size_t, ctypes.c_uint32,
+                                             ctypes.c_int32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_int32),
+                                             ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ExternError)]
+    L.cfn_guard_validate_console.restype = ctypes.c_void_p
     L.gg_session_set_params.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_size_t),
                                         ctypes.POINTER(ctypes.c_char_p), ctypes.c_size_t, ctypes.POINTER(ExternError)]
     L.gg_session_set_params.restype = ctypes.c_int32
@@ -251,6 +257,45 @@ def validate_structured(rules, data, output="json", params=None):
     if err.code != 0:
         _raise(err)
     return _take_string(p), code.value
+
+
+CONSOLE_OUTPUT_FORMATS = {"single-line-summary": 4, "json": 0, "yaml": 1}
+
+
+def summary_flags(values):
+    """--show-summary values folded as Validate::execute does (validate.rs:254-268): `none` resets"""
+    st = 0
+    for v in values:
+        if v == "none":
+            st = 0
+            continue
+        st |= {"pass": 1, "fail": 2, "skip": 4, "all": 7}[v]
+    return st
+
+
+def validate_console(rules, data, summary=("fail",), output="single-line-summary", verbose=False, print_json=False,
+                     params=None):
+    """`cfn-guard validate` without --structured (console reporters) -> (stdout, exit_code, stderr), the
+    oracle's guard_oracle.console.validate_console contract: an evaluation error returns what was written
+    before it, exit code -1 and "Error occurred <error>" in stderr; a failure before any evaluation
+    (a data or parameter file that does not load) raises GuardError."""
+    R = (ValidateInput * max(1, len(rules)))(*[ValidateInput(_b(t), _b(n)) for n, t in rules])
+    D = (ValidateInput * max(1, len(data)))(*[ValidateInput(_b(t), _b(n)) for n, t in data])
+    params = params or []
+    P = (ValidateInput * max(1, len(params)))(*[ValidateInput(_b(t), _b(n)) for n, t in params])
+    code = ctypes.c_int32(0)
+    etext = ctypes.c_void_p(None)
+    err = ExternError()
+    flags = (1 if verbose else 0) | (2 if print_json else 0)
+    p = lib().cfn_guard_validate_console(D, len(data), R, len(rules), P, len(params), summary_flags(summary),
+                                         CONSOLE_OUTPUT_FORMATS[output], flags, ctypes.byref(code), ctypes.byref(etext),
+                                         ctypes.byref(err))
+    stderr = _take_string(etext.value) if etext.value else ""
+    if not p:
+        _raise(err)
+    if err.code != 0 and err.message:
+        lib().cfn_guard_free_string(err.message)
+    return _take_string(p), code.value, stderr
 
 
 TEST_OUTPUT_FORMATS = {"text": 4, "json": 0, "yaml": 1, "junit": 3}

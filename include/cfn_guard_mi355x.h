@@ -66,6 +66,26 @@ char *cfn_guard_validate_batch_params(const validate_input_t *docs, size_t n_doc
                                       size_t n_rules, const validate_input_t *params, size_t n_params,
                                       int32_t output_format, int32_t *exit_code, extern_err_t *err);
 
+/* `cfn-guard validate [-r <rules>]+ [-d <data>]+ [-i <params>]* [-o single-line-summary|json|yaml]
+ * [-S <summary>] [--verbose] [--print-json]` -- the console reporters, not --structured
+ * (commands/validate.rs:253-487, 552-596, 690-758; reporters/validate/{summary_table,cfn,tf,
+ * generic_summary,common}.rs).  rules and docs in the CLI's walk order (file name = what the CLI
+ * prints for it); show_summary: CFN_GUARD_SUMMARY_* bits (the CLI default is _FAIL; 0 = `-S none`);
+ * output_format: CFN_GUARD_OUTPUT_TEXT (single-line-summary), _JSON or _YAML; flags:
+ * CFN_GUARD_CONSOLE_VERBOSE | CFN_GUARD_CONSOLE_PRINT_JSON.  Returns stdout (free with
+ * cfn_guard_free_string); *err_text gets stderr (rules-file parse errors, "Error occurred ..."), or NULL.
+ * *exit_code: 0 / 19 (a rule FAILed) / 5 (a rules file did not parse; the last non-zero code wins) /
+ * -1 with err set when evaluation aborted -- stdout then holds what was written before the abort. */
+#define CFN_GUARD_SUMMARY_PASS 1u
+#define CFN_GUARD_SUMMARY_FAIL 2u
+#define CFN_GUARD_SUMMARY_SKIP 4u
+#define CFN_GUARD_CONSOLE_VERBOSE 1u
+#define CFN_GUARD_CONSOLE_PRINT_JSON 2u
+char *cfn_guard_validate_console(const validate_input_t *docs, size_t n_docs, const validate_input_t *rules,
+                                 size_t n_rules, const validate_input_t *params, size_t n_params, uint32_t show_summary,
+                                 int32_t output_format, uint32_t flags, int32_t *exit_code, char **err_text,
+                                 extern_err_t *err);
+
 /* `cfn-guard test -r <rules> -t <spec files> [-o json|yaml|junit]` (commands/test.rs,
  * reporters/test/generic.rs and structured.rs): one rules file x n_specs test-spec files
  * (YAML / JSON `Vec<TestSpec>`); output_format CFN_GUARD_OUTPUT_TEXT (the default text report),

@@ -250,6 +250,11 @@ def populate(clause, parent, path_tree):
             populate(ch, path, path_tree)
 
 
+# char::is_whitespace (str::trim) -- Python's str.strip() would also take U+001C..U+001F
+_RUST_WS = "\t\n\x0b\x0c\r \x85\xa0\u1680\u2000\u2001\u2002\u2003\u2004\u2005\u2006\u2007\u2008\u2009\u200a" \
+           "\u2028\u2029\u202f\u205f\u3000"
+
+
 def emit_messages(out, prefix, message, error, width):
     """common.rs:763-824"""
     if message:
@@ -259,7 +264,7 @@ def emit_messages(out, prefix, message, error, width):
             parts = message.split("\n")
         else:
             parts = [message]
-        parts = [p.strip() for p in parts]
+        parts = [p.strip(_RUST_WS) for p in parts]
         parts = [p for p in parts if p]
         if not parts:
             raise Panic("index out of bounds: the len is 0 but the index is 0")
@@ -490,7 +495,7 @@ def _print_resources(out, data_file, rules_file, not_compliant, by_res, ew):
         out.append("}\n")
 
 
-CFN_RESOURCES = re.compile(r"^/Resources/([^/\n]+)(/?P<rest>.*$)?")
+CFN_RESOURCES = re.compile(r"^/Resources/([^/]+)(/?P<rest>.*$)?")
 
 
 def _get_resource_name(key, count, matches):
@@ -557,7 +562,7 @@ def cfn_single_line(out, data_file, text, rules_file, paths, fr):
     _print_resources(out, data_file, rules_file, nc, by_res, _CfnErr(ReadCursor(text)))
 
 
-RESOURCE_CHANGE = re.compile(r"/resource_changes/([^/\n]+)/change/after/(.*)?")
+RESOURCE_CHANGE = re.compile(r"/resource_changes/([^/]+)/change/after/(.*)?")
 
 
 def tf_single_line(out, data_file, rules_file, paths, fr):
