@@ -1705,7 +1705,7 @@ static void load_stats(const GpuLoadStats& st, double* out) {
   if (!out) return;
   out[0] = st.kernel_ms; out[1] = (double)st.nodes; out[2] = (double)st.distinct_strings;
   out[3] = (double)st.pool_bytes; out[4] = (double)st.text_bytes; out[5] = st.h2d_ms; out[6] = st.d2h_ms;
-  out[7] = (double)st.table_retries;
+  out[7] = (double)st.table_retries; out[8] = (double)st.refused_docs;
 }
 
 int32_t gg_session_add_docs_device(gg_session* s, const char* const* texts, const size_t* lens, const char* const* names,
@@ -1720,7 +1720,31 @@ int32_t gg_session_add_docs_device(gg_session* s, const char* const* texts, cons
     for (size_t i = 0; i < n; i++) nm[i] = names ? names[i] : std::string();
     GpuLoadStats st;
     DocBatch b;
-    if (!gpu_load_json(b, texts, lens, nm, n, st, why)) { set_note(err, why); return 1; }
+    std::vector<uint32_t> refused;
+    if (!gpu_load_json(b, texts, lens, nm, n, st, why, &refused)) { set_note(err, why); return 1; }
+    if (!refused.empty()) {
+      // the documents the device refused, built by the host loader (libyaml) on host threads and
+      // spliced in at their positions: their nodes are appended to the arena, strings re-interned
+      // (merge_batches), and their roots / bases moved to the placeholders the device left
+      const size_t nt = std::min<size_t>(refused.size(), report_threads());
+      std::vector<DocBatch> parts(nt);
+      std::vector<LoadError> errs(nt);
+      std::vector<int> ok(nt, 1);
+      parallel_run(nt, [&](size_t t) {
+        for (size_t j = refused.size() * t / nt; j < refused.size() * (t + 1) / nt && ok[t]; j++) {
+          const uint32_t d = refused[j];
+          if (!load_document(parts[t], texts[d], lens[d], nm[d], LOAD_LIBYAML, errs[t])) ok[t] = 0;
+        }
+      });
+      for (size_t t = 0; t < nt; t++)
+        if (!ok[t]) { set_note(err, "host loader: " + error_display(errs[t].kind, errs[t].msg)); return 1; }
+      merge_batches(b, parts);
+      for (size_t j = 0; j < refused.size(); j++) {
+        b.roots[refused[j]] = b.roots[n + j];
+        b.base[refused[j]] = b.base[n + j];
+      }
+      b.roots.resize(n); b.base.resize(n); b.names.resize(n);
+    }
     s->docs = std::move(b);
     s->uploaded = false;
     load_stats(st, stats);

@@ -19,12 +19,17 @@ struct GpuLoadStats {
   double h2d_ms = 0, d2h_ms = 0;
   uint64_t text_bytes = 0, nodes = 0, distinct_strings = 0, pool_bytes = 0;
   uint32_t table_retries = 0;   // intern-table doublings
+  uint64_t refused_docs = 0;    // documents outside the device subset, built by the host loader
 };
 
 // Appends `n` documents (texts[i] of lens[i] bytes, named names[i]) to the EMPTY batch `out`.
-// Returns false with `why` set when any document is outside the subset the device parser proves
-// identical to the host loader (the caller then loads the batch on the host); `out` is unchanged.
+// A document outside the subset the device parser proves identical to the host loader (libyaml-only
+// syntax, duplicate keys, nesting past 64, a float beyond the exact fast path, a raw character libyaml
+// reads specially) is refused on its own: with `refused` non-null its index is appended there and
+// `out` holds an empty placeholder for it (the caller builds it with the host loader); with
+// `refused` null the whole batch is refused.  Returns false with `why` set when the batch is refused
+// (batch-wide limits, or strict mode); `out` is then unchanged.
 bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, const std::vector<std::string>& names,
-                   size_t n, GpuLoadStats& st, std::string& why);
+                   size_t n, GpuLoadStats& st, std::string& why, std::vector<uint32_t>* refused = nullptr);
 
 }  // namespace gg

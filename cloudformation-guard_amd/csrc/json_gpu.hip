@@ -15,8 +15,10 @@
 //   5. fix        slots in nodes -> ids;
 //   6. verify     every occurrence's decoded bytes are compared with its id's pool bytes, so a
 //                 fingerprint collision cannot merge two strings silently (the batch is refused).
-// Anything outside the subset refuses the batch; the caller then loads it on the host, so results
-// never depend on which loader ran.
+// A document outside the subset is refused on its own (per-document flag): the passes skip it, the
+// host loader builds it (doc_loader.cpp, the libyaml path) and its nodes join the batch at the
+// document's position, so results never depend on which loader ran.  Only batch-wide limits (string
+// table or pool full, sizes) refuse the whole batch.
 #include "json_gpu.h"
 
 #include <hip/hip_runtime.h>
@@ -67,7 +69,8 @@ struct JArgs {
   uint8_t* pool;
   unsigned long long* pool_cursor;
   uint64_t pool_cap;
-  uint32_t* bad;                // first refusal reason (BAD_*), 0 = none
+  uint32_t* bad;                // batch-wide refusal (BAD_TABLE / BAD_POOL: grow and retry), 0 = none
+  uint32_t* doc_bad;            // per document: its refusal reason (BAD_*), 0 = loaded on the device
 };
 
 __device__ inline void refuse(const JArgs& A, uint32_t why) { atomicCAS(A.bad, 0u, why); }
@@ -97,14 +100,36 @@ __device__ inline uint64_t mix64(uint64_t x) {
 }
 
 // Decodes the JSON string whose opening quote is at `q`; calls sink(byte) per decoded byte.
-// Returns the index after the closing quote, or 0 when the string is outside the subset
-// (raw bytes outside 0x20..0x7E, bad escapes, surrogate \u escapes: the host path rejects them too).
+// Returns the index after the closing quote, or 0 when the string is outside the subset (bad
+// escapes, surrogate \u escapes, control bytes, malformed UTF-8, and the raw characters libyaml's
+// reader treats specially: C1 controls and U+FFFE / U+FFFF, which it rejects, and U+0085 / U+2028 /
+// U+2029, which it reads as line breaks).  Raw UTF-8 passes through as it is, as libyaml keeps it;
+// `cont` counts its continuation bytes, because libyaml's marks count characters, not bytes
+// (a mark's column = bytes since the line start - continuation bytes since it).
 template <typename Sink>
-__device__ uint64_t decode_string(Text& T, uint64_t q, Sink&& sink) {
+__device__ uint64_t decode_string(Text& T, uint64_t q, Sink&& sink, uint32_t& cont) {
   uint64_t i = q + 1;
   for (;;) {
     const uint32_t c = T.at(i);
     if (c == '"') return i + 1;
+    if (c >= 0x80u && c < 0x100u) {
+      // one UTF-8 sequence: lead byte, 1-3 continuation bytes, shortest form, a scalar value
+      const uint32_t n = c >= 0xF0u ? 3u : (c >= 0xE0u ? 2u : (c >= 0xC2u ? 1u : 0u));
+      if (!n || c > 0xF4u) return 0;
+      uint32_t cp = c & (0x3Fu >> n);
+      for (uint32_t k = 1; k <= n; k++) {
+        const uint32_t b = T.at(i + k);
+        if ((b & 0xC0u) != 0x80u) return 0;
+        cp = (cp << 6) | (b & 0x3Fu);
+      }
+      if ((n == 2 && cp < 0x800u) || (n == 3 && (cp < 0x10000u || cp > 0x10FFFFu))) return 0;
+      if (cp >= 0xD800u && cp <= 0xDFFFu) return 0;
+      if (cp < 0xA0u || cp == 0x2028u || cp == 0x2029u || cp == 0xFFFEu || cp == 0xFFFFu) return 0;
+      for (uint32_t k = 0; k <= n; k++) sink((uint8_t)T.at(i + k));
+      cont += n;
+      i += n + 1;
+      continue;
+    }
     if (c < 0x20u || c > 0x7Eu) return 0;
     if (c != '\\') { sink((uint8_t)c); i++; continue; }
     const uint32_t e = T.at(i + 1);
@@ -268,14 +293,20 @@ __device__ void parse_doc(const JArgs& A, uint32_t d) {
   Text T(A.text, b0, b1 - b0);
   uint64_t i = 0, ls = 0;
   uint32_t line = 0;
+  uint32_t cont = 0;   // UTF-8 continuation bytes since the line start (marks count characters)
   auto ws = [&]() {
     for (;;) {
       const uint32_t c = T.at(i);
       if (c == ' ') i++;
-      else if (c == '\n') { i++; line++; ls = i; }
+      else if (c == '\n') { i++; line++; ls = i; cont = 0; }
       else break;
     }
   };
+  auto column = [&]() { return (uint32_t)(i - ls) - cont; };
+  // this document is outside the subset: the passes skip it and the host loads it
+  auto bad = [&](uint32_t why) { A.doc_bad[d] = why; };
+  if (MODE == M_COUNT) { A.n_nodes[d] = 0; A.n_cont[d] = 0; A.n_str[d] = 0; }
+  else if (A.doc_bad[d]) return;
   const uint64_t nb = (MODE >= M_EMIT) ? A.node_base[d] : 0;
   const uint64_t cb = (MODE >= M_COUNTS) ? A.cont_base[d] : 0;
   uint32_t nn = 1, nc = 0, ns = 0, ci = 0, next = 1;
@@ -298,14 +329,14 @@ __device__ void parse_doc(const JArgs& A, uint32_t d) {
       end = decode_string(T, i, [&](uint8_t c) {
         if (pos >= want || A.pool[(uint64_t)id + pos] != c) same = false;
         pos++;
-      });
-      if (end && (!same || pos != want)) { refuse(A, BAD_VERIFY); return 0; }
+      }, cont);
+      if (end && (!same || pos != want)) { bad(BAD_VERIFY); return 0; }
       return end;
     }
     end = decode_string(T, i, [&](uint8_t c) {
       fp.h = (fp.h ^ c) * 0x100000001b3ull;
       fp.len++;
-    });
+    }, cont);
     if (!end) return 0;
     if (MODE == M_EMIT) {
       const uint64_t key64 = mix64(fp.h ^ ((uint64_t)fp.len * 0x9E3779B97F4A7C15ull)) | 1ull;
@@ -333,7 +364,7 @@ __device__ void parse_doc(const JArgs& A, uint32_t d) {
       return true;
     }
     if (c == '{' || c == '[') {
-      if (sp >= kMaxDepth) { refuse(A, BAD_DEPTH); return false; }
+      if (sp >= kMaxDepth) { bad(BAD_DEPTH); return false; }
       const uint32_t is_map = c == '{';
       const uint32_t k = ci++;
       nc++;
@@ -363,7 +394,7 @@ __device__ void parse_doc(const JArgs& A, uint32_t d) {
     if (MODE == M_EMIT) {
       DNode& nd = A.nodes[nb + rel];
       nd.count = 0; nd.a = 0; nd.b = 0; nd.parent = parent;
-      if (!scalar(T, i, L, nd)) { refuse(A, BAD_NUMBER); return false; }
+      if (!scalar(T, i, L, nd)) { bad(BAD_NUMBER); return false; }
     }
     i += L;
     return true;
@@ -371,27 +402,27 @@ __device__ void parse_doc(const JArgs& A, uint32_t d) {
 
   ws();
   const uint32_t c0 = T.at(i);
-  if (c0 != '{' && c0 != '[') { refuse(A, BAD_SYNTAX); return; }
+  if (c0 != '{' && c0 != '[') { bad(BAD_SYNTAX); return; }
   if (MODE == M_EMIT) {
     DNode& r = A.nodes[nb];
     r.key_off = NONE; r.key_len = 0; r.key_hash = 0;
     const bool list = c0 == '[';
-    A.line[nb] = list ? 0 : line; A.col[nb] = list ? 0 : (uint32_t)(i - ls);   // emit_root: lists keep (0,0)
+    A.line[nb] = list ? 0 : line; A.col[nb] = list ? 0 : column();   // emit_root: lists keep (0,0)
     A.kline[nb] = 0; A.kcol[nb] = 0;
   }
-  if (!value(0, NONE)) { refuse(A, BAD_SYNTAX); return; }
+  if (!value(0, NONE)) { bad(BAD_SYNTAX); return; }
   while (sp) {
     Frame& F = st[sp - 1];
     const uint32_t close = F.map ? '}' : ']';
     // one element of F
     const uint32_t cs = F.first + F.j;
     if (F.map) {
-      if (T.at(i) != '"') { refuse(A, BAD_SYNTAX); return; }
+      if (T.at(i) != '"') { bad(BAD_SYNTAX); return; }
       const uint64_t kstart = i;
-      const uint32_t kl = line, kc = (uint32_t)(i - ls);
+      const uint32_t kl = line, kc = column();
       uint32_t slot = 0, len = 0;
       const uint64_t e = string_at(cs, true, &slot, &len);
-      if (!e) { refuse(A, BAD_SYNTAX); return; }
+      if (!e) { bad(BAD_SYNTAX); return; }
       i = e;
       ns++;
       if (MODE == M_EMIT) {
@@ -400,7 +431,7 @@ __device__ void parse_doc(const JArgs& A, uint32_t d) {
         A.kline[nb + cs] = kl; A.kcol[nb + cs] = kc;
       }
       while (T.at(i) == ' ') i++;
-      if (T.at(i) != ':' || line != kl || i - kstart > 1000) { refuse(A, BAD_SYNTAX); return; }
+      if (T.at(i) != ':' || line != kl || i - kstart > 1000) { bad(BAD_SYNTAX); return; }
       i++;
       ws();
     } else if (MODE == M_EMIT) {
@@ -408,11 +439,11 @@ __device__ void parse_doc(const JArgs& A, uint32_t d) {
       nd.key_off = NONE; nd.key_len = 0; nd.key_hash = 0;
       A.kline[nb + cs] = 0; A.kcol[nb + cs] = 0;
     }
-    if (MODE == M_EMIT) { A.line[nb + cs] = line; A.col[nb + cs] = (uint32_t)(i - ls); }
+    if (MODE == M_EMIT) { A.line[nb + cs] = line; A.col[nb + cs] = column(); }
     F.j++;
     nn++;
     const uint32_t depth_before = sp;
-    if (!value(cs, F.slot)) { refuse(A, BAD_SYNTAX); return; }
+    if (!value(cs, F.slot)) { bad(BAD_SYNTAX); return; }
     if (sp > depth_before) continue;   // a nested container: its elements come first
     // after an element: ',' or the close of this container (and of every container it completes)
     for (;;) {
@@ -421,17 +452,17 @@ __device__ void parse_doc(const JArgs& A, uint32_t d) {
       ws();
       const uint32_t c = T.at(i);
       if (c == ',') { i++; ws(); break; }
-      if (c != gclose) { refuse(A, BAD_SYNTAX); return; }
+      if (c != gclose) { bad(BAD_SYNTAX); return; }
       i++;
       // container complete
       if (MODE == M_COUNTS) A.counts[cb + G.k] = G.j;
       if (MODE == M_EMIT && G.map) {
         // duplicate keys (the host fast path refuses them too; IndexMap keeps the last value)
-        if (G.j > kMaxPairwiseKeys) { refuse(A, BAD_DUPKEY); return; }
+        if (G.j > kMaxPairwiseKeys) { bad(BAD_DUPKEY); return; }
         for (uint32_t p = 1; p < G.j; p++) {
           const uint32_t kp = A.nodes[nb + G.first + p].key_hash;
           for (uint32_t q = 0; q < p; q++)
-            if (A.nodes[nb + G.first + q].key_hash == kp) { refuse(A, BAD_DUPKEY); return; }
+            if (A.nodes[nb + G.first + q].key_hash == kp) { bad(BAD_DUPKEY); return; }
         }
       }
       sp--;
@@ -440,7 +471,7 @@ __device__ void parse_doc(const JArgs& A, uint32_t d) {
     (void)close;
   }
   ws();
-  if (i != T.n) { refuse(A, BAD_SYNTAX); return; }
+  if (i != T.n) { bad(BAD_SYNTAX); return; }
   if (MODE == M_COUNT) { A.n_nodes[d] = nn; A.n_cont[d] = nc; A.n_str[d] = ns; }
 }
 
@@ -464,7 +495,8 @@ __global__ void __launch_bounds__(256) json_own_kernel(JArgs A) {
     const uint32_t doc = (uint32_t)(A.towner[s] >> 32), q = (uint32_t)A.towner[s];
     Text T(A.text, A.off[doc], A.off[doc + 1] - A.off[doc]);
     uint64_t p = at;
-    decode_string(T, q, [&](uint8_t c) { A.pool[p++] = c; });
+    uint32_t cont = 0;
+    decode_string(T, q, [&](uint8_t c) { A.pool[p++] = c; }, cont);
   }
 }
 
@@ -578,7 +610,7 @@ struct Staging {
 }  // namespace
 
 bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, const std::vector<std::string>& names,
-                   size_t n, GpuLoadStats& st, std::string& why) {
+                   size_t n, GpuLoadStats& st, std::string& why, std::vector<uint32_t>* refused) {
   static const char* kWhy[] = {"", "outside the strict-JSON subset", "nesting deeper than 64", "duplicate map keys",
                                "a float outside the exact fast path", "string table full", "string pool full",
                                "string fingerprint collision", "batch too large"};
@@ -605,12 +637,13 @@ bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, 
   JCHK(hipMemcpy(d_off.p, off.data(), (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice));
   st.h2d_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 
-  DevArr<uint32_t> d_nn, d_nc, d_ns, d_bad;
-  d_nn.alloc(n); d_nc.alloc(n); d_ns.alloc(n); d_bad.alloc(1);
+  DevArr<uint32_t> d_nn, d_nc, d_ns, d_bad, d_doc_bad, d_doc_bad0;
+  d_nn.alloc(n); d_nc.alloc(n); d_ns.alloc(n); d_bad.alloc(1); d_doc_bad.alloc(n); d_doc_bad0.alloc(n);
   JCHK(hipMemset(d_bad.p, 0, 4));
+  JCHK(hipMemset(d_doc_bad.p, 0, n * 4));
   JArgs A{};
   A.text = d_text.p; A.off = d_off.p; A.ndocs = (uint32_t)n;
-  A.n_nodes = d_nn.p; A.n_cont = d_nc.p; A.n_str = d_ns.p; A.bad = d_bad.p;
+  A.n_nodes = d_nn.p; A.n_cont = d_nc.p; A.n_str = d_ns.p; A.bad = d_bad.p; A.doc_bad = d_doc_bad.p;
   const uint32_t dgrid = grid_for(n, 256);
   float ms_total = 0, ms = 0;
   auto bad_now = [&]() {
@@ -628,6 +661,8 @@ bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, 
   JCHK(hipEventSynchronize(e1));
   JCHK(hipEventElapsedTime(&ms, e0, e1)); ms_total += ms;
   if (bad_now()) return false;
+  // the count pass's per-document refusals; a table / pool retry starts again from them
+  JCHK(hipMemcpy(d_doc_bad0.p, d_doc_bad.p, n * 4, hipMemcpyDeviceToDevice));
   std::vector<uint32_t> nn(n), nc(n), ns(n);
   JCHK(hipMemcpy(nn.data(), d_nn.p, n * 4, hipMemcpyDeviceToHost));
   JCHK(hipMemcpy(nc.data(), d_nc.p, n * 4, hipMemcpyDeviceToHost));
@@ -681,6 +716,7 @@ bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, 
     JCHK(hipMemset(d_tkey.p, 0, tslots * 8));
     JCHK(hipMemset(d_pool_cursor.p, 0, 8));
     JCHK(hipMemset(d_pool.p, 0, pool_cap + 16));
+    JCHK(hipMemcpy(d_doc_bad.p, d_doc_bad0.p, n * 4, hipMemcpyDeviceToDevice));
     A.tkey = d_tkey.p; A.tlen = d_tlen.p; A.towner = d_towner.p; A.tid = d_tid.p; A.tmask = tslots - 1;
 
     // 2. counts, 3. emit, 4. own, 5. fix, 6. verify
@@ -718,6 +754,19 @@ bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, 
     out.clear();   // refused: the batch stays empty
     return false;
   }
+  std::vector<uint32_t> doc_bad(n);
+  JCHK(hipMemcpy(doc_bad.data(), d_doc_bad.p, n * 4, hipMemcpyDeviceToHost));
+  for (size_t k = 0; k < n; k++) {
+    if (!doc_bad[k]) continue;
+    if (!refused) {   // strict: one refused document refuses the batch
+      why = doc_bad[k] < 9 ? kWhy[doc_bad[k]] : "refused";
+      resizer.join();
+      out.clear();
+      return false;
+    }
+    refused->push_back((uint32_t)k);
+  }
+  st.refused_docs = refused ? refused->size() : 0;
 
   // results to the host batch (the host keeps the reporter's columns and the intern index)
   t0 = std::chrono::steady_clock::now();

@@ -182,7 +182,8 @@ def parse_rules(text, name="r.guard"):
     return rc
 
 
-LOAD_STATS = ("kernel_ms", "nodes", "distinct_strings", "pool_bytes", "text_bytes", "h2d_ms", "d2h_ms", "table_retries")
+LOAD_STATS = ("kernel_ms", "nodes", "distinct_strings", "pool_bytes", "text_bytes", "h2d_ms", "d2h_ms", "table_retries",
+              "refused_docs")
 
 
 def _load_result(rc, err, st):

@@ -193,9 +193,13 @@ int32_t gg_session_add_synthetic(gg_session *s, uint64_t first, size_t n, int32_
  * Loader::load + PathAwareValue::try_from, guard/src/rules/libyaml/loader.rs:31-195 and
  * guard/src/rules/path_value.rs:414-478, as called from validate.rs:760-787).  Parses and interns
  * the documents on the MI355X into an EMPTY session, building the arena gg_session_add_docs builds.
- * Returns 0 when loaded, 1 when some document is outside the device subset (nothing loaded, err->message
- * says why; load the batch with gg_session_add_docs), -1 on error.  stats (may be NULL, 8 doubles):
- * kernel ms, nodes, distinct strings, pool bytes, text bytes, H2D ms, D2H ms, intern-table doublings. */
+ * A document outside the device subset (libyaml-only syntax, duplicate keys, nesting past 64, a float
+ * beyond the exact fast path, a raw character libyaml reads specially) is built by the host loader
+ * and spliced in at its position.  Returns 0 when loaded, 1 when the batch is refused as a whole
+ * (a batch-wide limit, or a refused document the host loader rejects too: nothing loaded, err->message
+ * says why; gg_session_add_docs reports the loader error), -1 on error.  stats (may be NULL, 9 doubles):
+ * kernel ms, nodes, distinct strings, pool bytes, text bytes, H2D ms, D2H ms, intern-table doublings,
+ * documents built by the host loader. */
 int32_t gg_session_add_docs_device(gg_session *s, const char *const *texts, const size_t *lens, const char *const *names,
                                    size_t n, double *stats, extern_err_t *err);
 int32_t gg_session_add_synthetic_device(gg_session *s, uint64_t first, size_t n, int32_t n_resources, int32_t nthreads,

@@ -2,8 +2,11 @@
 
 * arena parity: gg_loader_device_check builds the same documents with both loaders and compares
   every node (kind, count, links, scalars, marks, string bytes, one pool entry per distinct string);
-* refusals: documents outside the device subset refuse the whole batch, so the caller loads it on
-  the host (a YAML document, duplicate keys, nesting past 64, a float beyond the exact fast path);
+* raw UTF-8: strings with non-ASCII characters load on the device with libyaml's character-counted
+  column marks;
+* refusals: a document outside the device subset (a YAML document, duplicate keys, nesting past 64, a
+  float beyond the exact fast path, a raw character libyaml reads specially) is refused on its own:
+  the session builds it with the host loader at its position (the strict check refuses the batch);
 * end to end: a session loaded on the device reports byte-identically to one loaded on the host,
   and to the oracle.
 """
@@ -78,13 +81,56 @@ def test_arena_parity_fixture_json():
     ('{"x": 0.12345678901234567890}', "float"),
     ('{"x": 1e400}', "float"),
     ('{"x": 99999999999999999999}', "float"),
-    ('{"x": "café"}', "subset"),
     ('{"x": 1}x', "subset"),
+    ('{"x": "a\u0085b"}', "subset"),   # raw NEL: a line break to libyaml
+    ('{"x": "a\u2028b"}', "subset"),   # raw LINE SEPARATOR
+    ('{"x": "a\u0090b"}', "subset"),   # raw C1 control: libyaml rejects it
 ])
 def test_refusals(doc, why):
     rc, msg = guard_amd.loader_device_check(synth.cfn_corpus(3, n_resources=5) + [doc])
     assert rc == -1
     assert why in msg
+
+
+UTF8_DOCS = [
+    '{"x": "café", "ключ": "значение", "e": "😀 ok", "t": "中文字符", "n": "\u00a0nbsp"}',
+    '{"Resources": {"Bücket": {"Type": "AWS::S3::Bucket", "Properties": {"Tags": [{"Key": "ñame", "Value": "日本"}], '
+    '"BucketName": "x"}}}}',
+]
+
+
+def test_arena_parity_utf8():
+    """raw UTF-8 strings on the device; pretty-printed, so keys and values after a non-ASCII character
+    on the same line check the character-counted columns"""
+    docs = UTF8_DOCS + [json.dumps(json.loads(d), indent=2, ensure_ascii=False) for d in UTF8_DOCS]
+    docs += [json.dumps({"a": "é" * 40, "b": ["ü", {"c": "😀😀", "d": 1}]}, ensure_ascii=False)]
+    _check(docs)
+    for d in docs:
+        _check([d])
+
+
+def test_session_refused_documents_load_on_the_host():
+    """documents the device refuses are built by the host loader at their positions: the session's
+    report equals a host-loaded session's and the oracle's"""
+    rules = rule_pack()
+    base = synth.cfn_corpus(12, start=700, n_resources=15)
+    odd = ['Resources:\n  b:\n    Type: AWS::S3::Bucket\n    Properties: {BucketName: x}\n',
+           '{"Resources": {"a": {"Type": "AWS::S3::Bucket"}, "a": {"Type": "AWS::IAM::Role"}}}',
+           '{"Resources": {"v": {"Type": "AWS::EC2::Volume", "Properties": {"Size": 0.12345678901234567890}}}}',
+           UTF8_DOCS[1]]
+    texts = base[:3] + [odd[0]] + base[3:7] + odd[1:3] + base[7:] + [odd[3]]
+    names = ["m%d.json" % i for i in range(len(texts))]
+    s = guard_amd.Session()
+    for name, text in rules:
+        s.add_rules(text, name)
+    st = s.add_docs_device(texts, names)
+    assert st is not None and st["refused_docs"] == 3   # the YAML, duplicate-key and long-float documents
+    s.eval(1)
+    dev = s.report()
+    s.close()
+    assert dev == _session(rules, texts, names, False)
+    exp, ecode, _ = oracle_validate(rules, list(zip(names, texts)))
+    assert dev == (exp, ecode)
 
 
 def _session(rules, texts, names, device):
