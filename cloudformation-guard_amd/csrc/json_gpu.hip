@@ -304,7 +304,7 @@ __device__ void parse_doc(const JArgs& A, uint32_t d) {
   };
   auto column = [&]() { return (uint32_t)(i - ls) - cont; };
   // this document is outside the subset: the passes skip it and the host loads it
-  auto bad = [&](uint32_t why) { A.doc_bad[d] = why; };
+  auto bad = [&](uint32_t why) { if (!A.doc_bad[d]) A.doc_bad[d] = why; };   // the first reason
   if (MODE == M_COUNT) { A.n_nodes[d] = 0; A.n_cont[d] = 0; A.n_str[d] = 0; }
   else if (A.doc_bad[d]) return;
   const uint64_t nb = (MODE >= M_EMIT) ? A.node_base[d] : 0;
