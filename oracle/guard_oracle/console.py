@@ -799,7 +799,10 @@ def report_eval(out, status, root, rules_file, data_file, text, doc, output, fla
             out.extend(part)
             return
         except _Internal:
-            pass
+            pass   # raised before anything is written: the next reporter runs
+        except GuardError:
+            out.extend(part)   # a panic mid-report: what was written stays written
+            raise
     if "/resource_changes" in paths:
         if output in ("json", "yaml"):
             return structured()

@@ -78,6 +78,37 @@ def test_console_packs_vs_oracle(pack):
         assert got[0] == exp[0], (pack, opts)
 
 
+def _console_pack():
+    d = os.path.join(G, "console_rulepack")
+    rules = _pack("console_rulepack")
+    data = [(f, open(os.path.join(d, f)).read()) for f in ("cdk_template.yaml", "tf_plan.json", "plain.json")]
+    return rules, data
+
+
+def test_console_branches_vs_oracle():
+    """tests/golden/console_rulepack reaches every reporter branch: CFN resources with CDK paths and code
+    snippets (unary / binary / IN / unresolved / block / disjunction / `some` / parameterized rules with
+    messages), a Terraform plan's resource_changes (TfAware), generic data (dependent rules, a block whose
+    query cannot resolve)"""
+    rules, data = _console_pack()
+    for opts in OPTS + [{"summary": ("all",), "print_json": True}]:
+        exp = oracle_console(rules, data, **opts)
+        got = guard_amd.validate_console(rules, data, **opts)
+        assert got == exp, opts
+
+
+def test_console_terraform_unresolved_panics_like_the_reference():
+    """tf.rs single_line: a failing value that stops at .../change/after does not match
+    RESOURCE_CHANGE_EXTRACTION -> unreachable!(): the run aborts with the panic text"""
+    rules = [("tf_unresolved.guard", open(os.path.join(G, "console_rulepack", "tf_unresolved.guard.txt")).read())]
+    _, data = _console_pack()
+    exp = oracle_console(rules, data[1:2])
+    got = guard_amd.validate_console(rules, data[1:2])
+    assert exp[1] == got[1] == -1
+    assert "internal error: entered unreachable code" in exp[2] and "internal error: entered unreachable code" in got[2]
+    assert got[0] == exp[0]
+
+
 def test_console_parse_error_and_params():
     rules = [("bad.guard", "rule {"), ("db_param_port_rule.guard",
                                         open(os.path.join(G, "params", "db_param_port_rule.guard")).read())]
