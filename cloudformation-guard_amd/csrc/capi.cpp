@@ -25,6 +25,7 @@
 #include "eval_device.h"
 #include "host_format.h"
 #include "json_gpu.h"
+#include "eisel_lemire.h"
 #include "program.h"
 #include "reporter.h"
 #include "synth_corpus.h"
@@ -1606,6 +1607,16 @@ char* gg_load_dump(const char* text, size_t len, int32_t mode, extern_err_t* err
     dump_node(D, D.base[0], D.roots[0], o);
     return dup_str(o);
   } catch (std::exception& e) { set_err(err, -1, e.what()); return nullptr; }
+}
+
+// the device loader's float parser (eisel_lemire.h) on the host: 1 = *out holds the correctly rounded
+// double of the JSON number s[0..n), 0 = the loader refuses it (its document goes to the host loader)
+int32_t gg_parse_f64(const char* s, size_t n, double* out) {
+  uint64_t bits = 0;
+  if (!parse_json_f64([&](uint64_t k) -> uint32_t { return k < n ? (unsigned char)s[k] : 256u; }, (uint64_t)n, kPow5_128, bits))
+    return 0;
+  memcpy(out, &bits, 8);
+  return 1;
 }
 
 int32_t gg_regex_match(const char* pattern, const char* text, size_t len, uint32_t* stats) {

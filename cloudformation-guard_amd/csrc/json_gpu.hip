@@ -23,6 +23,10 @@
 
 #include <hip/hip_runtime.h>
 
+#define GG_HD __host__ __device__
+#define GG_POW5_QUAL __constant__
+#include "eisel_lemire.h"
+
 #include <algorithm>
 #include <chrono>
 #include <cstdlib>
@@ -198,12 +202,9 @@ __device__ uint64_t plain_len(Text& T, uint64_t i) {
 
 __device__ inline bool after_plain_ok(uint32_t c) { return c == 256u || c == ' ' || c == '\n' || c == ',' || c == ']' || c == '}'; }
 
-__constant__ double kPow10[23] = {1e0, 1e1, 1e2, 1e3, 1e4, 1e5, 1e6, 1e7, 1e8, 1e9, 1e10, 1e11,
-                                  1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
-
 // Scalar typing of a plain token (host JsonFast::v2: true / false / null, then Rust i64::from_str,
-// then f64): i64 exactly; f64 by Clinger's fast path (<= 15 significant digits, |exponent| <= 22:
-// one correctly rounded multiply or divide of two exact doubles); any other float refuses.
+// then f64::from_str): i64 exactly; f64 correctly rounded by Eisel-Lemire (eisel_lemire.h); a
+// significand it cannot decide or an infinite result refuses the document (the host loader parses it).
 __device__ bool scalar(Text& T, uint64_t i, uint64_t L, DNode& d) {
   const uint32_t c0 = T.at(i);
   if (c0 == 't') { d.kind = K_BOOL; d.a = 1; return true; }
@@ -226,35 +227,8 @@ __device__ bool scalar(Text& T, uint64_t i, uint64_t L, DNode& d) {
     d.kind = K_INT; d.a = (uint32_t)u; d.b = (uint32_t)(u >> 32);
     return true;
   }
-  uint64_t m = 0;
-  int32_t digits = 0, exp10 = 0;
-  bool frac = false;
-  uint64_t k = j;
-  for (; k < i + L; k++) {
-    const uint32_t c = T.at(k);
-    if (c == '.') { frac = true; continue; }
-    if (c == 'e' || c == 'E') break;
-    if (m == 0 && c == '0') { if (frac) exp10--; continue; }   // leading zeros
-    if (digits >= 15) return false;
-    m = m * 10ull + (c - '0');
-    digits++;
-    if (frac) exp10--;
-  }
-  if (k < i + L) {
-    k++;
-    bool eneg = false;
-    if (T.at(k) == '+' || T.at(k) == '-') { eneg = T.at(k) == '-'; k++; }
-    int32_t e = 0;
-    for (; k < i + L; k++) { e = e * 10 + (int32_t)(T.at(k) - '0'); if (e > 10000) return false; }
-    exp10 += eneg ? -e : e;
-  }
-  double v;
-  if (m == 0) v = 0.0;
-  else if (exp10 >= 0 && exp10 <= 22) v = (double)m * kPow10[exp10];
-  else if (exp10 < 0 && exp10 >= -22) v = (double)m / kPow10[-exp10];
-  else return false;
-  if (neg) v = -v;
-  const uint64_t u = (uint64_t)__double_as_longlong(v);
+  uint64_t u = 0;
+  if (!parse_json_f64([&](uint64_t k) { return T.at(i + k); }, L, kPow5_128, u)) return false;
   d.kind = K_FLOAT; d.a = (uint32_t)u; d.b = (uint32_t)(u >> 32);
   return true;
 }
@@ -612,7 +586,7 @@ struct Staging {
 bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, const std::vector<std::string>& names,
                    size_t n, GpuLoadStats& st, std::string& why, std::vector<uint32_t>* refused) {
   static const char* kWhy[] = {"", "outside the strict-JSON subset", "nesting deeper than 64", "duplicate map keys",
-                               "a float outside the exact fast path", "string table full", "string pool full",
+                               "a number the host types (beyond 64 bits, or an infinite / undecided float)", "string table full", "string pool full",
                                "string fingerprint collision", "batch too large"};
   if (!out.nodes.empty() || !out.roots.empty()) { why = "the device loader fills an empty batch"; return false; }
   if (n == 0) return true;

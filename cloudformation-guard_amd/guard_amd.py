@@ -134,6 +134,7 @@ def lib():
     L.gg_parse_rules.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(ExternError)]
     L.gg_parse_rules.restype = ctypes.c_int32
     L.gg_regex_match.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint32)]
+    L.gg_parse_f64.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_double)]
     L.gg_regex_match.restype = ctypes.c_int32
     L.gg_session_report_bytes.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int32),
                                           ctypes.POINTER(ExternError)]
@@ -152,6 +153,13 @@ def program_stats(text, name="r.guard"):
     out = (ctypes.c_uint32 * 5)()
     rc = lib().gg_program_stats(_b(text), _b(name), out)
     return rc, list(out)
+
+
+def parse_f64(text):
+    """the device loader's float parser on the host: the double, or None when it refuses the number"""
+    b = _b(text)
+    out = ctypes.c_double(0)
+    return out.value if lib().gg_parse_f64(b, len(b), ctypes.byref(out)) == 1 else None
 
 
 def regex_match(pattern, text):

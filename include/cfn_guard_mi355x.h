@@ -204,6 +204,9 @@ int32_t gg_session_add_docs_device(gg_session *s, const char *const *texts, cons
                                    size_t n, double *stats, extern_err_t *err);
 int32_t gg_session_add_synthetic_device(gg_session *s, uint64_t first, size_t n, int32_t n_resources, int32_t nthreads,
                                         double *stats, extern_err_t *err);
+/* Host diagnostic: the device loader's float parser (Eisel-Lemire, csrc/eisel_lemire.h) on the JSON
+ * number s[0..n): 1 = *out is the correctly rounded double, 0 = refused (its document loads on the host). */
+int32_t gg_parse_f64(const char *s, size_t n, double *out);
 /* 1 = the device loader builds the host loader's arena (up to string ids), 0 = differs, -1 = refused */
 int32_t gg_loader_device_check(const char *const *texts, const size_t *lens, size_t n, extern_err_t *err);
 

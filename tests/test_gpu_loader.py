@@ -56,6 +56,14 @@ def test_arena_parity_corpora():
     _check(synth.config_corpus(16, start=3, n_groups=4))
 
 
+def test_arena_parity_exact_floats():
+    """floats beyond Clinger's fast path (more than 15 digits, large exponents, subnormals) parse on the
+    device by Eisel-Lemire, bit-identical to the host loader's"""
+    _check(['{"f": [0.12345678901234567890, 2.2250738585072014e-308, 4.9e-324, 123456789012345678.5, '
+            '1.7976931348623157e308, 0.30000000000000004, 9007199254740993.0, 1e-400, 3.141592653589793238462643]}',
+            '[1.0000000000000002, 0.1e-5, 5e-324, 2.4703282292062328e-324, 6.02214076e23]'])
+
+
 def test_arena_parity_pretty_printed():
     """multi-line documents: line / column marks of keys and values"""
     docs = [json.dumps(json.loads(d), indent=k) for k, d in
@@ -78,7 +86,6 @@ def test_arena_parity_fixture_json():
     ("Resources:\n  a: 1\n", "subset"),
     ('{"a": 1, "a": 2}', "duplicate"),
     ("[" * 70 + "]" * 70, "deeper"),
-    ('{"x": 0.12345678901234567890}', "float"),
     ('{"x": 1e400}', "float"),
     ('{"x": 99999999999999999999}', "float"),
     ('{"x": 1}x', "subset"),
