@@ -123,7 +123,7 @@ def test_session_refused_documents_load_on_the_host():
     base = synth.cfn_corpus(12, start=700, n_resources=15)
     odd = ['Resources:\n  b:\n    Type: AWS::S3::Bucket\n    Properties: {BucketName: x}\n',
            '{"Resources": {"a": {"Type": "AWS::S3::Bucket"}, "a": {"Type": "AWS::IAM::Role"}}}',
-           '{"Resources": {"v": {"Type": "AWS::EC2::Volume", "Properties": {"Size": 0.12345678901234567890}}}}',
+           '{"Resources": {"v": {"Type": "AWS::EC2::Volume", "Properties": {"Size": 99999999999999999999}}}}',
            UTF8_DOCS[1]]
     texts = base[:3] + [odd[0]] + base[3:7] + odd[1:3] + base[7:] + [odd[3]]
     names = ["m%d.json" % i for i in range(len(texts))]
@@ -131,7 +131,7 @@ def test_session_refused_documents_load_on_the_host():
     for name, text in rules:
         s.add_rules(text, name)
     st = s.add_docs_device(texts, names)
-    assert st is not None and st["refused_docs"] == 3   # the YAML, duplicate-key and long-float documents
+    assert st is not None and st["refused_docs"] == 3   # the YAML, duplicate-key and beyond-u64 documents
     s.eval(1)
     dev = s.report()
     s.close()
