@@ -1,10 +1,13 @@
 """Console (non-structured) `cfn-guard validate` cases pinned by the reference's own tests
 (guard/tests/validate.rs:237-345, 405-418, 488-540) and their golden outputs
-(guard/resources/validate/output-dir/*.out, copied to tests/golden/validate/output-dir).
+(guard/resources/validate/output-dir/*.out and functions/output/*.out, copied to
+tests/golden/validate/output-dir and tests/golden/validate/functions/output).
 
-Each case: (name, rules [(name, text)], data [(name, text)], options, expected stdout, exit code).
+Each case: (name, rules [(name, text)], data [(name, text)], options, expected stdout, exit code,
+needs look-around).  expected None: the reference test asserts the exit code only.
 Data names are the file names the tests' sanitize_path leaves of the CLI's canonical paths
 (tests/utils.rs:130-150); data read from stdin is named STDIN (validate.rs:303-312)."""
+import json
 import os
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "validate")
@@ -81,5 +84,65 @@ def cases():
          {"verbose": True}, _out("payload_verbose_non_compliant.out"), 19, False),
         ("stdin_verbose_yaml", _rules(pr), _stdin("s3-public-read-prohibited-template-compliant.yaml"),
          {"verbose": True, "output": "yaml"}, _out("payload_verbose_yaml_compliant.out"), 0, False),
+        # validate.rs:733-749: a count() over an unresolved query compared with a literal
+        ("failing_count_show_summary_all", _fn_rules("count_with_message.guard"), _fn_data(), all_,
+         _fn_out("failing_count_show_summary_all.out"), 19, False),
+        # validate.rs:709-731 (the count() member of test_validate_with_fn_expr_success)
+        ("fn_expr_success_count", _fn_rules("count.guard"), _fn_data(), allv, None, 0, False),
+        # validate.rs:566-597: --payload, data / rules named DATA_STDIN[i] / RULES_STDIN[i]
+        ("payload_flag_fail", *_payload(PAYLOAD_FAIL), {}, PAYLOAD_FAIL_OUT, 19, False),
+        ("payload_flag", *_payload(PAYLOAD_OK), {}, None, 0, False),
     ]
+    # validate.rs:788-807: rules-dir (one look-behind rule) against a non-compliant template
+    for ss in (("pass", "fail"), ("skip", "fail"), ("skip", "pass")):
+        c.append(("show_summary_" + "_".join(ss),
+                  _rules(*["rules-dir/" + f for f in _dir("rules-dir", (".guard", ".ruleset"))]),
+                  _data("data-dir/s3-public-read-prohibited-template-non-compliant.yaml"),
+                  {"summary": ss}, None, 19, True))
     return c
+
+
+FN = os.path.join(GOLD, "functions")
+
+
+def _fn_rules(*names):
+    out = []
+    for n in names:
+        with open(os.path.join(FN, "rules", n)) as f:
+            out.append((n, f.read()))
+    return out
+
+
+def _fn_data():
+    with open(os.path.join(FN, "data", "template.yaml")) as f:
+        return [("template.yaml", f.read())]
+
+
+def _fn_out(name):
+    with open(os.path.join(FN, "output", name)) as f:
+        return f.read()
+
+
+def _payload(text):
+    """validate.rs:438-464: the payload's data / rules strings, named by position"""
+    p = json.loads(text)
+    return ([("RULES_STDIN[%d]" % (i + 1), r) for i, r in enumerate(p["rules"])],
+            [("DATA_STDIN[%d]" % (i + 1), d) for i, d in enumerate(p["data"])])
+
+
+# validate.rs:568, 584: both payloads carry this document twice
+_VOL = ('{"Resources":{"NewVolume":{"Type":"AWS::EC2::Volume","Properties":{"Size":500,"Encrypted":false,'
+        '"AvailabilityZone":"us-west-2b"}},"NewVolume2":{"Type":"AWS::EC2::Volume","Properties":{"Size":50,'
+        '"Encrypted":false,"AvailabilityZone":"us-west-2c"}}},"Parameters":{"InstanceName":"TestInstance"}}')
+PAYLOAD_OK = json.dumps({"data": [_VOL, _VOL], "rules": ['Parameters.InstanceName == "TestInstance"'] * 2})
+PAYLOAD_FAIL = json.dumps({"data": [_VOL, _VOL], "rules": ['Parameters.InstanceName == "TestInstance"',
+                                                           'Parameters.InstanceName == "SomeRandomString"']})
+PAYLOAD_FAIL_OUT = "".join(
+    "DATA_STDIN[%d] Status = FAIL\n"
+    "FAILED rules\n"
+    "RULES_STDIN[2]/default    FAIL\n"
+    "---\n"
+    "Evaluating data DATA_STDIN[%d] against rules RULES_STDIN[2]\n"
+    "Number of non-compliant resources 0\n" % (i, i) for i in (1, 2))
+# validate.rs:555-564: a type block over a query that resolves nothing -> an evaluation error (exit -1)
+PAYLOAD_TYPE_BLOCK = json.dumps({"data": ["{}"], "rules": ["d1z::Y\n\t\tm<0m<03333333"]})

@@ -18,7 +18,16 @@ def test_console_golden(case):
     name, rules, data, opts, expected, code, _ = case
     out, rc, err = validate_console(rules, data, **opts)
     assert rc == code, err
-    assert out == expected
+    if expected is not None:
+        assert out == expected
+
+
+def test_payload_type_block_over_nothing_is_an_evaluation_error():
+    # validate.rs:555-564: exit INTERNAL_FAILURE, nothing on stdout
+    rules, data = console_cases._payload(console_cases.PAYLOAD_TYPE_BLOCK)
+    out, rc, err = validate_console(rules, data)
+    assert (out, rc) == ("", -1)
+    assert "Unable to resolve type block query: d1z::Y" in err
 
 
 def test_summary_flags_fold():
