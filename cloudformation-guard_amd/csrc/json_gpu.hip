@@ -2,9 +2,12 @@
 //
 // One lane parses one document (documents are a few KB; a lane walks its text through a 16-byte
 // window, so each load serves 16 bytes).  Passes, each a kernel over all documents:
-//   1. count      validate the subset the host fast path accepts (doc_loader.cpp load_json_fast)
-//                 and count nodes, containers, string occurrences;
-//   2. counts     the child count of every container, in pre-order (host: JsonFast::v1);
+//   1. count      validate the subset the host fast path accepts (doc_loader.cpp load_json_fast),
+//                 count nodes, containers, string occurrences, and record the child count of every
+//                 container, in pre-order (host: JsonFast::v1), as 16-bit counts at a document's
+//                 half text offset (a container takes two bytes at least, so a document's counts
+//                 never reach the next one's);
+//   2. (folded into 1)
 //   3. emit       the nodes in the host layout -- each container's children contiguous, blocks in
 //                 DFS pre-order (host: JsonFast::v2) -- with marks, scalar typing, and every
 //                 string inserted into a device hash table keyed by a 64-bit fingerprint of its
@@ -34,6 +37,13 @@
 #include <stdexcept>
 #include <thread>
 
+#ifndef GG_JDIAG_NODUP
+#define GG_JDIAG_NODUP 0   // diagnostic A/B builds only: skip the duplicate-key check
+#endif
+#ifndef GG_JDIAG_NOINTERN
+#define GG_JDIAG_NOINTERN 0   // diagnostic A/B builds only: skip the intern table
+#endif
+
 namespace gg {
 namespace {
 
@@ -42,7 +52,7 @@ namespace {
 enum : uint32_t { M_COUNT = 0, M_COUNTS = 1, M_EMIT = 2, M_VERIFY = 3 };
 enum : uint32_t {
   BAD_NONE = 0, BAD_SYNTAX = 1, BAD_DEPTH = 2, BAD_DUPKEY = 3, BAD_NUMBER = 4, BAD_TABLE = 5, BAD_POOL = 6,
-  BAD_VERIFY = 7, BAD_SIZE = 8,
+  BAD_VERIFY = 7, BAD_SIZE = 8, BAD_WIDE = 9,
 };
 static const uint32_t kMaxDepth = 64;
 static const uint32_t kMaxPairwiseKeys = 256;
@@ -57,8 +67,7 @@ struct JArgs {
   uint32_t* n_str;
   // pass 2 / 3 inputs
   const uint64_t* node_base;    // per document: first node
-  const uint64_t* cont_base;    // per document: first container count
-  uint32_t* counts;
+  uint16_t* counts;             // child counts: document d's container k at off[d] / 2 + k
   DNode* nodes;
   uint32_t* line;
   uint32_t* col;
@@ -94,6 +103,31 @@ struct Text {
     const uint32_t word = k < 4 ? w.x : (k < 8 ? w.y : (k < 12 ? w.z : w.w));
     return (word >> ((k & 3u) * 8u)) & 0xFFu;
   }
+  // bit 7 of each byte of x set where the byte ends a plain string run: '"', '\\', a control
+  // byte (< 0x20), DEL or a non-ASCII byte (SWAR; only the lowest flagged byte is exact, which is
+  // the one plain_run uses)
+  __device__ static uint32_t special(uint32_t x) {
+    const uint32_t q = x ^ 0x22222222u, b = x ^ 0x5C5C5C5Cu, d = x ^ 0x7F7F7F7Fu;
+    const uint32_t zq = (q - 0x01010101u) & ~q, zb = (b - 0x01010101u) & ~b, zd = (d - 0x01010101u) & ~d;
+    const uint32_t lt = (x - 0x20202020u) & ~x;
+    return (zq | zb | zd | lt | x) & 0x80808080u;
+  }
+  // the number of plain printable ASCII bytes from i to the first special byte, the end of i's
+  // 16-byte block or the end of the document (0 when byte i is special)
+  __device__ uint32_t plain_run(uint64_t i) {
+    if (i >= n) return 0;
+    const uint64_t g = base + i, a = g & ~15ull;
+    if (a != wb) { w = *(const uint4*)(s + a); wb = a; }
+    const uint32_t k = (uint32_t)(g - a);
+    uint64_t lo = (uint64_t)special(w.x) | ((uint64_t)special(w.y) << 32);
+    uint64_t hi = (uint64_t)special(w.z) | ((uint64_t)special(w.w) << 32);
+    if (k < 8) lo &= ~0ull << (8u * k);
+    else { lo = 0; hi &= ~0ull << (8u * (k - 8u)); }
+    const uint32_t first = lo ? (uint32_t)__builtin_ctzll(lo) >> 3 : (hi ? 8u + ((uint32_t)__builtin_ctzll(hi) >> 3) : 16u);
+    const uint64_t left = n - i;
+    const uint32_t r = first - k;
+    return left < r ? (uint32_t)left : r;
+  }
 };
 
 __device__ inline uint64_t mix64(uint64_t x) {
@@ -110,10 +144,18 @@ __device__ inline uint64_t mix64(uint64_t x) {
 // U+2029, which it reads as line breaks).  Raw UTF-8 passes through as it is, as libyaml keeps it;
 // `cont` counts its continuation bytes, because libyaml's marks count characters, not bytes
 // (a mark's column = bytes since the line start - continuation bytes since it).
-template <typename Sink>
+// BYTES: the sink reads the decoded bytes (false: only the end of the string matters, and plain
+// runs are skipped a 16-byte block at a time)
+template <bool BYTES = true, typename Sink>
 __device__ uint64_t decode_string(Text& T, uint64_t q, Sink&& sink, uint32_t& cont) {
   uint64_t i = q + 1;
   for (;;) {
+    const uint32_t r = T.plain_run(i);
+    if (r) {
+      if (BYTES) for (uint32_t u = 0; u < r; u++) sink((uint8_t)T.at(i + u));
+      i += r;
+      continue;
+    }
     const uint32_t c = T.at(i);
     if (c == '"') return i + 1;
     if (c >= 0x80u && c < 0x100u) {
@@ -259,6 +301,7 @@ struct Frame {
   uint32_t slot;    // the container's own node (document-relative)
   uint32_t k;       // pre-order container index
   uint32_t map;     // 1 map, 0 list
+  uint32_t bloom[4];   // EMIT, maps: 128-bit filter of the key slots seen so far
 };
 
 template <uint32_t MODE>
@@ -282,7 +325,7 @@ __device__ void parse_doc(const JArgs& A, uint32_t d) {
   if (MODE == M_COUNT) { A.n_nodes[d] = 0; A.n_cont[d] = 0; A.n_str[d] = 0; }
   else if (A.doc_bad[d]) return;
   const uint64_t nb = (MODE >= M_EMIT) ? A.node_base[d] : 0;
-  const uint64_t cb = (MODE >= M_COUNTS) ? A.cont_base[d] : 0;
+  const uint64_t cb = b0 >> 1;
   uint32_t nn = 1, nc = 0, ns = 0, ci = 0, next = 1;
   Frame st[kMaxDepth];
   uint32_t sp = 0;
@@ -298,23 +341,39 @@ __device__ void parse_doc(const JArgs& A, uint32_t d) {
       const DNode& nd = A.nodes[nb + rel];
       const uint32_t id = key ? nd.key_off : nd.a;
       const uint32_t want = key ? nd.key_len : nd.count;
-      uint32_t pos = 0;
+      // compared 4 bytes at a time: a pool string is 16-byte aligned and zero padded (json_own_kernel)
+      uint32_t pos = 0, word = 0;
       bool same = true;
+      const uint32_t* pw = (const uint32_t*)(A.pool + id);
       end = decode_string(T, i, [&](uint8_t c) {
-        if (pos >= want || A.pool[(uint64_t)id + pos] != c) same = false;
+        word |= (uint32_t)c << ((pos & 3u) * 8u);
         pos++;
+        if ((pos & 3u) == 0) {
+          if (pos > want || pw[(pos >> 2) - 1] != word) same = false;
+          word = 0;
+        }
       }, cont);
+      if (end && (pos & 3u) && (pos > want || pw[pos >> 2] != word)) same = false;
       if (end && (!same || pos != want)) { bad(BAD_VERIFY); return 0; }
       return end;
     }
-    end = decode_string(T, i, [&](uint8_t c) {
-      fp.h = (fp.h ^ c) * 0x100000001b3ull;
+    // fingerprint of the decoded bytes, 4 at a time (the device table's own key: nothing outside
+    // this loader compares it)
+    uint32_t word = 0;
+    end = decode_string<MODE == M_EMIT>(T, i, [&](uint8_t c) {
+      word |= (uint32_t)c << ((fp.len & 3u) * 8u);
       fp.len++;
+      if ((fp.len & 3u) == 0) { fp.h = (fp.h ^ word) * 0x100000001b3ull; word = 0; }
     }, cont);
     if (!end) return 0;
+    fp.h = (fp.h ^ word) * 0x100000001b3ull;
     if (MODE == M_EMIT) {
       const uint64_t key64 = mix64(fp.h ^ ((uint64_t)fp.len * 0x9E3779B97F4A7C15ull)) | 1ull;
+#if GG_JDIAG_NOINTERN
+      const uint32_t s = (uint32_t)key64 & 1023u;
+#else
       const uint32_t s = intern_slot(A, key64, fp.len, d, (uint32_t)i);
+#endif
       if (s == ~0u) { refuse(A, BAD_TABLE); return 0; }
       *slot_out = s;
       *len_out = fp.len;
@@ -356,10 +415,11 @@ __device__ void parse_doc(const JArgs& A, uint32_t d) {
       ws();
       if (T.at(i) == (is_map ? (uint32_t)'}' : (uint32_t)']')) {
         i++;
-        if (MODE == M_COUNTS) A.counts[cb + k] = 0;
+        if (MODE == M_COUNT) A.counts[cb + k] = 0;
         return true;
       }
       st[sp].first = first; st[sp].j = 0; st[sp].slot = rel; st[sp].k = k; st[sp].map = is_map;
+      if (MODE == M_EMIT && is_map) { st[sp].bloom[0] = 0; st[sp].bloom[1] = 0; st[sp].bloom[2] = 0; st[sp].bloom[3] = 0; }
       sp++;
       return true;
     }
@@ -403,6 +463,18 @@ __device__ void parse_doc(const JArgs& A, uint32_t d) {
         DNode& nd = A.nodes[nb + cs];
         nd.key_off = slot; nd.key_len = len; nd.key_hash = slot;
         A.kline[nb + cs] = kl; A.kcol[nb + cs] = kc;
+#if !GG_JDIAG_NODUP
+        // duplicate keys (the host fast path refuses them too; IndexMap keeps the last value): the
+        // earlier keys of this map are compared only when the map's filter has seen this slot's bit
+        if (F.j >= kMaxPairwiseKeys) { bad(BAD_DUPKEY); return; }
+        const uint32_t bit = (slot ^ (slot >> 7) ^ (slot >> 14)) & 127u;
+        uint32_t& bw = F.bloom[bit >> 5];
+        if ((bw >> (bit & 31u)) & 1u) {
+          for (uint32_t q = 0; q < F.j; q++)
+            if (A.nodes[nb + F.first + q].key_hash == slot) { bad(BAD_DUPKEY); return; }
+        }
+        bw |= 1u << (bit & 31u);
+#endif
       }
       while (T.at(i) == ' ') i++;
       if (T.at(i) != ':' || line != kl || i - kstart > 1000) { bad(BAD_SYNTAX); return; }
@@ -429,15 +501,9 @@ __device__ void parse_doc(const JArgs& A, uint32_t d) {
       if (c != gclose) { bad(BAD_SYNTAX); return; }
       i++;
       // container complete
-      if (MODE == M_COUNTS) A.counts[cb + G.k] = G.j;
-      if (MODE == M_EMIT && G.map) {
-        // duplicate keys (the host fast path refuses them too; IndexMap keeps the last value)
-        if (G.j > kMaxPairwiseKeys) { bad(BAD_DUPKEY); return; }
-        for (uint32_t p = 1; p < G.j; p++) {
-          const uint32_t kp = A.nodes[nb + G.first + p].key_hash;
-          for (uint32_t q = 0; q < p; q++)
-            if (A.nodes[nb + G.first + q].key_hash == kp) { bad(BAD_DUPKEY); return; }
-        }
+      if (MODE == M_COUNT) {
+        if (G.j > 0xFFFFu) { bad(BAD_WIDE); return; }
+        A.counts[cb + G.k] = (uint16_t)G.j;
       }
       sp--;
       if (!sp) break;
@@ -587,7 +653,7 @@ bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, 
                    size_t n, GpuLoadStats& st, std::string& why, std::vector<uint32_t>* refused) {
   static const char* kWhy[] = {"", "outside the strict-JSON subset", "nesting deeper than 64", "duplicate map keys",
                                "a number the host types (beyond 64 bits, or an infinite / undecided float)", "string table full", "string pool full",
-                               "string fingerprint collision", "batch too large"};
+                               "string fingerprint collision", "batch too large", "a container with more than 65535 elements"};
   if (!out.nodes.empty() || !out.roots.empty()) { why = "the device loader fills an empty batch"; return false; }
   if (n == 0) return true;
   if (n > 0xFFFFFFF0ull) { why = kWhy[BAD_SIZE]; return false; }
@@ -618,12 +684,14 @@ bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, 
   JArgs A{};
   A.text = d_text.p; A.off = d_off.p; A.ndocs = (uint32_t)n;
   A.n_nodes = d_nn.p; A.n_cont = d_nc.p; A.n_str = d_ns.p; A.bad = d_bad.p; A.doc_bad = d_doc_bad.p;
+  DevArr<uint16_t> d_counts; d_counts.alloc(total / 2 + 1);
+  A.counts = d_counts.p;
   const uint32_t dgrid = grid_for(n, 256);
   float ms_total = 0, ms = 0;
   auto bad_now = [&]() {
     uint32_t b = 0;
     JCHK(hipMemcpy(&b, d_bad.p, 4, hipMemcpyDeviceToHost));
-    if (b) why = b < 9 ? kWhy[b] : "refused";
+    if (b) why = b < 10 ? kWhy[b] : "refused";
     return b != 0;
   };
 
@@ -641,12 +709,12 @@ bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, 
   JCHK(hipMemcpy(nn.data(), d_nn.p, n * 4, hipMemcpyDeviceToHost));
   JCHK(hipMemcpy(nc.data(), d_nc.p, n * 4, hipMemcpyDeviceToHost));
   JCHK(hipMemcpy(ns.data(), d_ns.p, n * 4, hipMemcpyDeviceToHost));
-  std::vector<uint64_t> nbase(n), cbase(n);
-  uint64_t N = 0, C = 0, S = 0;
+  std::vector<uint64_t> nbase(n);
+  uint64_t N = 0, S = 0;
   for (size_t k = 0; k < n; k++) {
     if (nn[k] > kMaxDocNodes) { why = kWhy[BAD_SIZE]; return false; }
-    nbase[k] = N; cbase[k] = C;
-    N += nn[k]; C += nc[k]; S += ns[k];
+    nbase[k] = N;
+    N += nn[k]; S += ns[k];
   }
   // the host columns are sized (zero-filled: page faults, seconds at 1M documents) while the
   // device passes run; one thread per column
@@ -657,11 +725,9 @@ bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, 
     a.join(); b.join();
   });
   struct Joiner { std::thread& t; ~Joiner() { if (t.joinable()) t.join(); } } join_resizer{resizer};
-  DevArr<uint64_t> d_nbase, d_cbase;
-  d_nbase.alloc(n); d_cbase.alloc(n);
+  DevArr<uint64_t> d_nbase;
+  d_nbase.alloc(n);
   JCHK(hipMemcpy(d_nbase.p, nbase.data(), n * 8, hipMemcpyHostToDevice));
-  JCHK(hipMemcpy(d_cbase.p, cbase.data(), n * 8, hipMemcpyHostToDevice));
-  DevArr<uint32_t> d_counts; d_counts.alloc(C);
   DevArr<DNode> d_nodes; d_nodes.alloc(N);
   DevArr<uint32_t> d_line, d_col, d_kline, d_kcol;
   d_line.alloc(N); d_col.alloc(N); d_kline.alloc(N); d_kcol.alloc(N);
@@ -681,7 +747,7 @@ bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, 
   const uint64_t pool_max = std::min<uint64_t>(total + 16 * S + 16, 0xF0000000ull);
   uint64_t pool_cap = std::min<uint64_t>(std::max<uint64_t>(total / 4, 1ull << 20), pool_max);
   DevArr<uint8_t> d_pool;
-  A.node_base = d_nbase.p; A.cont_base = d_cbase.p; A.counts = d_counts.p; A.nodes = d_nodes.p;
+  A.node_base = d_nbase.p; A.nodes = d_nodes.p;
   A.line = d_line.p; A.col = d_col.p; A.kline = d_kline.p; A.kcol = d_kcol.p;
   for (;;) {
     if (d_pool.n != pool_cap + 16) d_pool.alloc(pool_cap + 16);
@@ -693,13 +759,16 @@ bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, 
     JCHK(hipMemcpy(d_doc_bad.p, d_doc_bad0.p, n * 4, hipMemcpyDeviceToDevice));
     A.tkey = d_tkey.p; A.tlen = d_tlen.p; A.towner = d_towner.p; A.tid = d_tid.p; A.tmask = tslots - 1;
 
-    // 2. counts, 3. emit, 4. own, 5. fix, 6. verify
+    // 3. emit, 4. own, 5. fix, 6. verify
     JCHK(hipEventRecord(e0));
-    hipLaunchKernelGGL(json_pass_kernel<M_COUNTS>, dim3(dgrid), dim3(256), 0, 0, A);
     hipLaunchKernelGGL(json_pass_kernel<M_EMIT>, dim3(dgrid), dim3(256), 0, 0, A);
+#if !GG_JDIAG_NOINTERN
     hipLaunchKernelGGL(json_own_kernel, dim3(grid_for(tslots, 256)), dim3(256), 0, 0, A);
     hipLaunchKernelGGL(json_fix_kernel, dim3(grid_for(N, 256)), dim3(256), 0, 0, A, N);
     hipLaunchKernelGGL(json_pass_kernel<M_VERIFY>, dim3(dgrid), dim3(256), 0, 0, A);
+#else
+    { const uint32_t diag = BAD_SIZE; JCHK(hipMemcpy(d_bad.p, &diag, 4, hipMemcpyHostToDevice)); }
+#endif
     JCHK(hipGetLastError());
     JCHK(hipEventRecord(e1));
     JCHK(hipEventSynchronize(e1));
@@ -733,7 +802,7 @@ bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, 
   for (size_t k = 0; k < n; k++) {
     if (!doc_bad[k]) continue;
     if (!refused) {   // strict: one refused document refuses the batch
-      why = doc_bad[k] < 9 ? kWhy[doc_bad[k]] : "refused";
+      why = doc_bad[k] < 10 ? kWhy[doc_bad[k]] : "refused";
       resizer.join();
       out.clear();
       return false;

@@ -56,6 +56,13 @@ def test_arena_parity_corpora():
     _check(synth.config_corpus(16, start=3, n_groups=4))
 
 
+def test_arena_parity_wide_maps():
+    """maps of 50-250 distinct keys (the duplicate-key filter sees colliding bits) and a 65535-element list"""
+    docs = ["{" + ", ".join('"key-%d-%d": %d' % (n, i, i) for i in range(n)) + "}" for n in (50, 130, 250)]
+    docs.append("[" + ",".join(["0"] * 65535) + "]")
+    _check(docs)
+
+
 def test_arena_parity_exact_floats():
     """floats beyond Clinger's fast path (more than 15 digits, large exponents, subnormals) parse on the
     device by Eisel-Lemire, bit-identical to the host loader's"""
@@ -92,6 +99,8 @@ def test_arena_parity_fixture_json():
     ('{"x": "a\u0085b"}', "subset"),   # raw NEL: a line break to libyaml
     ('{"x": "a\u2028b"}', "subset"),   # raw LINE SEPARATOR
     ('{"x": "a\u0090b"}', "subset"),   # raw C1 control: libyaml rejects it
+    ("{" + ", ".join('"k%d": %d' % (i, i) for i in range(100)) + ', "k37": 0}', "duplicate"),   # past the key filter
+    ("[" + ",".join(["1"] * 70000) + "]", "65535"),   # child counts are 16-bit on the device
 ])
 def test_refusals(doc, why):
     rc, msg = guard_amd.loader_device_check(synth.cfn_corpus(3, n_resources=5) + [doc])
