@@ -1,23 +1,23 @@
 // GPU document loader: strict-JSON text -> columnar node arena (see json_gpu.h).
 //
 // One lane parses one document (documents are a few KB; a lane walks its text through a 16-byte
-// window, so each load serves 16 bytes).  Passes, each a kernel over all documents:
+// window, so each load serves 16 bytes, and skips plain string runs a window at a time).  Passes:
 //   1. count      validate the subset the host fast path accepts (doc_loader.cpp load_json_fast),
 //                 count nodes, containers, string occurrences, and record the child count of every
 //                 container, in pre-order (host: JsonFast::v1), as 16-bit counts at a document's
 //                 half text offset (a container takes two bytes at least, so a document's counts
 //                 never reach the next one's);
-//   2. (folded into 1)
-//   3. emit       the nodes in the host layout -- each container's children contiguous, blocks in
+//   2. emit       the nodes in the host layout -- each container's children contiguous, blocks in
 //                 DFS pre-order (host: JsonFast::v2) -- with marks, scalar typing, and every
 //                 string inserted into a device hash table keyed by a 64-bit fingerprint of its
-//                 decoded bytes; nodes carry table slots for now; duplicate map keys are refused;
-//   4. own        every occupied slot copies its first occurrence's decoded bytes into the pool
+//                 decoded bytes; nodes carry table slots for now and each string occurrence's text
+//                 offset; duplicate map keys are refused (a per-map slot filter, then a scan);
+//   3. own        every occupied slot copies its first occurrence's decoded bytes into the pool
 //                 (16-byte aligned, zero padded: the evaluator compares in 16-byte chunks); the
 //                 pool offset is the string id, as on the host;
-//   5. fix        slots in nodes -> ids;
-//   6. verify     every occurrence's decoded bytes are compared with its id's pool bytes, so a
-//                 fingerprint collision cannot merge two strings silently (the batch is refused).
+//   4. fix+verify one wave per document over its nodes: slots -> ids, and every occurrence's
+//                 decoded bytes compared with its id's pool bytes, so a fingerprint collision
+//                 cannot merge two strings silently (the document is refused).
 // A document outside the subset is refused on its own (per-document flag): the passes skip it, the
 // host loader builds it (doc_loader.cpp, the libyaml path) and its nodes join the batch at the
 // document's position, so results never depend on which loader ran.  Only batch-wide limits (string
@@ -49,13 +49,24 @@ namespace {
 
 #define JCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) throw std::runtime_error(std::string("HIP: ") + hipGetErrorString(e_)); } while (0)
 
-enum : uint32_t { M_COUNT = 0, M_COUNTS = 1, M_EMIT = 2, M_VERIFY = 3 };
+enum : uint32_t { M_COUNT = 0, M_EMIT = 2 };
 enum : uint32_t {
   BAD_NONE = 0, BAD_SYNTAX = 1, BAD_DEPTH = 2, BAD_DUPKEY = 3, BAD_NUMBER = 4, BAD_TABLE = 5, BAD_POOL = 6,
   BAD_VERIFY = 7, BAD_SIZE = 8, BAD_WIDE = 9,
 };
 static const uint32_t kMaxDepth = 64;
 static const uint32_t kMaxPairwiseKeys = 256;
+
+// the emit pass's output per node: the node and its marks in one 64-byte record, so a lane writes
+// one line per node instead of seven scattered streams; the fix / verify pass splits the records
+// into the arena's columns with coalesced stores
+struct NodeRec {
+  DNode n;
+  uint32_t line, col, kline, kcol;
+  uint32_t kpos, vpos;   // document offsets of the key's and the string value's opening quotes
+  uint32_t pad0, pad1;
+};
+static_assert(sizeof(NodeRec) == 64, "one 64-byte record per node");
 
 struct JArgs {
   const uint8_t* text;          // all documents, 16 zero bytes of padding at the end
@@ -68,6 +79,7 @@ struct JArgs {
   // pass 2 / 3 inputs
   const uint64_t* node_base;    // per document: first node
   uint16_t* counts;             // child counts: document d's container k at off[d] / 2 + k
+  NodeRec* recs;                // emit -> fix / verify
   DNode* nodes;
   uint32_t* line;
   uint32_t* col;
@@ -82,6 +94,7 @@ struct JArgs {
   uint8_t* pool;
   unsigned long long* pool_cursor;
   uint64_t pool_cap;
+  uint64_t fp_mask;             // fingerprint bits kept (~0; tests narrow it to force collisions)
   uint32_t* bad;                // batch-wide refusal (BAD_TABLE / BAD_POOL: grow and retry), 0 = none
   uint32_t* doc_bad;            // per document: its refusal reason (BAD_*), 0 = loaded on the device
 };
@@ -330,33 +343,11 @@ __device__ void parse_doc(const JArgs& A, uint32_t d) {
   Frame st[kMaxDepth];
   uint32_t sp = 0;
 
-  // a string occurrence at i (the opening quote), for node `rel` (key or value): returns the
-  // index after it, 0 on refusal; EMIT -> *slot; VERIFY compares with the pool
-  auto string_at = [&](uint32_t rel, bool key, uint32_t* slot_out, uint32_t* len_out) -> uint64_t {
+  // a string occurrence at i (the opening quote): returns the index after it, 0 on refusal;
+  // EMIT -> its intern table slot and decoded length
+  auto string_at = [&](uint32_t* slot_out, uint32_t* len_out) -> uint64_t {
     Fp fp;
-    uint32_t h32 = 0;
-    (void)h32;
     uint64_t end;
-    if (MODE == M_VERIFY) {
-      const DNode& nd = A.nodes[nb + rel];
-      const uint32_t id = key ? nd.key_off : nd.a;
-      const uint32_t want = key ? nd.key_len : nd.count;
-      // compared 4 bytes at a time: a pool string is 16-byte aligned and zero padded (json_own_kernel)
-      uint32_t pos = 0, word = 0;
-      bool same = true;
-      const uint32_t* pw = (const uint32_t*)(A.pool + id);
-      end = decode_string(T, i, [&](uint8_t c) {
-        word |= (uint32_t)c << ((pos & 3u) * 8u);
-        pos++;
-        if ((pos & 3u) == 0) {
-          if (pos > want || pw[(pos >> 2) - 1] != word) same = false;
-          word = 0;
-        }
-      }, cont);
-      if (end && (pos & 3u) && (pos > want || pw[pos >> 2] != word)) same = false;
-      if (end && (!same || pos != want)) { bad(BAD_VERIFY); return 0; }
-      return end;
-    }
     // fingerprint of the decoded bytes, 4 at a time (the device table's own key: nothing outside
     // this loader compares it)
     uint32_t word = 0;
@@ -368,7 +359,7 @@ __device__ void parse_doc(const JArgs& A, uint32_t d) {
     if (!end) return 0;
     fp.h = (fp.h ^ word) * 0x100000001b3ull;
     if (MODE == M_EMIT) {
-      const uint64_t key64 = mix64(fp.h ^ ((uint64_t)fp.len * 0x9E3779B97F4A7C15ull)) | 1ull;
+      const uint64_t key64 = (mix64(fp.h ^ ((uint64_t)fp.len * 0x9E3779B97F4A7C15ull)) & A.fp_mask) | 1ull;
 #if GG_JDIAG_NOINTERN
       const uint32_t s = (uint32_t)key64 & 1023u;
 #else
@@ -381,19 +372,30 @@ __device__ void parse_doc(const JArgs& A, uint32_t d) {
     return end;
   };
 
+  // EMIT: the element being emitted -- its key (table slot and length; NONE: no key), the key's
+  // offset and mark, and the value's mark
+  uint32_t ekey = NONE, elen = 0, ekpos = 0, ekl = 0, ekc = 0, eline = 0, ecol = 0;
+  // EMIT: node `rel` and its marks, whole, in one record
+  auto put = [&](uint32_t rel, DNode nd, uint32_t parent, uint32_t vpos) {
+    nd.key_off = ekey; nd.key_len = elen; nd.key_hash = ekey == NONE ? 0u : ekey; nd.parent = parent;
+    NodeRec r;
+    r.n = nd; r.line = eline; r.col = ecol; r.kline = ekl; r.kcol = ekc; r.kpos = ekpos; r.vpos = vpos;
+    r.pad0 = 0; r.pad1 = 0;
+    A.recs[nb + rel] = r;
+  };
   // one value at i for node `rel` whose parent is `parent`; containers push a frame
   auto value = [&](uint32_t rel, uint32_t parent) -> bool {
     const uint32_t c = T.at(i);
     if (c == '"') {
       uint32_t slot = 0, len = 0;
-      const uint64_t e = string_at(rel, false, &slot, &len);
+      const uint64_t e = string_at(&slot, &len);
       if (!e) return false;
+      if (MODE == M_EMIT) {
+        DNode nd; nd.kind = K_STRING; nd.count = len; nd.a = slot; nd.b = slot;
+        put(rel, nd, parent, (uint32_t)i);
+      }
       i = e;
       ns++;
-      if (MODE == M_EMIT) {
-        DNode& nd = A.nodes[nb + rel];
-        nd.kind = K_STRING; nd.count = len; nd.a = slot; nd.b = slot; nd.parent = parent;
-      }
       return true;
     }
     if (c == '{' || c == '[') {
@@ -408,8 +410,8 @@ __device__ void parse_doc(const JArgs& A, uint32_t d) {
         next += cnt;
       }
       if (MODE == M_EMIT) {
-        DNode& nd = A.nodes[nb + rel];
-        nd.kind = is_map ? K_MAP : K_LIST; nd.count = cnt; nd.a = first; nd.b = 0; nd.parent = parent;
+        DNode nd; nd.kind = is_map ? K_MAP : K_LIST; nd.count = cnt; nd.a = first; nd.b = 0;
+        put(rel, nd, parent, 0);
       }
       i++;
       ws();
@@ -426,9 +428,9 @@ __device__ void parse_doc(const JArgs& A, uint32_t d) {
     const uint64_t L = plain_len(T, i);
     if (!L || !after_plain_ok(T.at(i + L))) return false;
     if (MODE == M_EMIT) {
-      DNode& nd = A.nodes[nb + rel];
-      nd.count = 0; nd.a = 0; nd.b = 0; nd.parent = parent;
+      DNode nd; nd.kind = K_NULL; nd.count = 0; nd.a = 0; nd.b = 0;
       if (!scalar(T, i, L, nd)) { bad(BAD_NUMBER); return false; }
+      put(rel, nd, parent, 0);
     }
     i += L;
     return true;
@@ -438,11 +440,8 @@ __device__ void parse_doc(const JArgs& A, uint32_t d) {
   const uint32_t c0 = T.at(i);
   if (c0 != '{' && c0 != '[') { bad(BAD_SYNTAX); return; }
   if (MODE == M_EMIT) {
-    DNode& r = A.nodes[nb];
-    r.key_off = NONE; r.key_len = 0; r.key_hash = 0;
     const bool list = c0 == '[';
-    A.line[nb] = list ? 0 : line; A.col[nb] = list ? 0 : column();   // emit_root: lists keep (0,0)
-    A.kline[nb] = 0; A.kcol[nb] = 0;
+    eline = list ? 0 : line; ecol = list ? 0 : column();   // emit_root: lists keep (0,0)
   }
   if (!value(0, NONE)) { bad(BAD_SYNTAX); return; }
   while (sp) {
@@ -455,14 +454,13 @@ __device__ void parse_doc(const JArgs& A, uint32_t d) {
       const uint64_t kstart = i;
       const uint32_t kl = line, kc = column();
       uint32_t slot = 0, len = 0;
-      const uint64_t e = string_at(cs, true, &slot, &len);
+      const uint64_t e = string_at(&slot, &len);
       if (!e) { bad(BAD_SYNTAX); return; }
       i = e;
       ns++;
       if (MODE == M_EMIT) {
-        DNode& nd = A.nodes[nb + cs];
-        nd.key_off = slot; nd.key_len = len; nd.key_hash = slot;
-        A.kline[nb + cs] = kl; A.kcol[nb + cs] = kc;
+        ekey = slot; elen = len;
+        ekpos = (uint32_t)kstart; ekl = kl; ekc = kc;
 #if !GG_JDIAG_NODUP
         // duplicate keys (the host fast path refuses them too; IndexMap keeps the last value): the
         // earlier keys of this map are compared only when the map's filter has seen this slot's bit
@@ -471,7 +469,7 @@ __device__ void parse_doc(const JArgs& A, uint32_t d) {
         uint32_t& bw = F.bloom[bit >> 5];
         if ((bw >> (bit & 31u)) & 1u) {
           for (uint32_t q = 0; q < F.j; q++)
-            if (A.nodes[nb + F.first + q].key_hash == slot) { bad(BAD_DUPKEY); return; }
+            if (A.recs[nb + F.first + q].n.key_hash == slot) { bad(BAD_DUPKEY); return; }
         }
         bw |= 1u << (bit & 31u);
 #endif
@@ -481,11 +479,10 @@ __device__ void parse_doc(const JArgs& A, uint32_t d) {
       i++;
       ws();
     } else if (MODE == M_EMIT) {
-      DNode& nd = A.nodes[nb + cs];
-      nd.key_off = NONE; nd.key_len = 0; nd.key_hash = 0;
-      A.kline[nb + cs] = 0; A.kcol[nb + cs] = 0;
+      ekey = NONE; elen = 0;
+      ekpos = 0; ekl = 0; ekc = 0;
     }
-    if (MODE == M_EMIT) { A.line[nb + cs] = line; A.col[nb + cs] = column(); }
+    if (MODE == M_EMIT) { eline = line; ecol = column(); }
     F.j++;
     nn++;
     const uint32_t depth_before = sp;
@@ -540,14 +537,65 @@ __global__ void __launch_bounds__(256) json_own_kernel(JArgs A) {
   }
 }
 
-// pass 5: table slots in the nodes -> string ids (pool offsets)
-__global__ void __launch_bounds__(256) json_fix_kernel(JArgs A, uint64_t nnodes) {
-  for (uint64_t n = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; n < nnodes; n += (uint64_t)gridDim.x * blockDim.x) {
-    DNode d = A.nodes[n];
-    bool w = false;
-    if (d.kind == K_STRING) { d.a = A.tid[d.a]; d.b = d.a; w = true; }
-    if (d.key_off != NONE) { d.key_off = A.tid[d.key_off]; d.key_hash = d.key_off; w = true; }
-    if (w) A.nodes[n] = d;
+// the decoded bytes of the string whose opening quote is at q equal pool string `id` of `want` bytes
+// (compared 4 bytes at a time: a pool string is 16-byte aligned and zero padded, json_own_kernel)
+__device__ bool same_string(const JArgs& A, Text& T, uint64_t q, uint32_t id, uint32_t want) {
+  uint32_t pos = 0, word = 0, cont = 0;
+  bool same = true;
+  const uint32_t* pw = (const uint32_t*)(A.pool + id);
+  const uint64_t end = decode_string(T, q, [&](uint8_t c) {
+    word |= (uint32_t)c << ((pos & 3u) * 8u);
+    pos++;
+    if ((pos & 3u) == 0) {
+      if (pos > want || pw[(pos >> 2) - 1] != word) same = false;
+      word = 0;
+    }
+  }, cont);
+  if ((pos & 3u) && (pos > want || pw[pos >> 2] != word)) same = false;
+  return end && same && pos == want;
+}
+
+// passes 5 + 6, one wave per document over its nodes (consecutive nodes' strings are neighbours in
+// the text): table slots -> string ids (pool offsets), and every string occurrence's decoded bytes
+// compared with its id's pool bytes, so a fingerprint collision cannot merge two strings silently
+// (the document is refused and loads on the host)
+__global__ void __launch_bounds__(256) json_fix_verify_kernel(JArgs A) {
+  if (*A.bad) return;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t waves = (gridDim.x * blockDim.x) >> 6;
+  DNode dead;   // the nodes a refused document left: placeholders whose key fields stay consistent
+  dead.kind = K_NULL; dead.count = 0; dead.a = 0; dead.b = 0; dead.key_off = NONE; dead.key_len = 0; dead.key_hash = 0;
+  dead.parent = NONE;
+  for (uint32_t d = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; d < A.ndocs; d += waves) {
+    const uint64_t nb = A.node_base[d], nn = A.n_nodes[d];
+    auto kill = [&]() {
+      for (uint64_t r = lane; r < nn; r += 64) {
+        A.nodes[nb + r] = dead; A.line[nb + r] = 0; A.col[nb + r] = 0; A.kline[nb + r] = 0; A.kcol[nb + r] = 0;
+      }
+    };
+    if (A.doc_bad[d]) { kill(); continue; }   // refused by the emit pass part way (count-pass refusals have no nodes)
+    Text T(A.text, A.off[d], A.off[d + 1] - A.off[d]);
+    bool ok = true;
+    for (uint64_t r = lane; r < nn; r += 64) {
+      const NodeRec rec = A.recs[nb + r];
+      DNode x = rec.n;
+      bool w = false;
+      if (x.kind == K_STRING) {
+        x.a = A.tid[x.a]; x.b = x.a; w = true;
+        if (!same_string(A, T, rec.vpos, x.a, x.count)) ok = false;
+      }
+      if (x.key_off != NONE) {
+        x.key_off = A.tid[x.key_off]; x.key_hash = x.key_off; w = true;
+        if (!same_string(A, T, rec.kpos, x.key_off, x.key_len)) ok = false;
+      }
+      (void)w;
+      A.nodes[nb + r] = x;
+      A.line[nb + r] = rec.line; A.col[nb + r] = rec.col; A.kline[nb + r] = rec.kline; A.kcol[nb + r] = rec.kcol;
+    }
+    if (__ballot(!ok)) {
+      kill();
+      if (lane == 0) A.doc_bad[d] = BAD_VERIFY;
+    }
   }
 }
 
@@ -683,6 +731,8 @@ bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, 
   JCHK(hipMemset(d_doc_bad.p, 0, n * 4));
   JArgs A{};
   A.text = d_text.p; A.off = d_off.p; A.ndocs = (uint32_t)n;
+  A.fp_mask = ~0ull;
+  if (const char* e = getenv("GG_JSON_FP_MASK")) A.fp_mask = strtoull(e, nullptr, 0);   // tests: forced collisions
   A.n_nodes = d_nn.p; A.n_cont = d_nc.p; A.n_str = d_ns.p; A.bad = d_bad.p; A.doc_bad = d_doc_bad.p;
   DevArr<uint16_t> d_counts; d_counts.alloc(total / 2 + 1);
   A.counts = d_counts.p;
@@ -748,6 +798,9 @@ bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, 
   uint64_t pool_cap = std::min<uint64_t>(std::max<uint64_t>(total / 4, 1ull << 20), pool_max);
   DevArr<uint8_t> d_pool;
   A.node_base = d_nbase.p; A.nodes = d_nodes.p;
+  DevArr<NodeRec> d_recs;
+  d_recs.alloc(N);
+  A.recs = d_recs.p;
   A.line = d_line.p; A.col = d_col.p; A.kline = d_kline.p; A.kcol = d_kcol.p;
   for (;;) {
     if (d_pool.n != pool_cap + 16) d_pool.alloc(pool_cap + 16);
@@ -759,13 +812,12 @@ bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, 
     JCHK(hipMemcpy(d_doc_bad.p, d_doc_bad0.p, n * 4, hipMemcpyDeviceToDevice));
     A.tkey = d_tkey.p; A.tlen = d_tlen.p; A.towner = d_towner.p; A.tid = d_tid.p; A.tmask = tslots - 1;
 
-    // 3. emit, 4. own, 5. fix, 6. verify
+    // 2. emit, 3. own, 4. fix + verify
     JCHK(hipEventRecord(e0));
     hipLaunchKernelGGL(json_pass_kernel<M_EMIT>, dim3(dgrid), dim3(256), 0, 0, A);
 #if !GG_JDIAG_NOINTERN
     hipLaunchKernelGGL(json_own_kernel, dim3(grid_for(tslots, 256)), dim3(256), 0, 0, A);
-    hipLaunchKernelGGL(json_fix_kernel, dim3(grid_for(N, 256)), dim3(256), 0, 0, A, N);
-    hipLaunchKernelGGL(json_pass_kernel<M_VERIFY>, dim3(dgrid), dim3(256), 0, 0, A);
+    hipLaunchKernelGGL(json_fix_verify_kernel, dim3(grid_for(n * 64ull, 256)), dim3(256), 0, 0, A);
 #else
     { const uint32_t diag = BAD_SIZE; JCHK(hipMemcpy(d_bad.p, &diag, 4, hipMemcpyHostToDevice)); }
 #endif

@@ -210,6 +210,31 @@ def test_synthetic_device_matches_host():
     b.close()
 
 
+def test_fingerprint_collisions_are_caught(monkeypatch):
+    """fingerprints narrowed to 4 bits (GG_JSON_FP_MASK): different strings share table slots, the
+    verification finds every occurrence whose bytes differ from its slot's pool string, and the
+    document is refused -- the strict check names the collision, a session loads those documents on
+    the host and reports as a host-loaded session does"""
+    monkeypatch.setenv("GG_JSON_FP_MASK", "0xF")
+    # lists of strings: no map, so no duplicate-key check sees the shared slots first
+    rc, msg = guard_amd.loader_device_check(['["alpha-%d", "beta-%d", "gamma-%d"]' % (i, i, i) for i in range(10)])
+    assert rc == -1 and "collision" in msg
+    # templates: keys of one map that share a slot read as duplicates first; either way refused
+    docs = synth.cfn_corpus(6, start=11, n_resources=8)
+    rules = rule_pack()
+    names = ["c%d.json" % i for i in range(len(docs))]
+    s = guard_amd.Session()
+    for name, text in rules:
+        s.add_rules(text, name)
+    st = s.add_docs_device(docs, names)
+    assert st is not None and st["refused_docs"] >= 1
+    s.eval(1)
+    dev = s.report()
+    s.close()
+    monkeypatch.delenv("GG_JSON_FP_MASK")
+    assert dev == _session(rules, docs, names, False)
+
+
 def test_intern_table_doubles_when_full(monkeypatch):
     """The device intern table starts small (cache-resident probes) and doubles when a batch has
     more distinct strings than it holds; the arena is still the host loader's."""
