@@ -512,8 +512,19 @@ __device__ void parse_doc(const JArgs& A, uint32_t d) {
   if (MODE == M_COUNT) { A.n_nodes[d] = nn; A.n_cont[d] = nc; A.n_str[d] = ns; }
 }
 
+// resident waves per SIMD the passes are compiled for (their VGPR budget: 512 / waves)
+#ifndef GG_JSON_WPE_COUNT
+#define GG_JSON_WPE_COUNT 8
+#endif
+#ifndef GG_JSON_WPE_EMIT
+#define GG_JSON_WPE_EMIT 6
+#endif
+#ifndef GG_JSON_WPE_FIX
+#define GG_JSON_WPE_FIX 8
+#endif
 template <uint32_t MODE>
-__global__ void __launch_bounds__(256) json_pass_kernel(JArgs A) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == M_EMIT ? GG_JSON_WPE_EMIT : GG_JSON_WPE_COUNT)))
+json_pass_kernel(JArgs A) {
   for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < A.ndocs; d += gridDim.x * blockDim.x) {
     if (*A.bad) return;
     parse_doc<MODE>(A, d);
@@ -559,7 +570,7 @@ __device__ bool same_string(const JArgs& A, Text& T, uint64_t q, uint32_t id, ui
 // the text): table slots -> string ids (pool offsets), and every string occurrence's decoded bytes
 // compared with its id's pool bytes, so a fingerprint collision cannot merge two strings silently
 // (the document is refused and loads on the host)
-__global__ void __launch_bounds__(256) json_fix_verify_kernel(JArgs A) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_JSON_WPE_FIX))) json_fix_verify_kernel(JArgs A) {
   if (*A.bad) return;
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t waves = (gridDim.x * blockDim.x) >> 6;
