@@ -125,6 +125,15 @@ struct Text {
     const uint32_t lt = (x - 0x20202020u) & ~x;
     return (zq | zb | zd | lt | x) & 0x80808080u;
   }
+  // bytes k .. k+3 of the current window, little-endian (zeros past its end)
+  __device__ uint32_t bytes4(uint32_t k) const {
+    const uint32_t j = k >> 2;
+    const uint32_t lo = j == 0 ? w.x : (j == 1 ? w.y : (j == 2 ? w.z : w.w));
+    const uint32_t hi = j == 0 ? w.y : (j == 1 ? w.z : (j == 2 ? w.w : 0u));
+    return __builtin_amdgcn_alignbyte(hi, lo, k & 3u);
+  }
+  // the window offset of document byte i (after plain_run(i) loaded its window)
+  __device__ uint32_t woff(uint64_t i) const { return (uint32_t)((base + i) & 15ull); }
   // the number of plain printable ASCII bytes from i to the first special byte, the end of i's
   // 16-byte block or the end of the document (0 when byte i is special)
   __device__ uint32_t plain_run(uint64_t i) {
@@ -143,6 +152,22 @@ struct Text {
   }
 };
 
+// The decoded bytes of a string as little-endian 4-byte words: on_word(word, bytes so far) for each
+// full word; a plain run is taken from the text window 4 bytes at a time.  The caller handles the
+// last partial word (`word`, len & 3 bytes).
+struct WordStream {
+  uint32_t word = 0, len = 0;
+  template <typename F>
+  __device__ void byte(uint32_t c, F&& on_word) {
+    word |= c << ((len & 3u) * 8u);
+    len++;
+    if ((len & 3u) == 0) { on_word(word, len); word = 0; }
+  }
+  // r plain bytes at offset k of T's window (k + r <= 16)
+  template <typename F>
+  __device__ void run(const struct Text& T, uint32_t k, uint32_t r, F&& on_word);
+};
+
 __device__ inline uint64_t mix64(uint64_t x) {
   x ^= x >> 30; x *= 0xbf58476d1ce4e5b9ull;
   x ^= x >> 27; x *= 0x94d049bb133111ebull;
@@ -157,15 +182,16 @@ __device__ inline uint64_t mix64(uint64_t x) {
 // U+2029, which it reads as line breaks).  Raw UTF-8 passes through as it is, as libyaml keeps it;
 // `cont` counts its continuation bytes, because libyaml's marks count characters, not bytes
 // (a mark's column = bytes since the line start - continuation bytes since it).
-// BYTES: the sink reads the decoded bytes (false: only the end of the string matters, and plain
-// runs are skipped a 16-byte block at a time)
+// The sink takes decoded bytes one by one (sink.byte(c)) and plain runs whole (sink.run(T, k, r): r
+// bytes at offset k of T's window).  BYTES: the sink reads the decoded bytes (false: only the end of
+// the string matters, and plain runs are skipped a 16-byte block at a time)
 template <bool BYTES = true, typename Sink>
 __device__ uint64_t decode_string(Text& T, uint64_t q, Sink&& sink, uint32_t& cont) {
   uint64_t i = q + 1;
   for (;;) {
     const uint32_t r = T.plain_run(i);
     if (r) {
-      if (BYTES) for (uint32_t u = 0; u < r; u++) sink((uint8_t)T.at(i + u));
+      if (BYTES) sink.run(T, T.woff(i), r);
       i += r;
       continue;
     }
@@ -184,13 +210,13 @@ __device__ uint64_t decode_string(Text& T, uint64_t q, Sink&& sink, uint32_t& co
       if ((n == 2 && cp < 0x800u) || (n == 3 && (cp < 0x10000u || cp > 0x10FFFFu))) return 0;
       if (cp >= 0xD800u && cp <= 0xDFFFu) return 0;
       if (cp < 0xA0u || cp == 0x2028u || cp == 0x2029u || cp == 0xFFFEu || cp == 0xFFFFu) return 0;
-      for (uint32_t k = 0; k <= n; k++) sink((uint8_t)T.at(i + k));
+      for (uint32_t k = 0; k <= n; k++) sink.byte(T.at(i + k));
       cont += n;
       i += n + 1;
       continue;
     }
     if (c < 0x20u || c > 0x7Eu) return 0;
-    if (c != '\\') { sink((uint8_t)c); i++; continue; }
+    if (c != '\\') { sink.byte(c); i++; continue; }
     const uint32_t e = T.at(i + 1);
     uint32_t out;
     switch (e) {
@@ -213,16 +239,29 @@ __device__ uint64_t decode_string(Text& T, uint64_t q, Sink&& sink, uint32_t& co
           else return 0;
         }
         if (cp >= 0xD800 && cp <= 0xDFFF) return 0;
-        if (cp < 0x80) sink((uint8_t)cp);
-        else if (cp < 0x800) { sink((uint8_t)(0xC0 | (cp >> 6))); sink((uint8_t)(0x80 | (cp & 0x3F))); }
-        else { sink((uint8_t)(0xE0 | (cp >> 12))); sink((uint8_t)(0x80 | ((cp >> 6) & 0x3F))); sink((uint8_t)(0x80 | (cp & 0x3F))); }
+        if (cp < 0x80) sink.byte(cp);
+        else if (cp < 0x800) { sink.byte(0xC0u | (cp >> 6)); sink.byte(0x80u | (cp & 0x3Fu)); }
+        else { sink.byte(0xE0u | (cp >> 12)); sink.byte(0x80u | ((cp >> 6) & 0x3Fu)); sink.byte(0x80u | (cp & 0x3Fu)); }
         i += 6;
         continue;
       }
       default: return 0;
     }
-    sink((uint8_t)out);
+    sink.byte(out);
     i += 2;
+  }
+}
+
+template <typename F>
+__device__ void WordStream::run(const Text& T, uint32_t k, uint32_t r, F&& on_word) {
+  while (r) {
+    const uint32_t p = len & 3u;
+    const uint32_t take = r < 4u - p ? r : 4u - p;
+    uint32_t chunk = T.bytes4(k);
+    if (take < 4u) chunk &= (1u << (8u * take)) - 1u;
+    word |= chunk << (8u * p);
+    len += take; k += take; r -= take;
+    if ((len & 3u) == 0) { on_word(word, len); word = 0; }
   }
 }
 
@@ -350,14 +389,18 @@ __device__ void parse_doc(const JArgs& A, uint32_t d) {
     uint64_t end;
     // fingerprint of the decoded bytes, 4 at a time (the device table's own key: nothing outside
     // this loader compares it)
-    uint32_t word = 0;
-    end = decode_string<MODE == M_EMIT>(T, i, [&](uint8_t c) {
-      word |= (uint32_t)c << ((fp.len & 3u) * 8u);
-      fp.len++;
-      if ((fp.len & 3u) == 0) { fp.h = (fp.h ^ word) * 0x100000001b3ull; word = 0; }
-    }, cont);
+    struct HashSink {
+      WordStream ws;
+      uint64_t h;
+      __device__ void byte(uint32_t c) { ws.byte(c, [&](uint32_t w, uint32_t) { h = (h ^ w) * 0x100000001b3ull; }); }
+      __device__ void run(const Text& T, uint32_t k, uint32_t r) {
+        ws.run(T, k, r, [&](uint32_t w, uint32_t) { h = (h ^ w) * 0x100000001b3ull; });
+      }
+    } hs{WordStream(), fp.h};
+    end = decode_string<MODE == M_EMIT>(T, i, hs, cont);
     if (!end) return 0;
-    fp.h = (fp.h ^ word) * 0x100000001b3ull;
+    fp.h = (hs.h ^ hs.ws.word) * 0x100000001b3ull;
+    fp.len = hs.ws.len;
     if (MODE == M_EMIT) {
       const uint64_t key64 = (mix64(fp.h ^ ((uint64_t)fp.len * 0x9E3779B97F4A7C15ull)) & A.fp_mask) | 1ull;
 #if GG_JDIAG_NOINTERN
@@ -544,26 +587,35 @@ __global__ void __launch_bounds__(256) json_own_kernel(JArgs A) {
     Text T(A.text, A.off[doc], A.off[doc + 1] - A.off[doc]);
     uint64_t p = at;
     uint32_t cont = 0;
-    decode_string(T, q, [&](uint8_t c) { A.pool[p++] = c; }, cont);
+    struct CopySink {
+      uint8_t* pool;
+      uint64_t p;
+      __device__ void byte(uint32_t c) { pool[p++] = (uint8_t)c; }
+      __device__ void run(const Text& T, uint32_t k, uint32_t r) {
+        for (uint32_t u = 0; u < r; u++) pool[p++] = (uint8_t)(T.bytes4(k + u) & 0xFFu);
+      }
+    } cs{A.pool, p};
+    decode_string(T, q, cs, cont);
   }
 }
 
 // the decoded bytes of the string whose opening quote is at q equal pool string `id` of `want` bytes
 // (compared 4 bytes at a time: a pool string is 16-byte aligned and zero padded, json_own_kernel)
 __device__ bool same_string(const JArgs& A, Text& T, uint64_t q, uint32_t id, uint32_t want) {
-  uint32_t pos = 0, word = 0, cont = 0;
-  bool same = true;
-  const uint32_t* pw = (const uint32_t*)(A.pool + id);
-  const uint64_t end = decode_string(T, q, [&](uint8_t c) {
-    word |= (uint32_t)c << ((pos & 3u) * 8u);
-    pos++;
-    if ((pos & 3u) == 0) {
-      if (pos > want || pw[(pos >> 2) - 1] != word) same = false;
-      word = 0;
-    }
-  }, cont);
-  if ((pos & 3u) && (pos > want || pw[pos >> 2] != word)) same = false;
-  return end && same && pos == want;
+  struct CmpSink {
+    WordStream ws;
+    const uint32_t* pw;
+    uint32_t want;
+    bool same;
+    __device__ void check(uint32_t w, uint32_t len) { if (len > want || pw[(len >> 2) - 1] != w) same = false; }
+    __device__ void byte(uint32_t c) { ws.byte(c, [&](uint32_t w, uint32_t len) { check(w, len); }); }
+    __device__ void run(const Text& T, uint32_t k, uint32_t r) { ws.run(T, k, r, [&](uint32_t w, uint32_t len) { check(w, len); }); }
+  } cs{WordStream(), (const uint32_t*)(A.pool + id), want, true};
+  uint32_t cont = 0;
+  const uint64_t end = decode_string(T, q, cs, cont);
+  const uint32_t pos = cs.ws.len;
+  if ((pos & 3u) && (pos > want || cs.pw[pos >> 2] != cs.ws.word)) cs.same = false;
+  return end && cs.same && pos == want;
 }
 
 // passes 5 + 6, one wave per document over its nodes (consecutive nodes' strings are neighbours in
