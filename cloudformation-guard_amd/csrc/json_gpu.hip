@@ -11,13 +11,14 @@
 //                 DFS pre-order (host: JsonFast::v2) -- with marks, scalar typing, and every
 //                 string inserted into a device hash table keyed by a 64-bit fingerprint of its
 //                 decoded bytes; nodes carry table slots for now and each string occurrence's text
-//                 offset; duplicate map keys are refused (a per-map slot filter, then a scan);
+//                 offset;
 //   3. own        every occupied slot copies its first occurrence's decoded bytes into the pool
 //                 (16-byte aligned, zero padded: the evaluator compares in 16-byte chunks); the
 //                 pool offset is the string id, as on the host;
-//   4. fix+verify one wave per document over its nodes: slots -> ids, and every occurrence's
-//                 decoded bytes compared with its id's pool bytes, so a fingerprint collision
-//                 cannot merge two strings silently (the document is refused).
+//   4. fix+verify one wave per document over its nodes: slots -> ids, every occurrence's decoded
+//                 bytes compared with its id's pool bytes, so a fingerprint collision cannot merge
+//                 two strings silently, and every map key against its earlier siblings (duplicate
+//                 keys); either refuses the document.
 // A document outside the subset is refused on its own (per-document flag): the passes skip it, the
 // host loader builds it (doc_loader.cpp, the libyaml path) and its nodes join the batch at the
 // document's position, so results never depend on which loader ran.  Only batch-wide limits (string
@@ -37,9 +38,6 @@
 #include <stdexcept>
 #include <thread>
 
-#ifndef GG_JDIAG_NODUP
-#define GG_JDIAG_NODUP 0   // diagnostic A/B builds only: skip the duplicate-key check
-#endif
 #ifndef GG_JDIAG_NOINTERN
 #define GG_JDIAG_NOINTERN 0   // diagnostic A/B builds only: skip the intern table
 #endif
@@ -353,7 +351,6 @@ struct Frame {
   uint32_t slot;    // the container's own node (document-relative)
   uint32_t k;       // pre-order container index
   uint32_t map;     // 1 map, 0 list
-  uint32_t bloom[4];   // EMIT, maps: 128-bit filter of the key slots seen so far
 };
 
 template <uint32_t MODE>
@@ -464,7 +461,6 @@ __device__ void parse_doc(const JArgs& A, uint32_t d) {
         return true;
       }
       st[sp].first = first; st[sp].j = 0; st[sp].slot = rel; st[sp].k = k; st[sp].map = is_map;
-      if (MODE == M_EMIT && is_map) { st[sp].bloom[0] = 0; st[sp].bloom[1] = 0; st[sp].bloom[2] = 0; st[sp].bloom[3] = 0; }
       sp++;
       return true;
     }
@@ -504,18 +500,8 @@ __device__ void parse_doc(const JArgs& A, uint32_t d) {
       if (MODE == M_EMIT) {
         ekey = slot; elen = len;
         ekpos = (uint32_t)kstart; ekl = kl; ekc = kc;
-#if !GG_JDIAG_NODUP
-        // duplicate keys (the host fast path refuses them too; IndexMap keeps the last value): the
-        // earlier keys of this map are compared only when the map's filter has seen this slot's bit
+        // duplicate keys are found by the fix / verify pass; maps past its scan bound are refused
         if (F.j >= kMaxPairwiseKeys) { bad(BAD_DUPKEY); return; }
-        const uint32_t bit = (slot ^ (slot >> 7) ^ (slot >> 14)) & 127u;
-        uint32_t& bw = F.bloom[bit >> 5];
-        if ((bw >> (bit & 31u)) & 1u) {
-          for (uint32_t q = 0; q < F.j; q++)
-            if (A.recs[nb + F.first + q].n.key_hash == slot) { bad(BAD_DUPKEY); return; }
-        }
-        bw |= 1u << (bit & 31u);
-#endif
       }
       while (T.at(i) == ' ') i++;
       if (T.at(i) != ':' || line != kl || i - kstart > 1000) { bad(BAD_SYNTAX); return; }
@@ -638,10 +624,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_JSO
     };
     if (A.doc_bad[d]) { kill(); continue; }   // refused by the emit pass part way (count-pass refusals have no nodes)
     Text T(A.text, A.off[d], A.off[d + 1] - A.off[d]);
-    bool ok = true;
+    bool ok = true, dup = false;
     for (uint64_t r = lane; r < nn; r += 64) {
       const NodeRec rec = A.recs[nb + r];
       DNode x = rec.n;
+      if (x.key_off != NONE) {
+        // duplicate map keys (the host fast path refuses them too; IndexMap keeps the last value):
+        // this key's slot against its earlier siblings' (siblings are contiguous; the lanes of one
+        // map read the same sibling at the same step)
+        for (uint32_t q = A.recs[nb + x.parent].n.a; q < (uint32_t)r; q++)
+          if (A.recs[nb + q].n.key_hash == x.key_hash) { dup = true; break; }
+      }
       bool w = false;
       if (x.kind == K_STRING) {
         x.a = A.tid[x.a]; x.b = x.a; w = true;
@@ -655,9 +648,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_JSO
       A.nodes[nb + r] = x;
       A.line[nb + r] = rec.line; A.col[nb + r] = rec.col; A.kline[nb + r] = rec.kline; A.kcol[nb + r] = rec.kcol;
     }
-    if (__ballot(!ok)) {
+    const bool any_dup = __ballot(dup) != 0;
+    if (any_dup || __ballot(!ok)) {
       kill();
-      if (lane == 0) A.doc_bad[d] = BAD_VERIFY;
+      if (lane == 0) A.doc_bad[d] = any_dup ? BAD_DUPKEY : BAD_VERIFY;
     }
   }
 }
