@@ -290,6 +290,10 @@ struct gg_session {
   hipStream_t stream = nullptr;        // caller stream (e.g. torch's current stream); null = the buffers' own stream
   hipEvent_t ev0 = nullptr, ev1 = nullptr;   // brackets of the most recent launch (= dv->evq[nq - 1])
   size_t nq = 0;
+  // the device loader's copy of docs.nodes[0, dev_nodes_n) (hipMalloc'ed): the next upload packs the
+  // arena from it instead of sending the nodes over PCIe again, then frees it
+  void* dev_nodes = nullptr;
+  size_t dev_nodes_n = 0;
   unsigned long long* ext_counts = nullptr;   // caller-owned device tally buffer (RCCL all-reduce)
   bool launched = false;
   std::vector<unsigned long long> counts;
@@ -319,6 +323,7 @@ struct gg_session {
     // drain it before the set goes back to the pool, where the next session's uploads reuse it
     if (dv && stream) hipStreamSynchronize(stream);
     release_bufs(dv);
+    if (dev_nodes) hipFree(dev_nodes);
   }
 };
 
@@ -341,7 +346,23 @@ void session_upload(gg_session* s) {
     // lane-mode tiles address their document by a 32-bit global node index (eval_core.inc Ctx)
     if (n >= 0xFFFFFFFFull) throw std::runtime_error("batch too large for one session: split it (>= 2^32 arena nodes)");
     DBuf<DNode> tmp;
-    tmp.upload(s->docs.nodes.data(), n, st);
+    const DNode* src = nullptr;
+    if (s->dev_nodes && s->dev_nodes_n <= n) {
+      // the device loader's nodes are already in HBM: only nodes the host appended since (documents
+      // the device refused, built by the host loader) cross PCIe
+      if (s->dev_nodes_n == n) {
+        src = (const DNode*)s->dev_nodes;
+      } else {
+        tmp.alloc(n);
+        HIPCHK(hipMemcpyAsync(tmp.p, s->dev_nodes, s->dev_nodes_n * sizeof(DNode), hipMemcpyDeviceToDevice, st));
+        HIPCHK(hipMemcpyAsync(tmp.p + s->dev_nodes_n, s->docs.nodes.data() + s->dev_nodes_n,
+                              (n - s->dev_nodes_n) * sizeof(DNode), hipMemcpyHostToDevice, st));
+        src = tmp.p;
+      }
+    } else {
+      tmp.upload(s->docs.nodes.data(), n, st);
+      src = tmp.p;
+    }
     s->dv->d_nodes.alloc(std::max<size_t>(n, 1));
     s->dv->d_klen.alloc(std::max<size_t>(n, 1));
     DBuf<uint32_t> bad;
@@ -349,12 +370,13 @@ void session_upload(gg_session* s) {
     HIPCHK(hipMemsetAsync(bad.p, 0, 4, st));
     if (n) {
       const uint32_t blocks = (uint32_t)std::min<size_t>((n + 255) / 256, (size_t)g_dev.ncu * 64);
-      hipLaunchKernelGGL(pack_nodes_kernel, dim3(blocks), dim3(256), 0, st, tmp.p, s->dv->d_nodes.p, s->dv->d_klen.p, (uint64_t)n, bad.p);
+      hipLaunchKernelGGL(pack_nodes_kernel, dim3(blocks), dim3(256), 0, st, src, s->dv->d_nodes.p, s->dv->d_klen.p, (uint64_t)n, bad.p);
       HIPCHK(hipGetLastError());
     }
     uint32_t b = 0;
     HIPCHK(hipMemcpyAsync(&b, bad.p, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    if (s->dev_nodes) { hipFree(s->dev_nodes); s->dev_nodes = nullptr; s->dev_nodes_n = 0; }
     if (b & 1u) throw std::runtime_error("a string or container is too large for the device arena (count >= 2^28)");
     if (b & 2u) throw std::runtime_error("arena invariant broken: a map entry's key offset is not its key id");
   }
@@ -1732,7 +1754,10 @@ int32_t gg_session_add_docs_device(gg_session* s, const char* const* texts, cons
     GpuLoadStats st;
     DocBatch b;
     std::vector<uint32_t> refused;
-    if (!gpu_load_json(b, texts, lens, nm, n, st, why, &refused)) { set_note(err, why); return 1; }
+    void* dev_nodes = nullptr;
+    if (!gpu_load_json(b, texts, lens, nm, n, st, why, &refused, &dev_nodes)) { set_note(err, why); return 1; }
+    struct Holder { void*& p; ~Holder() { if (p) hipFree(p); } } hold{dev_nodes};
+    const size_t dev_n = b.nodes.size();
     if (!refused.empty()) {
       // the documents the device refused, built by the host loader (libyaml) on host threads and
       // spliced in at their positions: their nodes are appended to the arena, strings re-interned
@@ -1758,6 +1783,9 @@ int32_t gg_session_add_docs_device(gg_session* s, const char* const* texts, cons
     }
     s->docs = std::move(b);
     s->uploaded = false;
+    if (s->dev_nodes) hipFree(s->dev_nodes);
+    s->dev_nodes = dev_nodes; s->dev_nodes_n = dev_n;
+    dev_nodes = nullptr;
     load_stats(st, stats);
     return 0;
   } catch (std::exception& e) { set_err(err, -1, e.what()); return -1; }

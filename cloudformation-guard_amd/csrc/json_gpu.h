@@ -28,8 +28,11 @@ struct GpuLoadStats {
 // reads specially) is refused on its own: with `refused` non-null its index is appended there and
 // `out` holds an empty placeholder for it (the caller builds it with the host loader); with
 // `refused` null the whole batch is refused.  Returns false with `why` set when the batch is refused
-// (batch-wide limits, or strict mode); `out` is then unchanged.
+// (batch-wide limits, or strict mode); `out` is then unchanged.  With `keep_nodes` non-null the
+// device copy of out.nodes (hipMalloc'ed, out.nodes.size() DNodes) is handed to the caller, who
+// frees it with hipFree: the session packs its arena from it instead of uploading the nodes again.
 bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, const std::vector<std::string>& names,
-                   size_t n, GpuLoadStats& st, std::string& why, std::vector<uint32_t>* refused = nullptr);
+                   size_t n, GpuLoadStats& st, std::string& why, std::vector<uint32_t>* refused = nullptr,
+                   void** keep_nodes = nullptr);
 
 }  // namespace gg

@@ -755,7 +755,8 @@ struct Staging {
 }  // namespace
 
 bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, const std::vector<std::string>& names,
-                   size_t n, GpuLoadStats& st, std::string& why, std::vector<uint32_t>* refused) {
+                   size_t n, GpuLoadStats& st, std::string& why, std::vector<uint32_t>* refused,
+                   void** keep_nodes) {
   static const char* kWhy[] = {"", "outside the strict-JSON subset", "nesting deeper than 64", "duplicate map keys",
                                "a number the host types (beyond 64 bits, or an infinite / undecided float)", "string table full", "string pool full",
                                "string fingerprint collision", "batch too large", "a container with more than 65535 elements"};
@@ -944,6 +945,7 @@ bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, 
   out.base.assign(nbase.begin(), nbase.end());
   out.names.assign(names.begin(), names.begin() + n);
   st.nodes = N; st.distinct_strings = distinct; st.pool_bytes = pool_used;
+  if (keep_nodes) { *keep_nodes = d_nodes.p; d_nodes.p = nullptr; }
   return true;
 }
 
