@@ -376,7 +376,10 @@ __device__ void parse_doc(const JArgs& A, uint32_t d) {
   const uint64_t nb = (MODE >= M_EMIT) ? A.node_base[d] : 0;
   const uint64_t cb = b0 >> 1;
   uint32_t nn = 1, nc = 0, ns = 0, ci = 0, next = 1;
+  // the open containers: the innermost one in registers (`top`), the ones around it in st[0, sp - 1)
+  // (scratch), so an element's bookkeeping does not go through memory
   Frame st[kMaxDepth];
+  Frame top{};
   uint32_t sp = 0;
 
   // a string occurrence at i (the opening quote): returns the index after it, 0 on refusal;
@@ -460,7 +463,8 @@ __device__ void parse_doc(const JArgs& A, uint32_t d) {
         if (MODE == M_COUNT) A.counts[cb + k] = 0;
         return true;
       }
-      st[sp].first = first; st[sp].j = 0; st[sp].slot = rel; st[sp].k = k; st[sp].map = is_map;
+      if (sp) st[sp - 1] = top;
+      top.first = first; top.j = 0; top.slot = rel; top.k = k; top.map = is_map;
       sp++;
       return true;
     }
@@ -484,7 +488,7 @@ __device__ void parse_doc(const JArgs& A, uint32_t d) {
   }
   if (!value(0, NONE)) { bad(BAD_SYNTAX); return; }
   while (sp) {
-    Frame& F = st[sp - 1];
+    Frame& F = top;
     const uint32_t close = F.map ? '}' : ']';
     // one element of F
     const uint32_t cs = F.first + F.j;
@@ -519,7 +523,7 @@ __device__ void parse_doc(const JArgs& A, uint32_t d) {
     if (sp > depth_before) continue;   // a nested container: its elements come first
     // after an element: ',' or the close of this container (and of every container it completes)
     for (;;) {
-      Frame& G = st[sp - 1];
+      Frame& G = top;
       const uint32_t gclose = G.map ? '}' : ']';
       ws();
       const uint32_t c = T.at(i);
@@ -533,6 +537,7 @@ __device__ void parse_doc(const JArgs& A, uint32_t d) {
       }
       sp--;
       if (!sp) break;
+      top = st[sp - 1];
     }
     (void)close;
   }
