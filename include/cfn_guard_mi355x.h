@@ -199,7 +199,8 @@ int32_t gg_session_add_synthetic(gg_session *s, uint64_t first, size_t n, int32_
  * (a batch-wide limit, or a refused document the host loader rejects too: nothing loaded, err->message
  * says why; gg_session_add_docs reports the loader error), -1 on error.  stats (may be NULL, 9 doubles):
  * kernel ms, nodes, distinct strings, pool bytes, text bytes, H2D ms, D2H ms, intern-table doublings,
- * documents built by the host loader. */
+ * documents built by the host loader.  The loaded nodes stay in HBM for the session's first upload
+ * (it packs the device arena from them; only host-built documents cross PCIe again). */
 int32_t gg_session_add_docs_device(gg_session *s, const char *const *texts, const size_t *lens, const char *const *names,
                                    size_t n, double *stats, extern_err_t *err);
 int32_t gg_session_add_synthetic_device(gg_session *s, uint64_t first, size_t n, int32_t n_resources, int32_t nthreads,
