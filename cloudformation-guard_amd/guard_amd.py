@@ -385,8 +385,10 @@ class Session:
             _raise(err)
 
     def add_docs_device(self, texts, names=None):
-        """Parses and interns strict-JSON documents on the MI355X (empty session only).  Returns the
-        loader statistics, or None when a document is outside the device subset (nothing loaded)."""
+        """Parses and interns strict-JSON documents on the MI355X (empty session only).  A document
+        outside the device subset is built by the host loader at its position (stats["refused_docs"]
+        counts them).  Returns the loader statistics, or None when the batch is refused as a whole
+        (a batch-wide limit: nothing loaded)."""
         n = len(texts)
         bufs = [_b(t) for t in texts]
         T = (ctypes.c_char_p * n)(*bufs)
