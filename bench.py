@@ -24,10 +24,12 @@ evaluator -- NOT the reference binary, which cannot be built here) run on a boun
 same documents x the same rule pack, in one process per core on the host cores of this box:
 `value` end to end (load + evaluate + structured report), `eval_only_value` evaluation alone.
 
-e2e (N = 1): the whole job a `validate --structured` user pays for, on the same workload -- host
-load (text -> arena, synthetic text generation included), upload (PCIe + device packing), one
-evaluation with statuses and records fetched to the host, and the structured JSON report rendered
-on the host (report_bytes, discarded) -- and the evaluations/s that total gives.
+e2e (N = 1): the whole job a `validate --structured` user pays for, on the same workload -- load
+(synthetic text generated on host threads, then parsed by the MI355X JSON loader, csrc/json_gpu.hip:
+text over PCIe, arena back for the reporter; --loader host parses on host threads instead), upload
+(device packing; PCIe too with the host loader), one evaluation with statuses and records fetched
+to the host, and the structured JSON report rendered on the host (report_bytes, discarded) -- and
+the evaluations/s that total gives.
 
 --workload: cfg2 (default; BASELINE.json configs[1], the metric's config), cfg3 (the same corpus x
 the 22-file full-registry stand-in, configs[2]) or cfg5 (AWS Config snapshots x the
@@ -158,8 +160,9 @@ def main():
                          "report time is scaled to the whole job")
     ap.add_argument("--resources", type=int, default=50)
     ap.add_argument("--threads", type=int, default=0, help="host loader threads (default: CPU share)")
-    ap.add_argument("--loader", choices=("host", "device"), default="host",
-                    help="document loader: host threads, or the MI355X JSON loader (csrc/json_gpu.hip)")
+    ap.add_argument("--loader", choices=("device", "host"), default="device",
+                    help="document loader: the MI355X JSON loader (csrc/json_gpu.hip; documents outside its "
+                         "subset are built on host threads), or host threads only")
     ap.add_argument("--gather-docs", type=int, default=200,
                     help="N > 1: each rank renders the structured JSON report of its first GATHER_DOCS documents "
                          "and rank 0 gathers them (sharding.gather_report; outside the timed region)")
