@@ -149,6 +149,26 @@ def test_session_refused_documents_load_on_the_host():
     assert dev == (exp, ecode)
 
 
+def test_device_then_host_documents_in_one_session():
+    """the device loader's nodes stay in HBM for the upload; documents the host loader appends after
+    them (and refused ones) cross PCIe on their own: the report equals an all-host session's"""
+    rules = rule_pack()
+    dev_texts = synth.cfn_corpus(10, start=900, n_resources=12) + [
+        '{"Resources": {"a": {"Type": "AWS::S3::Bucket"}, "a": {"Type": "AWS::IAM::Role"}}}']
+    host_texts = synth.cfn_corpus(5, start=950, n_resources=9)
+    names = ["d%d.json" % i for i in range(len(dev_texts) + len(host_texts))]
+    s = guard_amd.Session()
+    for name, text in rules:
+        s.add_rules(text, name)
+    st = s.add_docs_device(dev_texts, names[:len(dev_texts)])
+    assert st is not None and st["refused_docs"] == 1
+    s.add_docs(host_texts, names[len(dev_texts):])
+    s.eval(1)
+    got = s.report()
+    s.close()
+    assert got == _session(rules, dev_texts + host_texts, names, False)
+
+
 def _session(rules, texts, names, device):
     s = guard_amd.Session()
     for name, text in rules:
