@@ -32,8 +32,19 @@ to the host, and the structured JSON report rendered on the host (report_bytes, 
 the evaluations/s that total gives.
 
 --workload: cfg2 (default; BASELINE.json configs[1], the metric's config), cfg3 (the same corpus x
-the 22-file full-registry stand-in, configs[2]) or cfg5 (AWS Config snapshots x the
-network-reachability regex / join pack, configs[4]; --docs snapshots of ~33 CIs each).
+the 22-file full-registry stand-in, configs[2]), cfg4 (Terraform plan JSON with 200-2000
+resource_changes and module nesting 6-10 deep x the terraform-infra-related pack, configs[3];
+--docs plans, synth.tf_bench_corpus) or cfg5 (AWS Config snapshots x the network-reachability regex /
+join pack, configs[4]; --docs snapshots of ~33 CIs each).
+
+Host CPUs: the CPU share of this process -- its affinity set, capped by the pool's per-GPU allotment
+when the box declares one (OMP_NUM_THREADS; 16 host CPUs per GPU on the MI355X pool) -- sizes the
+cpu_baseline processes, the host loader threads and the report threads; the line names it with the
+machine's nproc and CPU model.
+
+Regex memo (DevProg::rx_memo, DESIGN.md 4.1): bench zeroes it before every launch by default
+(--rx-memo per-launch), so every timed step pays its own first DFA runs; --rx-memo warm keeps the
+library default (zeroed once per upload).
 """
 import argparse
 import json
@@ -57,17 +68,43 @@ def log(msg):
 
 
 def _cpu_share():
+    """host CPUs this process may use: its affinity set, capped by the per-GPU allotment the box declares
+    (OMP_NUM_THREADS: 16 per GPU on the MI355X pool, which also bounds worker pools there)"""
     try:
         n = len(os.sched_getaffinity(0))
     except Exception:
         n = os.cpu_count() or 1
-    return max(1, min(16, n))
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
+def host_info():
+    """the host the CPU figures ran on"""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except Exception:
+        aff = None
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": aff,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "cpu_share": _cpu_share()}
 
 
 def _workload_docs(workload, first, n, n_resources):
     import synth
     if workload == "cfg5":
         return synth.config_corpus(n, start=first)
+    if workload == "cfg4":
+        return synth.tf_bench_corpus(n, start=first)
     return synth.cfn_corpus(n, start=first, n_resources=n_resources)
 
 
@@ -109,7 +146,7 @@ def cpu_baseline(workload, n_resources, per_core):
     busy = max(r[0] for r in res)
     busy_eval = max(r[1] for r in res)
     return {"value": round(evals / busy, 2), "unit": "evals/s", "cores": cores, "kind": "port",
-            "eval_only_value": round(evals / busy_eval, 2),
+            "eval_only_value": round(evals / busy_eval, 2), "host": host_info(),
             "sample": "%d %s documents x %d rules files (%d evals) through the Python restatement of the reference "
                       "(oracle/guard_oracle, not the reference binary), one process per core; value = load + evaluate + "
                       "structured report, eval_only_value = evaluation alone; %.1f s wall"
@@ -151,9 +188,14 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", choices=("cfg2", "cfg3", "cfg5"), default="cfg2")
-    ap.add_argument("--docs", type=int, default=0, help="documents per GPU (default: 1M templates; cfg5 303031 "
-                                                         "snapshots = 10M configuration items)")
+    ap.add_argument("--workload", choices=("cfg2", "cfg3", "cfg4", "cfg5"), default="cfg2")
+    ap.add_argument("--docs", type=int, default=0, help="documents per GPU (default: 1M templates; cfg4 8192 plans; "
+                                                         "cfg5 303031 snapshots = 10M configuration items)")
+    ap.add_argument("--mode", choices=("auto", "lane", "wave"), default="auto",
+                    help="evaluation kernel: one tile per lane (+ wave-mode retry), one tile per wavefront, or the "
+                         "library's choice (gg_session_configure)")
+    ap.add_argument("--rx-memo", choices=("per-launch", "warm"), default="per-launch",
+                    help="regex is_match memo: zeroed before every launch, or kept warm across launches")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--e2e-report-docs", type=int, default=0,
                     help="documents whose structured report is rendered for e2e (0: all, the default); a sample's "
@@ -163,18 +205,20 @@ def main():
     ap.add_argument("--loader", choices=("device", "host"), default="device",
                     help="document loader: the MI355X JSON loader (csrc/json_gpu.hip; documents outside its "
                          "subset are built on host threads), or host threads only")
-    ap.add_argument("--gather-docs", type=int, default=200,
-                    help="N > 1: each rank renders the structured JSON report of its first GATHER_DOCS documents "
-                         "and rank 0 gathers them (sharding.gather_report; outside the timed region)")
+    ap.add_argument("--gather-docs", type=int, default=-1,
+                    help="N > 1: the structured JSON report of each rank's first GATHER_DOCS documents (-1: all, the "
+                         "default; 0: none) streamed to rank 0 in blocks (sharding.stream_report; outside the timed "
+                         "region), where a counting sink consumes it")
+    ap.add_argument("--gather-block", type=int, default=4096, help="documents per streamed report block")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-per-core", type=int, default=0)
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL); gloo only to rehearse N ranks sharing one GPU (GG_BENCH_DEVICE)")
     args = ap.parse_args()
     if not args.docs:
-        args.docs = 303_031 if args.workload == "cfg5" else 1_000_000
+        args.docs = {"cfg5": 303_031, "cfg4": 8192}.get(args.workload, 1_000_000)
     if not args.cpu_per_core:
-        args.cpu_per_core = {"cfg2": 400, "cfg3": 120, "cfg5": 600}[args.workload]
+        args.cpu_per_core = {"cfg2": 400, "cfg3": 120, "cfg4": 2, "cfg5": 600}[args.workload]
 
     import torch
     import guard_amd
@@ -192,9 +236,11 @@ def main():
         log("cpu baseline: %s evals/s" % cpu["value"])
     first, count = sharding.shard_range(rank, world, args.docs)
     texts = None
-    if args.workload == "cfg5":
+    t_gen = 0.0
+    if args.workload in ("cfg4", "cfg5"):
+        log("generate %d %s documents" % (count, args.workload))
         t0 = time.time()
-        texts = generate_docs("cfg5", first, count, args.resources, _cpu_share())
+        texts = generate_docs(args.workload, first, count, args.resources, _cpu_share())
         t_gen = time.time() - t0
     dist = None
     if world > 1:
@@ -209,22 +255,37 @@ def main():
     threads = args.threads or _cpu_share()
     rules = rulepack.rule_pack(args.workload)
     sess = guard_amd.Session()
+    if args.mode != "auto":
+        sess.configure(mode=1 if args.mode == "wave" else 0)
+    sess.set_option("rx_memo_per_launch", args.rx_memo == "per-launch")
     for name, text in rules:
         sess.add_rules(text, name)
     log("load %d documents" % count)
     t0 = time.time()
     load_stats = None
+    n_ci = 0
     if texts is not None:
-        sess.add_docs(texts, ["snapshot-%d.json" % (first + i) for i in range(count)], threads=threads)
-        n_ci = sum(t.count('"configurationItemStatus"') for t in texts)
+        prefix = "snapshot" if args.workload == "cfg5" else "plan"
+        names = ["%s-%d.json" % (prefix, first + i) for i in range(count)]
+        if args.workload == "cfg5":
+            n_ci = sum(t.count('"configurationItemStatus"') for t in texts)
+        n_changes = sum(t.count('"change":{') for t in texts) if args.workload == "cfg4" else 0
+        if args.loader == "device":
+            load_stats = sess.add_docs_device(texts, names)
+            if load_stats is None:
+                raise RuntimeError("device loader refused the %s corpus" % args.workload)
+        else:
+            sess.add_docs(texts, names, threads=threads)
         texts = None
     elif args.loader == "device":
         load_stats = sess.add_synthetic_device(first, count, n_resources=args.resources, threads=threads)
         if load_stats is None:
             raise RuntimeError("device loader refused the synthetic corpus")
-        load_stats["text_GBps"] = round(load_stats["text_bytes"] / (load_stats["kernel_ms"] / 1e3) / 1e9, 2)
+        t_gen = load_stats["gen_ms"] / 1e3
     else:
         sess.add_synthetic(first, count, n_resources=args.resources, threads=threads)
+    if load_stats is not None:
+        load_stats["text_GBps"] = round(load_stats["text_bytes"] / (load_stats["kernel_ms"] / 1e3) / 1e9, 2)
     t_load = time.time() - t0
     log("upload (load %.1f s)" % t_load)
     t0 = time.time()
@@ -281,20 +342,35 @@ def main():
     n_fail, n_pass, n_skip, n_err = sess.stat(4), sess.stat(5), sess.stat(6), sess.stat(7)
 
     gather = None
-    if world > 1 and args.gather_docs > 0:
-        # the report half of the multi-GPU path: every rank renders its documents'
-        # reports, rank 0 receives them over the collective backend (RCCL: device buffers) and
-        # stitches them in rank order with the job's exit code
+    if world > 1 and args.gather_docs != 0:
+        # the report half of the multi-GPU path: every rank renders its documents' reports
+        # in blocks, rank 0 receives them over the collective backend (RCCL: device buffers) in rank order
+        # and joins them into the job's report as they arrive -- here into a sink that counts the bytes
+        gdocs = ndocs if args.gather_docs < 0 else min(ndocs, args.gather_docs)
+
+        class _CountingSink:
+            n = 0
+            last = 0.0
+
+            def write(self, piece):
+                self.n += len(piece)
+                if time.time() - self.last > 20:
+                    self.last = time.time()
+                    log("gather: %.1f GB at rank 0" % (self.n / 1e9))
+
+        sink = _CountingSink() if rank == 0 else None
+        log("gather: streaming the JSON report of %d documents per rank to rank 0" % gdocs)
+        dist.barrier()
         t0 = time.time()
-        text, code = sess.report_range("json", 0, min(ndocs, args.gather_docs))
-        t_render = time.time() - t0
-        t0 = time.time()
-        merged, job_code = sharding.gather_report(text, code, dist, output="json")
+        job_code, gerr = sharding.stream_report(lambda f, c: sess.report_range_raw("json", f, c)[0], gdocs,
+                                                sess.exit_code("json"), dist, sink, output="json",
+                                                block_docs=args.gather_block, raw=True)
         t_gather = time.time() - t0
         if rank == 0:
-            gather = {"docs_per_rank": min(ndocs, args.gather_docs), "render_s": round(t_render, 3),
-                      "gather_s": round(t_gather, 3), "bytes": len(merged.encode()), "exit_code": job_code,
-                      "file_reports": merged.count('\n  {\n    "name": ')}
+            gather = {"docs_per_rank": gdocs, "docs": gdocs * world, "block_docs": args.gather_block,
+                      "gather_s": round(t_gather, 3), "bytes": sink.n,
+                      "GBps_at_rank0": round(sink.n / max(t_gather, 1e-9) / 1e9, 3), "exit_code": job_code,
+                      "error": gerr}
 
     e2e = None
     if rank == 0 and world == 1 and not args.no_e2e:
@@ -307,23 +383,34 @@ def main():
         # the synthetic documents are alike: the whole report costs ndocs / rdocs times the sample
         t_report = t_report_sample * ndocs / max(1, rdocs)
         t_eval = k_mean_ms / 1e3 + t_fetch
-        total = t_load + t_upload + t_eval + t_report
-        e2e = {"value": round(ntiles / total, 1), "unit": "evals/s", "load_s": round(t_load, 3),
+        # the documents' text is the job's input, resident in host memory when the job starts (a user's
+        # files): synthetic text generation is reported apart (gen_s), not counted in load_s -- except
+        # with --loader host on cfg2/3, where the native generator runs inside the host loader's threads
+        gen_in_load = args.loader == "host" and args.workload in ("cfg2", "cfg3")
+        t_load_job = t_load - (t_gen if (args.loader == "device" and args.workload in ("cfg2", "cfg3")) else 0.0)
+        total = t_load_job + t_upload + t_eval + t_report
+        e2e = {"value": round(ntiles / total, 1), "unit": "evals/s", "load_s": round(t_load_job, 3),
+               "gen_s": round(t_gen, 3), "gen_in_load": gen_in_load,
                "upload_s": round(t_upload, 3), "eval_fetch_s": round(t_eval, 3), "report_s": round(t_report, 3),
                "report_docs_rendered": rdocs, "report_s_rendered": round(t_report_sample, 3),
                "report_bytes_rendered": rep_bytes, "report_GBps": round(rep_bytes / t_report_sample / 1e9, 3),
-               "exit_code": rep_code, "report_threads": min(16, _cpu_share()),
+               "exit_code": rep_code, "report_threads": threads,
                "pcie_inclusive_value": round(ntiles / (t_upload + t_eval), 1),
-               "note": "one job: host load (incl. synthetic text generation%s) + upload + one evaluation with "
+               "note": "one job over input text resident in host memory: load (%s) + upload + one evaluation with "
                        "statuses/records fetched + structured JSON report rendered on the host and discarded "
-                       "(rendered for report_docs_rendered documents; report_s scaled to all when that is fewer)"
-                       % (", %.1f s of Python generation excluded" % t_gen if args.workload == "cfg5" else "")}
+                       "(rendered for report_docs_rendered documents; report_s scaled to all when that is fewer); "
+                       "synthetic text generation (gen_s) is not part of the job%s"
+                       % ("device JSON loader: text H2D, parse, arena D2H for the reporter" if args.loader == "device"
+                          else "host loader threads", " (inside load_s with --loader host)" if gen_in_load else "")}
 
     total_units = ntiles * world * args.steps
     value = total_units / elapsed
     if args.workload == "cfg5":
         workload = ("cfg5: %d AWS Config snapshots/GPU (%d configuration items) x %d-file network-reachability pack"
                     % (args.docs, n_ci * world, nfiles))
+    elif args.workload == "cfg4":
+        workload = ("cfg4: %d Terraform plans/GPU (%d resource_changes, 200-2000 per plan) x %d-file terraform pack"
+                    % (args.docs, n_changes * world, nfiles))
     else:
         workload = "%s: %d synthetic CFN templates/GPU (%d resources) x %d-file rule pack" % (
             args.workload, args.docs, args.resources, nfiles)
@@ -353,7 +440,9 @@ def main():
                        "loader": args.loader, "load_s": round(t_load, 2), "host_threads": threads,
                        "upload_s": round(t_upload, 2), "device_loader": load_stats,
                        "rule_tallies_sum": tally_sum, "rule_tallies_fetched": int(sum(tally)),
-                       "lane_tiles_retried_in_wave_mode": sess.stat(16)},
+                       "lane_tiles_retried_in_wave_mode": sess.stat(16),
+                       "kernel_mode": sess.stat(20), "regex_memo": args.rx_memo,
+                       "host": host_info()},
         }
         line["cpu_baseline"] = cpu
         line["e2e"] = e2e

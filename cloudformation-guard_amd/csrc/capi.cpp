@@ -10,6 +10,8 @@
 // library reports an explicit error when no HIP device is present.
 #include <hip/hip_runtime.h>
 
+#include <sched.h>
+
 #include <atomic>
 #include <chrono>
 #include <cstdlib>
@@ -77,34 +79,50 @@ void set_note(extern_err_t* err, const std::string& msg) {
 
 #define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { throw std::runtime_error(std::string("HIP: ") + hipGetErrorString(e_) + " at " #x); } } while (0)
 
+// Device contexts, created lazily per HIP device under one mutex ("device contexts
+// created lazily and guarded by a mutex").  The single-device entry points use the process default
+// device: the device current on the first calling thread -- torch.cuda.set_device(LOCAL_RANK) in a
+// one-process-per-GPU job -- or GG_DEVICE.  cfn_guard_validate_batch_devices names its devices.
+static constexpr int kMaxDevices = 64;
 struct DeviceState {
-  std::mutex mu;
   bool ready = false;
-  int device = 0;
   int ncu = 256;
-  std::string error;
-  hipStream_t stream = nullptr;
-  // One device per process (one process per GPU): the device current on the
-  // first calling thread -- torch.cuda.set_device(LOCAL_RANK) in a multi-GPU job -- or GG_DEVICE.
-  bool init() {
-    if (ready) return true;
-    int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) { error = "no HIP device available (the MI355X path has no CPU fallback)"; return false; }
-    int dev = 0;
-    if (const char* e = getenv("GG_DEVICE")) dev = atoi(e);
-    else if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-    if (dev < 0 || dev >= n) { error = "GG_DEVICE / current device out of range"; return false; }
-    device = dev;
-    if (hipSetDevice(dev) != hipSuccess) { error = "hipSetDevice failed"; return false; }
+};
+struct Devices {
+  std::mutex mu;
+  int count = -1;    // visible devices (-1: not probed yet)
+  int def = -1;      // process default device (-1: not resolved yet)
+  DeviceState dev[kMaxDevices];
+  // under mu: probes the devices once, initialises device d
+  bool init(int d, std::string& why) {
+    if (count < 0) {
+      int n = 0;
+      if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+      count = std::min(n, kMaxDevices);
+    }
+    if (count == 0) { why = "no HIP device available (the MI355X path has no CPU fallback)"; return false; }
+    if (d < 0 || d >= count) { why = "HIP device " + std::to_string(d) + " out of range (" + std::to_string(count) + " visible)"; return false; }
+    DeviceState& D = dev[d];
+    if (D.ready) return true;
+    if (hipSetDevice(d) != hipSuccess) { why = "hipSetDevice failed"; return false; }
     hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, dev) == hipSuccess) ncu = prop.multiProcessorCount;
+    if (hipGetDeviceProperties(&prop, d) == hipSuccess) D.ncu = prop.multiProcessorCount;
     hipDeviceSetLimit(hipLimitStackSize, 16384);
-    if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) { error = "stream creation failed"; return false; }
-    ready = true;
+    D.ready = true;
     return true;
   }
+  int resolve_default(std::string& why) {
+    if (def >= 0) return def;
+    int d = 0;
+    if (const char* e = getenv("GG_DEVICE")) d = atoi(e);
+    else if (hipGetDevice(&d) != hipSuccess) d = 0;
+    if (!init(d, why)) { if (why.find("out of range") != std::string::npos) why = "GG_DEVICE / current device out of range"; return -1; }
+    def = d;
+    return d;
+  }
 };
-DeviceState g_dev;
+Devices g_devs;
+int dev_ncu(int d) { return g_devs.dev[d >= 0 && d < kMaxDevices ? d : 0].ncu; }
 
 template <class T>
 struct DBuf {
@@ -233,9 +251,11 @@ struct DeviceBufs {
   DBuf<unsigned long long> d_counts;   // per (file, top rule) x {PASS, FAIL, SKIP, error}
   DBuf<unsigned long long> d_stats;    // diagnostic counters (stats build variant)
   hipStream_t stream = nullptr;
+  int device = 0;               // the HIP device every buffer above lives on
   std::vector<std::pair<hipEvent_t, hipEvent_t>> evq;   // launch brackets, reused
-  DeviceBufs() { HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking)); }
+  explicit DeviceBufs(int d) : device(d) { HIPCHK(hipSetDevice(d)); HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking)); }
   ~DeviceBufs() {
+    hipSetDevice(device);
     for (auto& pr : evq) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
     if (stream) hipStreamDestroy(stream);
   }
@@ -253,22 +273,23 @@ struct BufPool {
   static constexpr size_t kMaxFree = 8;               // idle sets kept
   static constexpr size_t kMaxKeepBytes = 1ull << 30; // larger sets (batch jobs) are freed, not kept
 };
-BufPool g_pool;
+BufPool g_pool[kMaxDevices];   // one per device: a set's buffers and stream belong to its device
 
-DeviceBufs* acquire_bufs() {
+DeviceBufs* acquire_bufs(int d) {
   {
-    std::lock_guard<std::mutex> lk(g_pool.mu);
-    if (!g_pool.free.empty()) { DeviceBufs* b = g_pool.free.back(); g_pool.free.pop_back(); return b; }
+    std::lock_guard<std::mutex> lk(g_pool[d].mu);
+    if (!g_pool[d].free.empty()) { DeviceBufs* b = g_pool[d].free.back(); g_pool[d].free.pop_back(); return b; }
   }
-  return new DeviceBufs();
+  return new DeviceBufs(d);
 }
 
 void release_bufs(DeviceBufs* b) {
   if (!b) return;
+  hipSetDevice(b->device);
   if (b->bytes() <= BufPool::kMaxKeepBytes) {
     if (hipStreamSynchronize(b->stream) == hipSuccess) {
-      std::lock_guard<std::mutex> lk(g_pool.mu);
-      if (g_pool.free.size() < BufPool::kMaxFree) { g_pool.free.push_back(b); return; }
+      std::lock_guard<std::mutex> lk(g_pool[b->device].mu);
+      if (g_pool[b->device].free.size() < BufPool::kMaxFree) { g_pool[b->device].free.push_back(b); return; }
     }
   }
   delete b;
@@ -282,7 +303,8 @@ struct gg_session {
   std::vector<std::unique_ptr<GpuProgram>> progs;
   std::vector<std::string> parse_errors;   // rules files that failed to parse (exit code 5)
   std::unique_ptr<DocBatch> params;        // merged input parameters (validate -i), one document
-  // device residency: buffers borrowed from the device-state pool at upload (DeviceBufs)
+  int device = -1;                         // HIP device (-1: the process default, resolved at first use)
+  // device residency: buffers borrowed from the device's pool at upload (DeviceBufs)
   DeviceBufs* dv = nullptr;
   uint32_t type_key = NONE;
   bool has_order = false;   // d_order holds a lane-mode document order (shape-sorted batches)
@@ -311,6 +333,8 @@ struct gg_session {
   int32_t mode = 0;               // 0: lane mode + wave-mode retry; 1: wave mode only
   bool verbose = false;           // wave mode recording the EventRecord tree (guard_eval_verbose_kernel)
   size_t rec_cap = 0;
+  size_t rx_memo_words = 0;       // words of the regex is_match memo (0: none)
+  bool rx_memo_per_launch = false;   // zero the memo before every launch (bench: no warm memo across steps)
   // results
   std::vector<TileOut> tiles;
   std::vector<uint8_t> rule_status;
@@ -319,26 +343,39 @@ struct gg_session {
   double last_kernel_ms = 0;
   std::string last_error;
   ~gg_session() {
+    if (device >= 0) hipSetDevice(device);
     // work enqueued on a caller stream (gg_session_set_stream) may still read or write these buffers:
     // drain it before the set goes back to the pool, where the next session's uploads reuse it
     if (dv && stream) hipStreamSynchronize(stream);
     release_bufs(dv);
-    if (dev_nodes) hipFree(dev_nodes);
+    if (dev_nodes) { if (device >= 0) hipSetDevice(device); hipFree(dev_nodes); }
   }
 };
 
 namespace {
 
-bool ensure_device(std::string& why) {
-  std::lock_guard<std::mutex> lk(g_dev.mu);
-  if (!g_dev.init()) { why = g_dev.error; return false; }
-  // the current device is per host thread: FFI callers may arrive on any thread
-  if (hipSetDevice(g_dev.device) != hipSuccess) { why = "hipSetDevice failed"; return false; }
+// makes device `d` (-1: the process default) current on this host thread, creating its context on
+// first use; *out receives the ordinal.  The current device is per host thread: FFI callers may arrive
+// on any thread.
+bool ensure_device(std::string& why, int d = -1, int* out = nullptr) {
+  std::lock_guard<std::mutex> lk(g_devs.mu);
+  if (d < 0) { d = g_devs.resolve_default(why); if (d < 0) return false; }
+  else if (!g_devs.init(d, why)) return false;
+  if (hipSetDevice(d) != hipSuccess) { why = "hipSetDevice failed"; return false; }
+  if (out) *out = d;
   return true;
 }
 
+// the session's device current on this thread (resolving the process default on first use)
+void bind_device(gg_session* s) {
+  std::string why;
+  if (!ensure_device(why, s->device, &s->device)) throw std::runtime_error(why);
+}
+
 void session_upload(gg_session* s) {
-  if (!s->dv) s->dv = acquire_bufs();
+  bind_device(s);
+  if (s->dv && s->dv->device != s->device) { release_bufs(s->dv); s->dv = nullptr; HIPCHK(hipSetDevice(s->device)); }
+  if (!s->dv) s->dv = acquire_bufs(s->device);
   hipStream_t st = s->dv->stream;
   {
     // host arena (32 B nodes) -> device arena (16 B packed nodes + key-length column)
@@ -369,7 +406,7 @@ void session_upload(gg_session* s) {
     bad.alloc(1);
     HIPCHK(hipMemsetAsync(bad.p, 0, 4, st));
     if (n) {
-      const uint32_t blocks = (uint32_t)std::min<size_t>((n + 255) / 256, (size_t)g_dev.ncu * 64);
+      const uint32_t blocks = (uint32_t)std::min<size_t>((n + 255) / 256, (size_t)dev_ncu(s->device) * 64);
       hipLaunchKernelGGL(pack_nodes_kernel, dim3(blocks), dim3(256), 0, st, src, s->dv->d_nodes.p, s->dv->d_klen.p, (uint64_t)n, bad.p);
       HIPCHK(hipGetLastError());
     }
@@ -418,7 +455,7 @@ void session_upload(gg_session* s) {
       B.nodes = s->dv->d_nodes.p; B.klen = s->dv->d_klen.p; B.bytes = s->dv->d_bytes.p; B.roots = s->dv->d_roots.p;
       B.base = s->dv->d_base.p; B.ndocs = (uint32_t)nd;
       B.res_map = s->dv->d_res_map.p; B.tix_off = s->dv->d_tix_off.p; B.tix = s->dv->d_tix.p; B.type_key = s->type_key;
-      const uint32_t blocks = std::min<uint32_t>((B.ndocs + 3) / 4, g_dev.ncu * 16);
+      const uint32_t blocks = std::min<uint32_t>((B.ndocs + 3) / 4, dev_ncu(s->device) * 16);
       hipLaunchKernelGGL(resource_type_kernel, dim3(blocks), dim3(256), 0, st, B);
       HIPCHK(hipGetLastError());
       // Shape-sorted batches: the lane kernel's 64 lanes run in lock-step, so a batch costs the union
@@ -463,7 +500,7 @@ void session_upload(gg_session* s) {
         d_top.upload(top8, 8, st);
         DBuf<unsigned long long> d_key;
         d_key.alloc(nd);
-        hipLaunchKernelGGL(shape_key_kernel, dim3(std::min<uint32_t>((uint32_t)((nd + 255) / 256), g_dev.ncu * 16)), dim3(256), 0, st,
+        hipLaunchKernelGGL(shape_key_kernel, dim3(std::min<uint32_t>((uint32_t)((nd + 255) / 256), dev_ncu(s->device) * 16)), dim3(256), 0, st,
                            B, (const uint32_t*)d_top.p, d_key.p);
         HIPCHK(hipGetLastError());
         std::vector<unsigned long long> key(nd);
@@ -494,6 +531,7 @@ void session_upload(gg_session* s) {
   size_t memo_total = 0;
   for (auto& p : s->progs) memo_total += (size_t)p->prog.hdr.n_regex * memo_words;
   const bool memo_on = memo_total && (!getenv("GG_RX_MEMO") || atoi(getenv("GG_RX_MEMO")) != 0);
+  s->rx_memo_words = memo_on ? memo_total : 0;
   if (memo_on) {
     s->dv->d_rx_memo.alloc(memo_total);
     HIPCHK(hipMemsetAsync(s->dv->d_rx_memo.p, 0, memo_total * 4, st));
@@ -518,14 +556,14 @@ void session_upload(gg_session* s) {
   size_t ntiles = s->docs.ndocs() * s->progs.size();
   size_t nbatches = (s->docs.ndocs() + 63) / 64 * s->progs.size();
   // wave mode: all tiles (mode 1) or only the lane kernel's overflow tiles (mode 0)
-  size_t wave_slots = s->mode == 1 ? (size_t)g_dev.ncu * 8 : (size_t)g_dev.ncu * 2;
+  size_t wave_slots = s->mode == 1 ? (size_t)dev_ncu(s->device) * 8 : (size_t)dev_ncu(s->device) * 2;
   uint32_t slots = (uint32_t)std::min<size_t>(std::max<size_t>(ntiles, 1), wave_slots);
   s->nslots = slots;
   s->dv->d_heaps.alloc((size_t)slots * s->heap_bytes);
   // lane-mode grid: waves per CU (default 8 = the kernel's occupancy at 2 waves/SIMD)
   size_t lane_waves_per_cu = 16;   // 4 waves per SIMD (build.py GG_LANE_WAVES_PER_EU); LDS holds 16 at cfg-2 program sizes
   if (const char* e = getenv("GG_LANE_WAVES_PER_CU")) lane_waves_per_cu = std::max(1, atoi(e));
-  s->lane_slots = s->mode == 1 ? 0 : (uint32_t)std::min<size_t>(std::max<size_t>(nbatches, 1), (size_t)g_dev.ncu * lane_waves_per_cu);
+  s->lane_slots = s->mode == 1 ? 0 : (uint32_t)std::min<size_t>(std::max<size_t>(nbatches, 1), (size_t)dev_ncu(s->device) * lane_waves_per_cu);
   // every one of the 8 per-XCD queues needs waves (block b serves queue b % 8)
   if (s->lane_slots) s->lane_slots = (std::max<uint32_t>(s->lane_slots, 8u) + 7u) & ~7u;
   s->dv->d_lane_heaps.alloc((size_t)s->lane_slots * 64 * s->lane_heap_bytes);
@@ -550,11 +588,16 @@ hipStream_t session_stream(gg_session* s) { return s->stream ? s->stream : s->dv
 
 // enqueues one evaluation of every tile (and the per-rule tally) on the session stream; no host sync
 void session_launch(gg_session* s) {
+  bind_device(s);
   hipStream_t st = session_stream(s);
   uint32_t ntiles = (uint32_t)(s->docs.ndocs() * s->progs.size());
   HIPCHK(hipMemsetAsync(s->dv->d_counters.p, 0, 32 * sizeof(uint32_t), st));
   unsigned long long* counts = s->ext_counts ? s->ext_counts : s->dv->d_counts.p;
   HIPCHK(hipMemsetAsync(counts, 0, s->ncounts * sizeof(unsigned long long), st));
+  // regex memo policy: by default it is zeroed once per upload and stays warm across launches (a pure
+  // function of the interned string); per-launch zeroing makes every launch pay its first DFA runs
+  if (s->rx_memo_per_launch && s->rx_memo_words)
+    HIPCHK(hipMemsetAsync(s->dv->d_rx_memo.p, 0, s->rx_memo_words * 4, st));
   LaunchArgs A{};
   A.docs.nodes = s->dv->d_nodes.p; A.docs.klen = s->dv->d_klen.p; A.docs.bytes = s->dv->d_bytes.p; A.docs.roots = s->dv->d_roots.p; A.docs.base = s->dv->d_base.p; A.docs.ndocs = (uint32_t)s->docs.ndocs();
   A.docs.res_map = s->dv->d_res_map.p; A.docs.tix_off = s->dv->d_tix_off.p; A.docs.tix = s->dv->d_tix.p; A.docs.type_key = s->type_key;
@@ -602,7 +645,7 @@ void session_launch(gg_session* s) {
     HIPCHK(hipGetLastError());
   }
   HIPCHK(hipEventRecord(s->ev1, st));
-  uint32_t cblocks = std::min<uint32_t>((ntiles + 255) / 256, g_dev.ncu * 4);
+  uint32_t cblocks = std::min<uint32_t>((ntiles + 255) / 256, dev_ncu(s->device) * 4);
   hipLaunchKernelGGL(rule_count_kernel, dim3(cblocks), dim3(256), s->ncounts * sizeof(uint32_t), st, s->dv->d_tiles.p,
                      s->dv->d_rule_status.p, s->dv->d_progs.p, A.nfiles, ntiles, s->max_top, counts);
   HIPCHK(hipGetLastError());
@@ -612,6 +655,7 @@ void session_launch(gg_session* s) {
 // waits for the last launch; returns the evaluation kernel's milliseconds (HIP events on its stream)
 double session_wait(gg_session* s) {
   if (!s->launched) return 0;
+  bind_device(s);
   HIPCHK(hipEventSynchronize(s->ev1));
   float ms = 0;
   HIPCHK(hipEventElapsedTime(&ms, s->ev0, s->ev1));
@@ -622,6 +666,7 @@ double session_wait(gg_session* s) {
 // kernel ms of every launch since the last drain (synchronises on the last one)
 size_t session_drain(gg_session* s, double* out, size_t cap) {
   size_t n = s->nq;
+  if (n) bind_device(s);
   if (n) HIPCHK(hipEventSynchronize(s->dv->evq[n - 1].second));
   for (size_t i = 0; i < n; i++) {
     float ms = 0;
@@ -641,6 +686,7 @@ uint32_t session_records_wanted(gg_session* s) {
 }
 
 void session_fetch(gg_session* s) {
+  bind_device(s);
   // the tally kernel runs after ev1 on a non-blocking stream: wait for the whole launch
   HIPCHK(hipStreamSynchronize(session_stream(s)));
   uint32_t ntiles = (uint32_t)(s->docs.ndocs() * s->progs.size());
@@ -687,53 +733,110 @@ double session_run(gg_session* s, bool fetch) {
   return ms;
 }
 
-// host threads for report rendering: GG_REPORT_THREADS, else the CPU share (at most 16)
+// host threads for report rendering and host loading: GG_REPORT_THREADS, else the process's CPU share --
+// its affinity set, capped by OMP_NUM_THREADS when the host declares an allotment (the MI355X pool: 16
+// host CPUs per GPU)
 unsigned report_threads() {
   if (const char* e = getenv("GG_REPORT_THREADS")) return (unsigned)std::max(1, atoi(e));
   unsigned n = std::thread::hardware_concurrency();
-  return std::max(1u, std::min(16u, n ? n : 1u));
+  cpu_set_t cs;
+  if (sched_getaffinity(0, sizeof(cs), &cs) == 0 && CPU_COUNT(&cs) > 0) n = (unsigned)CPU_COUNT(&cs);
+  if (const char* o = getenv("OMP_NUM_THREADS")) { const int k = atoi(o); if (k > 0) n = std::min(n, (unsigned)k); }
+  return std::max(1u, n ? n : 1u);
 }
 
-// structured report over (docs x programs) in format `fmt` (OutFormat); false + err for an aborting error
-// (cstr != null and JSON: the report goes to *cstr, a malloc'd buffer, without an intermediate string)
-// Documents [first, first + count) only (count SIZE_MAX: to the end): the report a run over just those
-// documents writes -- a rank's shard of a multi-GPU job (sharding.gather_report stitches them).
-bool session_report(gg_session* s, std::string& out, int32_t& exit_code, ReportError& err, int32_t fmt = OUT_JSON,
-                    char** cstr = nullptr, size_t first = 0, size_t count = SIZE_MAX) {
-  exit_code = s->parse_errors.empty() ? 0 : 5;
-  std::vector<const Program*> progs;
-  for (auto& p : s->progs) progs.push_back(&p->prog);
-  size_t nf = progs.size();
-  first = std::min(first, s->docs.ndocs());
-  const size_t nd = std::min(count, s->docs.ndocs() - first);
-  const size_t t0 = first * nf, t1 = (first + nd) * nf;
+// One shard of a structured report: documents [first, first + count) of a fetched session.
+struct ShardView {
+  gg_session* s;
+  size_t first, count;
+};
+
+// The structured report (format `fmt`, OutFormat) of shards in order -- each a contiguous document range
+// of its own session, together the job's documents in order -- joined into the bytes one session over all
+// of them writes: JSON parts concatenated, YAML streams concatenated, SARIF / JUnit writers absorbed in
+// order (so a job sharded over devices reports exactly as the one-device run).  false + err for an
+// aborting error.  (cstr != null and JSON: the report goes to *cstr, a malloc'd buffer, without an
+// intermediate string.)
+bool shards_report(const std::vector<ShardView>& sh, std::string& out, int32_t& exit_code, ReportError& err, int32_t fmt,
+                   char** cstr) {
+  exit_code = sh.empty() || sh[0].s->parse_errors.empty() ? 0 : 5;
   // the first tile in (doc, rules-file) order that raised an error aborts the run (structured.rs:110)
-  for (size_t t = t0; t < t1; t++) {
-    if (s->tiles[t].err) {
-      tile_error(s->docs, (uint32_t)(t / nf), *progs[t % nf], s->tiles[t], err);
-      exit_code = -1;
-      return false;
+  for (const ShardView& v : sh) {
+    const size_t nf = v.s->progs.size();
+    for (size_t t = v.first * nf; t < (v.first + v.count) * nf; t++) {
+      if (v.s->tiles[t].err) {
+        std::vector<const Program*> progs;
+        for (auto& p : v.s->progs) progs.push_back(&p->prog);
+        tile_error(v.s->docs, (uint32_t)(t / nf), *progs[t % nf], v.s->tiles[t], err);
+        exit_code = -1;
+        return false;
+      }
     }
   }
   out.clear();
-  auto tile = [&](size_t d, size_t f) {
-    return tile_view(s->tiles.data(), s->rule_status.data(), s->max_top, s->recs.data(), d * nf + f);
-  };
-  if (fmt == OUT_JSON && cstr) {
-    std::vector<TextBuf> parts;
-    if (!report_batch_json_parts(s->docs, progs, first, nd, tile, report_threads(), parts, err)) { exit_code = -1; return false; }
-    *cstr = json_parts_join(parts);
-  } else if (!report_batch(s->docs, progs, first, nd, tile, fmt, report_threads(), out, err)) {
-    exit_code = -1;
-    return false;
+  std::vector<TextBuf> all_parts;
+  std::vector<std::unique_ptr<ReportWriter>> writers;
+  std::vector<std::string> yaml_parts;
+  bool anyfail = false;
+  for (const ShardView& v : sh) {
+    gg_session* s = v.s;
+    std::vector<const Program*> progs;
+    for (auto& p : s->progs) progs.push_back(&p->prog);
+    const size_t nf = progs.size();
+    auto tile = [&](size_t d, size_t f) {
+      return tile_view(s->tiles.data(), s->rule_status.data(), s->max_top, s->recs.data(), d * nf + f);
+    };
+    bool ok;
+    if (fmt == OUT_JSON && cstr) {
+      std::vector<TextBuf> parts;
+      ok = report_batch_json_parts(s->docs, progs, v.first, v.count, tile, report_threads(), parts, err);
+      for (auto& p : parts) all_parts.push_back(std::move(p));
+    } else {
+      ok = report_batch_writers(s->docs, progs, v.first, v.count, tile, fmt, report_threads(), writers, yaml_parts, err);
+    }
+    if (!ok) { exit_code = -1; return false; }
+    for (size_t t = v.first * nf; t < (v.first + v.count) * nf; t++) if (s->tiles[t].status == ST_FAIL) anyfail = true;
   }
+  if (fmt == OUT_JSON && cstr) *cstr = json_parts_join(all_parts);
+  else out = report_writers_finish(fmt, writers, yaml_parts);
   // exit code 19 when any rules file FAILed; a rules-file parse error set 5 beforehand
   // (structured.rs:40-43).  CommonStructuredReporter overwrites it with 19 (structured.rs:110-112);
   // JunitReporter::update_exit_code keeps 5 (reporters/mod.rs:97-103, validate/xml.rs:62-66).
-  bool anyfail = false;
-  for (size_t t = t0; t < t1; t++) if (s->tiles[t].status == ST_FAIL) anyfail = true;
   if (anyfail && !(fmt == OUT_JUNIT && exit_code == 5)) exit_code = 19;
   return true;
+}
+
+// structured report over (docs x programs) in format `fmt`; documents [first, first + count) only (count
+// SIZE_MAX: to the end): the report a run over just those documents writes -- a rank's shard of a
+// multi-GPU job (sharding.gather_report stitches them).
+bool session_report(gg_session* s, std::string& out, int32_t& exit_code, ReportError& err, int32_t fmt = OUT_JSON,
+                    char** cstr = nullptr, size_t first = 0, size_t count = SIZE_MAX) {
+  first = std::min(first, s->docs.ndocs());
+  const size_t nd = std::min(count, s->docs.ndocs() - first);
+  return shards_report({ShardView{s, first, nd}}, out, exit_code, err, fmt, cstr);
+}
+
+// Contiguous document ranges, one per shard, balanced by text bytes (a document's arena and work are
+// proportional to its text); starts[k] = first document of shard k, starts[nshards] = n.
+// Every shard gets at least one document while documents remain (the algorithm of
+// sharding.shard_ranges_by_bytes).
+void shard_by_bytes(const size_t* lens, size_t n, size_t nshards, size_t* starts) {
+  double total = 0;
+  for (size_t i = 0; i < n; i++) total += (double)lens[i];
+  size_t start = 0;
+  double acc = 0;
+  for (size_t r = 0; r < nshards; r++) {
+    starts[r] = start;
+    const double target = total * (double)(r + 1) / (double)nshards;
+    size_t end = start;
+    while (end < n && (acc + (double)lens[end] <= target || end == start) && n - end > nshards - r - 1) {
+      acc += (double)lens[end];
+      end++;
+    }
+    if (r == nshards - 1) { while (end < n) { acc += (double)lens[end]; end++; } }
+    start = end;
+  }
+  starts[nshards] = n;
 }
 
 // Appends per-thread batches to dst.  Every distinct string of every part is interned into dst's
@@ -976,6 +1079,160 @@ char* cfn_guard_validate_batch_params(const validate_input_t* docs, size_t n_doc
     if (exit_code) *exit_code = -1;
     return nullptr;
   }
+}
+
+// ---------------------------------------------------------------- validate over several GPUs ---
+// cfn_guard_validate_batch_params with the documents sharded over devices: contiguous ranges balanced by
+// text bytes (shard_by_bytes), one host thread per shard that loads its documents (host loader, with the
+// input parameters merged), compiles the rules, uploads, evaluates and fetches on its device; then the
+// shards' reports join in document order (shards_report).  Error precedence is the one-device call's: the
+// first document (in order) that does not load, then a parameter-file error, then the first parameter merge
+// panic, then the first erroring tile, then the first report that aborts.
+namespace {
+char* validate_batch_devices(const validate_input_t* docs, size_t n_docs, const validate_input_t* rules, size_t n_rules,
+                             const validate_input_t* params, size_t n_params, int32_t output_format,
+                             const std::vector<int>& devices, int32_t* exit_code, extern_err_t* err) {
+  const size_t ns = std::max<size_t>(1, std::min(devices.size(), std::max<size_t>(n_docs, 1)));
+  std::vector<size_t> lens(n_docs), starts(ns + 1);
+  for (size_t i = 0; i < n_docs; i++) lens[i] = docs[i].content ? strlen(docs[i].content) : 0;
+  shard_by_bytes(lens.data(), n_docs, ns, starts.data());
+  // the input parameters, loaded once (read-only for the shards' merges)
+  std::unique_ptr<DocBatch> pbatch;
+  LoadError pe;
+  const bool params_ok = load_params(params, n_params, pbatch, pe);
+  struct Shard {
+    gg_session s;
+    size_t load_fail = SIZE_MAX, panic_doc = SIZE_MAX;
+    LoadError le, panic;
+  };
+  std::vector<std::unique_ptr<Shard>> sh(ns);
+  for (auto& x : sh) x.reset(new Shard());
+  // phase 1: load (every shard on its own thread)
+  parallel_run(ns, [&](size_t k) {
+    Shard& S = *sh[k];
+    S.s.device = devices[k];
+    for (size_t i = 0; i < n_rules; i++) {
+      std::string perr;
+      std::string name = rules[i].file_name ? rules[i].file_name : "";
+      if (!add_rules(&S.s, rules[i].content ? rules[i].content : "", name, perr))
+        S.s.parse_errors.push_back("Parsing error handling rule file = " + name + ", Error = " + error_display("ParseError", perr) + "\n---");
+    }
+    for (size_t i = starts[k]; i < starts[k + 1]; i++) {
+      const char* t = docs[i].content ? docs[i].content : "";
+      if (!load_document(S.s.docs, t, lens[i], docs[i].file_name ? docs[i].file_name : "", LOAD_LIBYAML, S.le)) {
+        S.load_fail = i;
+        return;
+      }
+      if (params_ok && S.panic_doc == SIZE_MAX && !merge_params_last(S.s.docs, pbatch.get(), S.panic)) S.panic_doc = i;
+    }
+  });
+  auto fail_with = [&](const std::string& kind, const std::string& msg) -> char* {
+    set_err(err, ffi_code(kind), error_display(kind, msg));
+    if (exit_code) *exit_code = -1;
+    return nullptr;
+  };
+  for (auto& x : sh) if (x->load_fail != SIZE_MAX) return fail_with(x->le.kind, x->le.msg);
+  if (!params_ok) return fail_with(pe.kind, pe.msg);
+  for (auto& x : sh) if (x->panic_doc != SIZE_MAX) return fail_with(x->panic.kind, x->panic.msg);
+  // phase 2: evaluate (every shard on its own thread and device)
+  parallel_run(ns, [&](size_t k) {
+    Shard& S = *sh[k];
+    if (S.s.progs.empty() || S.s.docs.ndocs() == 0) {
+      S.s.tiles.clear(); S.s.rule_status.clear(); S.s.recs.clear(); S.s.evaluated = true;
+      return;
+    }
+    session_upload(&S.s);
+    session_run(&S.s, true);
+  });
+  std::vector<ShardView> views;
+  for (auto& x : sh) views.push_back(ShardView{&x->s, 0, x->s.docs.ndocs()});
+  std::string out;
+  char* cs = nullptr;
+  int32_t code = 0;
+  ReportError re;
+  if (!shards_report(views, out, code, re, output_format, &cs)) return fail_with(re.kind, re.msg);
+  if (exit_code) *exit_code = code;
+  return cs ? cs : dup_str(out);
+}
+}  // namespace
+
+char* cfn_guard_validate_batch_devices(const validate_input_t* docs, size_t n_docs, const validate_input_t* rules,
+                                       size_t n_rules, const validate_input_t* params, size_t n_params,
+                                       int32_t output_format, const int32_t* devices, size_t n_devices, int32_t* exit_code,
+                                       extern_err_t* err) {
+  set_err(err, 0, "");
+  if (exit_code) *exit_code = 0;
+  if (output_format < OUT_JSON || output_format > OUT_JUNIT) {
+    set_err(err, 18, "IllegalArguments: unknown output format");
+    if (exit_code) *exit_code = -1;
+    return nullptr;
+  }
+  try {
+    std::vector<int> devs;
+    std::string why;
+    if (devices) {
+      for (size_t i = 0; i < n_devices; i++) devs.push_back(devices[i]);
+    } else {
+      int n = 0;
+      if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+      for (int d = 0; d < n; d++) devs.push_back(d);
+    }
+    if (devs.empty()) { set_err(err, -1, devices ? "IllegalArguments: an empty device list" : "no HIP device available (the MI355X path has no CPU fallback)"); if (exit_code) *exit_code = -1; return nullptr; }
+    for (int d : devs)
+      if (!ensure_device(why, d)) { set_err(err, -1, why); if (exit_code) *exit_code = -1; return nullptr; }
+    return validate_batch_devices(docs, n_docs, rules, n_rules, params, n_params, output_format, devs, exit_code, err);
+  } catch (std::exception& e) {
+    set_err(err, -1, e.what());
+    if (exit_code) *exit_code = -1;
+    return nullptr;
+  }
+}
+
+char* cfn_guard_validate_batch_gpus(const validate_input_t* docs, size_t n_docs, const validate_input_t* rules,
+                                    size_t n_rules, int32_t output_format, int32_t n_gpus, int32_t* exit_code,
+                                    extern_err_t* err) {
+  if (n_gpus <= 0)
+    return cfn_guard_validate_batch_devices(docs, n_docs, rules, n_rules, nullptr, 0, output_format, nullptr, 0, exit_code, err);
+  std::vector<int32_t> devs(n_gpus);
+  for (int32_t d = 0; d < n_gpus; d++) devs[d] = d;
+  return cfn_guard_validate_batch_devices(docs, n_docs, rules, n_rules, nullptr, 0, output_format, devs.data(), devs.size(),
+                                          exit_code, err);
+}
+
+/* host-only (tests): shard_by_bytes -- starts[0..nshards] of contiguous byte-balanced document ranges */
+int32_t gg_shard_by_bytes(const size_t* lens, size_t n, size_t nshards, size_t* starts) {
+  if (!nshards || !starts) return -1;
+  shard_by_bytes(lens, n, nshards, starts);
+  return 0;
+}
+
+/* the structured report of a fetched session rendered as the shards [cuts[k], cuts[k+1]) and joined by
+ * shards_report -- the multi-device join on one session's results (CPU tests, with loaded results) */
+char* gg_session_report_shards(gg_session* s, int32_t output_format, const size_t* cuts, size_t ncuts, int32_t* exit_code,
+                               extern_err_t* err) {
+  set_err(err, 0, "");
+  if (!s->evaluated) { set_err(err, -1, "session not evaluated"); return nullptr; }
+  try {
+    std::vector<ShardView> v;
+    size_t prev = 0;
+    for (size_t k = 0; k <= ncuts; k++) {
+      const size_t c = k < ncuts ? std::min(cuts[k], s->docs.ndocs()) : s->docs.ndocs();
+      if (c < prev) { set_err(err, 18, "IllegalArguments: cuts must not decrease"); return nullptr; }
+      v.push_back(ShardView{s, prev, c - prev});
+      prev = c;
+    }
+    std::string out;
+    char* cs = nullptr;
+    int32_t code = 0;
+    ReportError re;
+    if (!shards_report(v, out, code, re, output_format, &cs)) {
+      set_err(err, ffi_code(re.kind), error_display(re.kind, re.msg));
+      if (exit_code) *exit_code = -1;
+      return nullptr;
+    }
+    if (exit_code) *exit_code = code;
+    return cs ? cs : dup_str(out);
+  } catch (std::exception& e) { set_err(err, -1, e.what()); return nullptr; }
 }
 
 // ---------------------------------------------------------------- validate (console) ---
@@ -1396,6 +1653,12 @@ void gg_session_free(gg_session* s) { delete s; }
 
 void gg_session_set_stream(gg_session* s, void* stream) { s->stream = (hipStream_t)stream; }
 
+int32_t gg_session_set_device(gg_session* s, int32_t device) {
+  if (s->dv || s->dev_nodes || device < -1) return -1;   // before anything is on a device
+  s->device = device;
+  return 0;
+}
+
 int32_t gg_session_configure(gg_session* s, int32_t mode, uint32_t lane_heap_bytes) {
   if (mode != 0 && mode != 1) return -1;
   if (lane_heap_bytes && lane_heap_bytes < 32 * 1024) return -1;   // frames + record staging + tables
@@ -1405,11 +1668,18 @@ int32_t gg_session_configure(gg_session* s, int32_t mode, uint32_t lane_heap_byt
   return 0;
 }
 
+int32_t gg_session_set_option(gg_session* s, int32_t option, int64_t value) {
+  switch (option) {
+    case GG_OPT_RX_MEMO_PER_LAUNCH: s->rx_memo_per_launch = value != 0; return 0;
+    default: return -1;
+  }
+}
+
 int32_t gg_session_launch(gg_session* s, extern_err_t* err) {
   set_err(err, 0, "");
   try {
     std::string why;
-    if (!ensure_device(why)) { set_err(err, -1, why); return -1; }
+    if (!ensure_device(why, s->device, &s->device)) { set_err(err, -1, why); return -1; }
     if (!s->uploaded) session_upload(s);
     // launch / fetch callers (multi-GPU: launch, all-reduce the tallies, fetch) get no second launch,
     // so the large-heap pass must exist from the first one: a tile that outgrows the wave heap is then
@@ -1423,7 +1693,7 @@ int32_t gg_session_launch(gg_session* s, extern_err_t* err) {
 double gg_session_wait(gg_session* s, extern_err_t* err) {
   set_err(err, 0, "");
   std::string why;
-  if (!ensure_device(why)) { set_err(err, -1, why); return -1; }
+  if (!ensure_device(why, s->device, &s->device)) { set_err(err, -1, why); return -1; }
   try { return session_wait(s); } catch (std::exception& e) { set_err(err, -1, e.what()); return -1; }
 }
 
@@ -1431,7 +1701,7 @@ int32_t gg_session_fetch(gg_session* s, extern_err_t* err) {
   set_err(err, 0, "");
   try {
     std::string why;
-    if (!ensure_device(why)) { set_err(err, -1, why); return -1; }
+    if (!ensure_device(why, s->device, &s->device)) { set_err(err, -1, why); return -1; }
     session_wait(s);
     if (session_records_wanted(s) > s->rec_cap) { set_err(err, -1, "record arena overflow: run gg_session_eval first"); return -1; }
     session_fetch(s);
@@ -1738,7 +2008,7 @@ static void load_stats(const GpuLoadStats& st, double* out) {
   if (!out) return;
   out[0] = st.kernel_ms; out[1] = (double)st.nodes; out[2] = (double)st.distinct_strings;
   out[3] = (double)st.pool_bytes; out[4] = (double)st.text_bytes; out[5] = st.h2d_ms; out[6] = st.d2h_ms;
-  out[7] = (double)st.table_retries; out[8] = (double)st.refused_docs;
+  out[7] = (double)st.table_retries; out[8] = (double)st.refused_docs; out[9] = 0;
 }
 
 int32_t gg_session_add_docs_device(gg_session* s, const char* const* texts, const size_t* lens, const char* const* names,
@@ -1746,7 +2016,7 @@ int32_t gg_session_add_docs_device(gg_session* s, const char* const* texts, cons
   set_err(err, 0, "");
   try {
     std::string why;
-    if (!ensure_device(why)) { set_err(err, -1, why); return -1; }
+    if (!ensure_device(why, s->device, &s->device)) { set_err(err, -1, why); return -1; }
     if (s->docs.ndocs()) { set_err(err, 18, "IllegalArguments: the device loader fills an empty session"); return -1; }
     if (s->params) { set_note(err, "input parameters are merged by the host loader (gg_session_add_docs)"); return 1; }
     std::vector<std::string> nm(n);
@@ -1796,6 +2066,7 @@ int32_t gg_session_add_synthetic_device(gg_session* s, uint64_t first, size_t n,
   set_err(err, 0, "");
   try {
     if (nthreads < 1) nthreads = 1;
+    const auto g0 = std::chrono::steady_clock::now();
     std::vector<std::string> texts(n), names(n);
     auto work = [&](int t) {
       for (size_t i = n * t / nthreads; i < n * (t + 1) / nthreads; i++) {
@@ -1807,7 +2078,10 @@ int32_t gg_session_add_synthetic_device(gg_session* s, uint64_t first, size_t n,
     std::vector<const char*> p(n), nm(n);
     std::vector<size_t> l(n);
     for (size_t i = 0; i < n; i++) { p[i] = texts[i].data(); l[i] = texts[i].size(); nm[i] = names[i].c_str(); }
-    return gg_session_add_docs_device(s, p.data(), l.data(), nm.data(), n, stats, err);
+    const double gen_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - g0).count();
+    const int32_t rc = gg_session_add_docs_device(s, p.data(), l.data(), nm.data(), n, stats, err);
+    if (stats) stats[9] = gen_ms;
+    return rc;
   } catch (std::exception& e) { set_err(err, -1, e.what()); return -1; }
 }
 
@@ -1856,7 +2130,7 @@ int32_t gg_session_upload(gg_session* s, extern_err_t* err) {
   set_err(err, 0, "");
   try {
     std::string why;
-    if (!ensure_device(why)) { set_err(err, -1, why); return -1; }
+    if (!ensure_device(why, s->device, &s->device)) { set_err(err, -1, why); return -1; }
     session_upload(s);
     return 0;
   } catch (std::exception& e) { set_err(err, -1, e.what()); return -1; }
@@ -1867,7 +2141,7 @@ int32_t gg_session_eval(gg_session* s, int32_t iters, double* ms_out, extern_err
   set_err(err, 0, "");
   try {
     std::string why;
-    if (!ensure_device(why)) { set_err(err, -1, why); return -1; }
+    if (!ensure_device(why, s->device, &s->device)) { set_err(err, -1, why); return -1; }
     if (!s->uploaded) session_upload(s);
     for (int32_t i = 0; i < iters; i++) {
       double ms = session_run(s, i == iters - 1);
@@ -1900,7 +2174,13 @@ char* gg_session_report_format(gg_session* s, int32_t output_format, int32_t* ex
 
 char* gg_session_report_range(gg_session* s, int32_t output_format, size_t first, size_t count, int32_t* exit_code,
                               extern_err_t* err) {
+  return gg_session_report_range_n(s, output_format, first, count, nullptr, exit_code, err);
+}
+
+char* gg_session_report_range_n(gg_session* s, int32_t output_format, size_t first, size_t count, size_t* len,
+                                int32_t* exit_code, extern_err_t* err) {
   set_err(err, 0, "");
+  if (len) *len = 0;
   if (!s->evaluated) { set_err(err, -1, "session not evaluated"); return nullptr; }
   if (output_format < OUT_JSON || output_format > OUT_JUNIT) { set_err(err, 18, "IllegalArguments: unknown output format"); return nullptr; }
   try {
@@ -1914,6 +2194,7 @@ char* gg_session_report_range(gg_session* s, int32_t output_format, size_t first
       return nullptr;
     }
     if (exit_code) *exit_code = code;
+    if (len) *len = cs ? strlen(cs) : out.size();
     return cs ? cs : dup_str(out);
   } catch (std::exception& e) { set_err(err, -1, e.what()); return nullptr; }
 }
@@ -1980,7 +2261,7 @@ int64_t gg_session_stat(gg_session* s, int32_t what) {
     case 15: return (int64_t)s->heap_bytes;
     case 16: {   // tiles the lane kernel handed to wave mode in the last launch
       uint32_t v = 0;
-      if (s->dv && s->dv->d_counters.p) HIPCHK(hipMemcpy(&v, s->dv->d_counters.p + 3, 4, hipMemcpyDeviceToHost));
+      if (s->dv && s->dv->d_counters.p) { bind_device(s); HIPCHK(hipMemcpy(&v, s->dv->d_counters.p + 3, 4, hipMemcpyDeviceToHost)); }
       return v;
     }
     case 17: return (int64_t)s->lane_slots;
@@ -1990,6 +2271,8 @@ int64_t gg_session_stat(gg_session* s, int32_t what) {
       for (auto& p : s->progs) m = std::max(m, p->prog.blob.size() * 4 - (size_t)p->prog.hdr.n_dfa * 2);
       return (int64_t)m;
     }
+    case 20: return (int64_t)s->mode;   // 0 lane mode (+ wave retry), 1 wave mode
+    case 21: return (int64_t)s->parse_errors.size();   // rules files that did not parse (exit code 5)
     default: return -1;
   }
 }
@@ -2007,6 +2290,7 @@ double gg_session_last_kernel_ms(gg_session* s) { return s->last_kernel_ms; }
 // map entries scanned by key lookups, fast-filter tests, tiles
 int32_t gg_session_kernel_stats(gg_session* s, uint64_t* out, size_t n) {
   if (!s->dv || !s->dv->d_stats.p) return -1;
+  bind_device(s);
   std::vector<unsigned long long> v(32);
   HIPCHK(hipMemcpy(v.data(), s->dv->d_stats.p, 32 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   for (size_t i = 0; i < n && i < 32; i++) out[i] = v[i];

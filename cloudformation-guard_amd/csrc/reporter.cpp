@@ -1473,9 +1473,10 @@ void ReportWriter::absorb(ReportWriter& later) {
   L.ndocs = 0;
 }
 
-bool report_batch(const DocBatch& docs, const std::vector<const Program*>& progs, size_t first, size_t ndocs,
-                  const std::function<TileResult(size_t doc, size_t file)>& tile, int32_t fmt, unsigned nthreads,
-                  std::string& out, ReportError& err) {
+bool report_batch_writers(const DocBatch& docs, const std::vector<const Program*>& progs, size_t first, size_t ndocs,
+                          const std::function<TileResult(size_t doc, size_t file)>& tile, int32_t fmt, unsigned nthreads,
+                          std::vector<std::unique_ptr<ReportWriter>>& writers, std::vector<std::string>& yaml_parts,
+                          ReportError& err) {
   const size_t nf = progs.size();
   const size_t T = std::max<size_t>(1, std::min<size_t>(nthreads, (ndocs + 255) / 256));
   std::vector<std::unique_ptr<ReportWriter>> w(T);
@@ -1497,14 +1498,37 @@ bool report_batch(const DocBatch& docs, const std::vector<const Program*>& progs
   // the first document (in order) whose report aborts decides the error (structured.rs:99-133)
   for (size_t t = 0; t < T; t++) if (err_doc[t] != SIZE_MAX) { err = errs[t]; return false; }
   if (fmt == OUT_YAML) {
-    if (!ndocs) { out = ReportWriter(fmt).finish(); return true; }
-    // a block sequence's items are emitted independently: the chunks' streams concatenate
-    out.clear();
-    for (auto& y : yaml_out) out += y;
+    // a block sequence's items are emitted independently: the ranges' streams concatenate
+    for (size_t t = 0; t < T; t++) if (first + ndocs * (t + 1) / T > first + ndocs * t / T) yaml_parts.push_back(std::move(yaml_out[t]));
     return true;
   }
-  for (size_t t = 1; t < T; t++) w[0]->absorb(*w[t]);
-  out = w[0]->finish();
+  for (auto& x : w) writers.push_back(std::move(x));
+  return true;
+}
+
+std::string report_writers_finish(int32_t fmt, std::vector<std::unique_ptr<ReportWriter>>& writers,
+                                  std::vector<std::string>& yaml_parts) {
+  if (fmt == OUT_YAML) {
+    if (yaml_parts.empty()) return ReportWriter(fmt).finish();
+    std::string out;
+    size_t n = 0;
+    for (auto& y : yaml_parts) n += y.size();
+    out.reserve(n);
+    for (auto& y : yaml_parts) out += y;
+    return out;
+  }
+  if (writers.empty()) return ReportWriter(fmt).finish();
+  for (size_t t = 1; t < writers.size(); t++) writers[0]->absorb(*writers[t]);
+  return writers[0]->finish();
+}
+
+bool report_batch(const DocBatch& docs, const std::vector<const Program*>& progs, size_t first, size_t ndocs,
+                  const std::function<TileResult(size_t doc, size_t file)>& tile, int32_t fmt, unsigned nthreads,
+                  std::string& out, ReportError& err) {
+  std::vector<std::unique_ptr<ReportWriter>> w;
+  std::vector<std::string> yaml_parts;
+  if (!report_batch_writers(docs, progs, first, ndocs, tile, fmt, nthreads, w, yaml_parts, err)) return false;
+  out = report_writers_finish(fmt, w, yaml_parts);
   return true;
 }
 

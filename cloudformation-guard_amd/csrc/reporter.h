@@ -8,6 +8,7 @@
 #include <cstring>
 #include <exception>
 #include <functional>
+#include <memory>
 #include <new>
 #include <string>
 #include <thread>
@@ -156,6 +157,17 @@ class ReportWriter {
 bool report_batch(const DocBatch& docs, const std::vector<const Program*>& progs, size_t first, size_t ndocs,
                   const std::function<TileResult(size_t doc, size_t file)>& tile, int32_t fmt, unsigned nthreads,
                   std::string& out, ReportError& err);
+
+// report_batch in two halves, so several shards' reports join into one: the unfinished writers of
+// documents [first, first + ndocs) in order (JSON / SARIF / JUnit), or for YAML each range's finished
+// stream (a block sequence's items concatenate).  report_writers_finish absorbs the writers in order
+// (or joins the YAML streams) -- the bytes one writer fed every document in order writes.
+bool report_batch_writers(const DocBatch& docs, const std::vector<const Program*>& progs, size_t first, size_t ndocs,
+                          const std::function<TileResult(size_t doc, size_t file)>& tile, int32_t fmt, unsigned nthreads,
+                          std::vector<std::unique_ptr<ReportWriter>>& writers, std::vector<std::string>& yaml_parts,
+                          ReportError& err);
+std::string report_writers_finish(int32_t fmt, std::vector<std::unique_ptr<ReportWriter>>& writers,
+                                  std::vector<std::string>& yaml_parts);
 
 // Growable text buffer for the streamed JSON writer: malloc / realloc storage (large blocks grow by
 // mremap, without a copy) and std::string's append interface, so fragment appends are an inline bounds

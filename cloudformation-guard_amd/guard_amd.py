@@ -60,6 +60,21 @@ def lib():
                                                   ctypes.POINTER(ValidateInput), ctypes.c_size_t, ctypes.c_int32,
                                                   ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ExternError)]
     L.cfn_guard_validate_batch_params.restype = ctypes.c_void_p
+    L.cfn_guard_validate_batch_devices.argtypes = [ctypes.POINTER(ValidateInput), ctypes.c_size_t,
+                                                   ctypes.POINTER(ValidateInput), ctypes.c_size_t,
+                                                   ctypes.POINTER(ValidateInput), ctypes.c_size_t, ctypes.c_int32,
+                                                   ctypes.POINTER(ctypes.c_int32), ctypes.c_size_t,
+                                                   ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ExternError)]
+    L.cfn_guard_validate_batch_devices.restype = ctypes.c_void_p
+    L.gg_shard_by_bytes.argtypes = [ctypes.POINTER(ctypes.c_size_t), ctypes.c_size_t, ctypes.c_size_t,
+                                    ctypes.POINTER(ctypes.c_size_t)]
+    L.gg_shard_by_bytes.restype = ctypes.c_int32
+    L.gg_session_report_shards.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_size_t),
+                                           ctypes.c_size_t, ctypes.POINTER(ctypes.c_int32),
+                                           ctypes.POINTER(ExternError)]
+    L.gg_session_report_shards.restype = ctypes.c_void_p
+    L.gg_session_set_device.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+    L.gg_session_set_device.restype = ctypes.c_int32
     L.cfn_guard_validate_console.argtypes = [ctypes.POINTER(ValidateInput), ctypes.c_size_t,
                                              ctypes.POINTER(ValidateInput), ctypes.c_size_t,
                                              ctypes.POINTER(ValidateInput), ctypes.c_size_t, ctypes.c_uint32,
@@ -72,6 +87,10 @@ def lib():
     L.gg_session_report_range.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_size_t, ctypes.c_size_t,
                                           ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ExternError)]
     L.gg_session_report_range.restype = ctypes.c_void_p
+    L.gg_session_report_range_n.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_size_t, ctypes.c_size_t,
+                                            ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_int32),
+                                            ctypes.POINTER(ExternError)]
+    L.gg_session_report_range_n.restype = ctypes.c_void_p
     L.cfn_guard_test_dir.argtypes = [ctypes.POINTER(ValidateInput), ctypes.c_size_t, ctypes.POINTER(ValidateInput),
                                      ctypes.POINTER(ctypes.c_size_t), ctypes.c_int32, ctypes.c_bool,
                                      ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ExternError)]
@@ -113,6 +132,8 @@ def lib():
     L.gg_session_counts_device.restype = ctypes.c_void_p
     L.gg_session_counts.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
     L.gg_session_configure.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint32]
+    L.gg_session_set_option.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64]
+    L.gg_session_set_option.restype = ctypes.c_int32
     L.gg_session_bind_counts.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
     L.gg_session_bind_counts.restype = None
     L.gg_session_drain_kernel_ms.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ExternError)]
@@ -191,7 +212,10 @@ def parse_rules(text, name="r.guard"):
 
 
 LOAD_STATS = ("kernel_ms", "nodes", "distinct_strings", "pool_bytes", "text_bytes", "h2d_ms", "d2h_ms", "table_retries",
-              "refused_docs")
+              "refused_docs", "gen_ms")
+
+
+SESSION_OPTIONS = {"rx_memo_per_launch": 1}
 
 
 def _load_result(rc, err, st):
@@ -225,6 +249,19 @@ def _take_string(p):
     s = ctypes.string_at(p).decode("utf-8")
     lib().cfn_guard_free_string(p)
     return s
+
+
+def _owned_bytes(p, n):
+    """a uint8 numpy array over n bytes the library malloc'd at p (no copy); freed with the array"""
+    import numpy as np
+    import weakref
+    if not p or n == 0:
+        if p:
+            lib().cfn_guard_free_string(p)
+        return np.zeros(0, dtype=np.uint8)
+    buf = (ctypes.c_uint8 * n).from_address(p)
+    weakref.finalize(buf, lib().cfn_guard_free_string, p)
+    return np.frombuffer(buf, dtype=np.uint8)
 
 
 def _raise(err):
@@ -266,6 +303,36 @@ def validate_structured(rules, data, output="json", params=None):
     if err.code != 0:
         _raise(err)
     return _take_string(p), code.value
+
+
+def validate_structured_devices(rules, data, devices=None, output="json", params=None):
+    """validate_structured with the documents sharded over HIP devices in this process
+    (cfn_guard_validate_batch_devices): contiguous byte-balanced ranges, one per entry of `devices`
+    (ordinals may repeat; None: every visible device), reports joined in document order -- the same
+    (text, exit_code) as validate_structured."""
+    R = (ValidateInput * max(1, len(rules)))(*[ValidateInput(_b(t), _b(n)) for n, t in rules])
+    D = (ValidateInput * max(1, len(data)))(*[ValidateInput(_b(t), _b(n)) for n, t in data])
+    params = params or []
+    P = (ValidateInput * max(1, len(params)))(*[ValidateInput(_b(t), _b(n)) for n, t in params])
+    devs = None if devices is None else (ctypes.c_int32 * max(1, len(devices)))(*devices)
+    code = ctypes.c_int32(0)
+    err = ExternError()
+    p = lib().cfn_guard_validate_batch_devices(D, len(data), R, len(rules), P, len(params), OUTPUT_FORMATS[output],
+                                               devs, 0 if devices is None else len(devices), ctypes.byref(code),
+                                               ctypes.byref(err))
+    if err.code != 0:
+        _raise(err)
+    return _take_string(p), code.value
+
+
+def shard_by_bytes(sizes, nshards):
+    """the library's byte-balanced split (gg_shard_by_bytes): [(first, count)] per shard"""
+    n = len(sizes)
+    L = (ctypes.c_size_t * max(1, n))(*sizes)
+    S = (ctypes.c_size_t * (nshards + 1))()
+    if lib().gg_shard_by_bytes(L, n, nshards, S) != 0:
+        raise ValueError("nshards must be positive")
+    return [(S[k], S[k + 1] - S[k]) for k in range(nshards)]
 
 
 CONSOLE_OUTPUT_FORMATS = {"single-line-summary": 4, "json": 0, "yaml": 1}
@@ -437,6 +504,36 @@ class Session:
             _raise(err)
         return _take_string(p), code.value
 
+    def report_range_raw(self, output="json", first=0, count=None):
+        """report_range as a uint8 numpy array over the library's buffer: no copy, no decode (bulk
+        consumers: the streamed multi-rank gather); the buffer is freed with the array"""
+        code = ctypes.c_int32(0)
+        ln = ctypes.c_size_t(0)
+        err = ExternError()
+        n = ctypes.c_size_t(-1).value if count is None else count
+        p = lib().gg_session_report_range_n(self.s, OUTPUT_FORMATS[output], first, n, ctypes.byref(ln), ctypes.byref(code),
+                                            ctypes.byref(err))
+        if err.code != 0:
+            _raise(err)
+        return _owned_bytes(p, ln.value), code.value
+
+    def report_shards(self, output="json", cuts=()):
+        """the report rendered as the shards [0, cuts[0]), [cuts[0], cuts[1]), ... and joined as the
+        multi-device entry joins its devices' shards"""
+        code = ctypes.c_int32(0)
+        err = ExternError()
+        C = (ctypes.c_size_t * max(1, len(cuts)))(*cuts)
+        p = lib().gg_session_report_shards(self.s, OUTPUT_FORMATS[output], C, len(cuts), ctypes.byref(code),
+                                           ctypes.byref(err))
+        if err.code != 0:
+            _raise(err)
+        return _take_string(p), code.value
+
+    def set_device(self, device):
+        """the session's HIP device (before documents are loaded on / uploaded to a device)"""
+        if lib().gg_session_set_device(self.s, device) != 0:
+            raise ValueError("set_device after the session holds device state")
+
     def report_bytes(self, output="json", max_docs=0):
         """renders the report of the first max_docs documents (0: all) in blocks and discards it;
         returns (bytes, exit code)"""
@@ -481,6 +578,11 @@ class Session:
         """mode 0: one tile per lane (+ wave-mode retry of overflowing tiles); 1: one tile per wave."""
         if lib().gg_session_configure(self.s, mode, lane_heap_bytes) != 0:
             raise ValueError("bad session configuration")
+
+    def set_option(self, option, value):
+        """gg_session_set_option; option "rx_memo_per_launch": zero the regex memo before every launch"""
+        if lib().gg_session_set_option(self.s, SESSION_OPTIONS[option], int(value)) != 0:
+            raise ValueError("unknown session option %r" % (option,))
 
     def set_stream(self, stream_handle):
         lib().gg_session_set_stream(self.s, ctypes.c_void_p(stream_handle))
@@ -531,7 +633,19 @@ class Session:
 
     STAT = {"ndocs": 0, "nfiles": 1, "nodes": 2, "bytes": 3, "fail": 4, "pass": 5, "skip": 6, "errors": 7,
             "records": 8, "arena_bytes": 9, "first_error": 10, "record_bytes": 11, "record_cap": 12,
-            "max_top": 13, "slots": 14, "heap_bytes": 15, "retried": 16, "lane_slots": 17}
+            "max_top": 13, "slots": 14, "heap_bytes": 15, "retried": 16, "lane_slots": 17, "mode": 20,
+            "parse_errors": 21}
+
+    def exit_code(self, output="json"):
+        """the structured run's exit code over the evaluated documents, as the report would set it:
+        -1 an evaluation error, 19 a FAIL (JUnit keeps 5 when a rules file did not parse), 5 an unparsable
+        rules file, else 0 (structured.rs:40-43, 110-112; reporters/mod.rs:97-103)"""
+        if self.stat(self.STAT["errors"]) > 0:
+            return -1
+        parse = self.stat(self.STAT["parse_errors"]) > 0
+        if self.stat(self.STAT["fail"]) > 0 and not (output == "junit" and parse):
+            return 19
+        return 5 if parse else 0
 
 
 def synth_cfn_doc(index, n_resources=50):

@@ -204,6 +204,17 @@ def tf_corpus(n, start=0, n_resources=200):
     return [json.dumps(tf_plan_doc(start + i, n_resources), separators=(",", ":")) for i in range(n)]
 
 
+def tf_bench_size(i):
+    """resources of bench plan i: 200-2000, seeded (xorshift32 seed 9191 ^ i), SURVEY.md 8(d) cfg 4"""
+    return 200 + XorShift32(9191 ^ i).next() % 1801
+
+
+def tf_bench_corpus(n, start=0):
+    """the cfg-4 bench corpus: plan i = tf_plan_doc(i, tf_bench_size(i)) (200-2000 resource_changes,
+    module nesting putting the deepest values 6-10 levels below the root)"""
+    return [json.dumps(tf_plan_doc(start + i, tf_bench_size(start + i)), separators=(",", ":")) for i in range(n)]
+
+
 # ---------------------------------------------------------------------------------------------
 # cfg 5 (BASELINE.json configs[4]; SURVEY.md 8d): AWS Config configuration items of one account
 # snapshot, wrapped into a CloudFormation-shaped `Resources` map keyed by resource id (the

@@ -66,6 +66,22 @@ char *cfn_guard_validate_batch_params(const validate_input_t *docs, size_t n_doc
                                       size_t n_rules, const validate_input_t *params, size_t n_params,
                                       int32_t output_format, int32_t *exit_code, extern_err_t *err);
 
+/* cfn_guard_validate_batch_params over several GPUs of this process (SURVEY.md 8(b) "n_gpus", 8(e)): the
+ * documents are split into contiguous ranges balanced by text bytes, one per entry of `devices` (HIP
+ * ordinals; an ordinal may repeat -- two shards on one GPU), each range loaded, evaluated and fetched on its
+ * own host thread and device, and the shards' reports joined in document order on the host: the same bytes
+ * and exit code as the one-device call, with its error precedence.  devices NULL: every visible device
+ * (n_devices ignored).  Replaces, for a caller that owns the node's GPUs in one process, the per-file loop
+ * of CommonStructuredReporter::report (reporters/validate/structured.rs:99-133). */
+char *cfn_guard_validate_batch_devices(const validate_input_t *docs, size_t n_docs, const validate_input_t *rules,
+                                       size_t n_rules, const validate_input_t *params, size_t n_params,
+                                       int32_t output_format, const int32_t *devices, size_t n_devices,
+                                       int32_t *exit_code, extern_err_t *err);
+/* the n_gpus form of SURVEY.md 8(b): devices 0 .. n_gpus - 1 (n_gpus <= 0: every visible device), no -i. */
+char *cfn_guard_validate_batch_gpus(const validate_input_t *docs, size_t n_docs, const validate_input_t *rules,
+                                    size_t n_rules, int32_t output_format, int32_t n_gpus, int32_t *exit_code,
+                                    extern_err_t *err);
+
 /* `cfn-guard validate [-r <rules>]+ [-d <data>]+ [-i <params>]* [-o single-line-summary|json|yaml]
  * [-S <summary>] [--verbose] [--print-json]` -- the console reporters, not --structured
  * (commands/validate.rs:253-487, 552-596, 690-758; reporters/validate/{summary_table,cfn,tf,
@@ -125,10 +141,23 @@ int32_t gg_session_upload(gg_session *s, extern_err_t *err);
 int32_t gg_session_eval(gg_session *s, int32_t iters, double *ms_out, extern_err_t *err);
 char *gg_session_report(gg_session *s, int32_t *exit_code, extern_err_t *err);
 char *gg_session_report_format(gg_session *s, int32_t output_format, int32_t *exit_code, extern_err_t *err);
+/* the session's HIP device (-1: the process default); before its documents or buffers are on a device */
+int32_t gg_session_set_device(gg_session *s, int32_t device);
 /* the structured report of documents [first, first + count) alone (count SIZE_MAX: to the end): what a
  * run over just those documents writes -- one rank's shard of a multi-GPU job */
 char *gg_session_report_range(gg_session *s, int32_t output_format, size_t first, size_t count, int32_t *exit_code,
                               extern_err_t *err);
+/* gg_session_report_range with the report's length in bytes in *len (bulk consumers skip a strlen) */
+char *gg_session_report_range_n(gg_session *s, int32_t output_format, size_t first, size_t count, size_t *len,
+                                int32_t *exit_code, extern_err_t *err);
+/* the report rendered as the shards [0, cuts[0]), [cuts[0], cuts[1]), ... [cuts[ncuts-1], ndocs) and joined
+ * as cfn_guard_validate_batch_devices joins its devices' shards (the multi-device join, testable on loaded
+ * results without a GPU) */
+char *gg_session_report_shards(gg_session *s, int32_t output_format, const size_t *cuts, size_t ncuts, int32_t *exit_code,
+                               extern_err_t *err);
+/* host-only: the byte-balanced split of cfn_guard_validate_batch_devices -- starts[0..nshards] (starts[k] =
+ * first document of shard k, starts[nshards] = n); 0, or -1 for nshards == 0 */
+int32_t gg_shard_by_bytes(const size_t *lens, size_t n, size_t nshards, size_t *starts);
 int64_t gg_session_stat(gg_session *s, int32_t what);
 /* Diagnostic: save an evaluation's results (tiles, rule statuses, records) / load them into a session
  * holding the same rules files and documents (no GPU needed to render its reports). */
@@ -144,6 +173,11 @@ void gg_session_set_stream(gg_session *s, void *hip_stream);
 /* mode 0 (default): one tile per lane, tiles that outgrow the lane heap re-run one tile per
  * wavefront; mode 1: one tile per wavefront for every tile.  lane_heap_bytes 0 keeps 64 KB. */
 int32_t gg_session_configure(gg_session *s, int32_t mode, uint32_t lane_heap_bytes);
+/* session options (0 = set, -1 = unknown option).  GG_OPT_RX_MEMO_PER_LAUNCH: 1 zeroes the regex
+ * is_match memo (2 bits per (pool string, regex), filled by the first evaluation that runs the DFA) before
+ * every launch, so each launch pays its own first DFA runs; 0 (default) zeroes it once per upload. */
+#define GG_OPT_RX_MEMO_PER_LAUNCH 1
+int32_t gg_session_set_option(gg_session *s, int32_t option, int64_t value);
 int32_t gg_session_launch(gg_session *s, extern_err_t *err);  /* enqueue; no host sync */
 double gg_session_wait(gg_session *s, extern_err_t *err);     /* kernel ms of the last launch */
 int32_t gg_session_fetch(gg_session *s, extern_err_t *err);   /* statuses + records to host */
@@ -197,9 +231,9 @@ int32_t gg_session_add_synthetic(gg_session *s, uint64_t first, size_t n, int32_
  * beyond the exact fast path, a raw character libyaml reads specially) is built by the host loader
  * and spliced in at its position.  Returns 0 when loaded, 1 when the batch is refused as a whole
  * (a batch-wide limit, or a refused document the host loader rejects too: nothing loaded, err->message
- * says why; gg_session_add_docs reports the loader error), -1 on error.  stats (may be NULL, 9 doubles):
+ * says why; gg_session_add_docs reports the loader error), -1 on error.  stats (may be NULL, 10 doubles):
  * kernel ms, nodes, distinct strings, pool bytes, text bytes, H2D ms, D2H ms, intern-table doublings,
- * documents built by the host loader.  The loaded nodes stay in HBM for the session's first upload
+ * documents built by the host loader, host text-generation ms (gg_session_add_synthetic_device; else 0).  The loaded nodes stay in HBM for the session's first upload
  * (it packs the device arena from them; only host-built documents cross PCIe again). */
 int32_t gg_session_add_docs_device(gg_session *s, const char *const *texts, const size_t *lens, const char *const *names,
                                    size_t n, double *stats, extern_err_t *err);

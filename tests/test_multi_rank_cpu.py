@@ -150,3 +150,79 @@ def test_byte_balanced_shard_ranges():
     assert max(loads) <= 100 and min(c for _, c in r) >= 1
     assert sharding.shard_ranges_by_bytes([1] * 8, 4) == [(0, 2), (2, 2), (4, 2), (6, 2)]
     assert sharding.shard_ranges_by_bytes([5], 2) == [(0, 0), (0, 1)]   # fewer documents than ranks
+
+
+# ---- streamed gather in bounded blocks (sharding.stream_report) ----
+STREAM_DOCS = 4
+
+
+def _stream_worker(rank, world, port, q, fail_at):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import io
+    out = {}
+    for fmt in ("json", "yaml", "sarif", "junit"):
+        first, n = sharding.shard_range(rank, world, STREAM_DOCS)
+        _, code = _shard_report(first, n, fmt)
+
+        def render(f, c, first=first, fmt=fmt):
+            if fail_at is not None and rank == fail_at[0] and f == fail_at[1]:
+                raise RuntimeError("report of document %d aborted" % (first + f))
+            return _shard_report(first + f, c, fmt)[0]
+        sink = io.StringIO()
+        # blocks of one document: every block is smaller than one rank's report
+        res = sharding.stream_report(render, n, code, dist, sink, output=fmt, block_docs=1, lookahead=2)
+        out[fmt] = (sink.getvalue() if rank == 0 else None, res)
+        if fmt in ("json", "yaml") and fail_at is None:
+            # the bulk path: bytes blocks in, memoryview pieces out (no decode per block)
+            bsink = io.BytesIO()
+            res = sharding.stream_report(lambda f, c: render(f, c).encode(), n, code, dist, bsink, output=fmt,
+                                         block_docs=2, raw=True)
+            out[fmt + "_raw"] = (bsink.getvalue().decode() if rank == 0 else None, res)
+    q.put((rank, out))
+    dist.destroy_process_group()
+
+
+def _run_stream(fail_at=None, world=2):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_stream_worker, args=(r, world, port, q, fail_at)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return got
+
+
+def test_streamed_report_in_one_document_blocks_matches_single_process():
+    got = _run_stream()
+    for fmt in ("json", "yaml", "sarif", "junit", "json_raw", "yaml_raw"):
+        full, code = _shard_report(0, 2 * STREAM_DOCS, fmt.split("_")[0])
+        text, res = got[0][fmt]
+        assert res == (code, None), fmt
+        assert text == full, fmt
+        assert got[1][fmt] == (None, (code, None)), fmt
+
+
+def test_streamed_report_error_ends_the_stream_on_every_rank():
+    got = _run_stream(fail_at=(1, 2))   # rank 1's third block aborts
+    for fmt in ("json", "yaml", "sarif", "junit"):
+        for r in (0, 1):
+            code, msg = got[r][fmt][1]
+            assert code == -1, (fmt, r)
+        assert got[0][fmt][1][1] == "report of document %d aborted" % (STREAM_DOCS + 2)
+
+
+def test_report_merger_sarif_and_junit_edges():
+    full, _ = _shard_report(0, 3, "sarif")
+    # three shards, the middle one with no documents: artifacts de-duplicated and in order
+    parts = [_shard_report(0, 1, "sarif")[0], _shard_report(1, 0, "sarif")[0], _shard_report(1, 2, "sarif")[0]]
+    assert sharding.merge_reports(parts, "sarif") == full
+    j = [_shard_report(0, 0, "junit")[0], _shard_report(0, 3, "junit")[0]]
+    assert sharding.merge_reports(j, "junit") == _shard_report(0, 3, "junit")[0]
+    with pytest.raises(ValueError):
+        sharding.merge_reports(["{}"], "sarif")
