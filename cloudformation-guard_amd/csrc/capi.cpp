@@ -39,6 +39,10 @@ __global__ void guard_eval_lanes_kernel(LaunchArgs A);
 __global__ void resource_type_kernel(DevBatch D);
 __global__ void shape_key_kernel(DevBatch D, const uint32_t* top8, unsigned long long* key);
 __global__ void pack_nodes_kernel(const DNode* in, DNodeP* out, uint32_t* klen, uint64_t n, uint32_t* bad);
+__global__ void rec_block_sums_kernel(const TileOut* tiles, uint32_t n, uint32_t* bsum);
+__global__ void rec_scan_sums_kernel(uint32_t* bsum, uint32_t nb, uint32_t* total);
+__global__ void rec_compact_kernel(const TileOut* tiles, uint32_t n, const uint32_t* bsum, const Rec* src, Rec* dst,
+                                   uint32_t* dense_off);
 __global__ void rule_count_kernel(const TileOut* tiles, const uint8_t* rule_status, const DevProg* progs, uint32_t nfiles,
                                   uint32_t ntiles, uint32_t max_top, unsigned long long* counts);
 }
@@ -247,6 +251,9 @@ struct DeviceBufs {
   DBuf<TileOut> d_tiles;
   DBuf<uint8_t> d_rule_status;
   DBuf<Rec> d_recs;
+  DBuf<Rec> d_recs_dense;       // session_fetch: the records compacted into tile order
+  DBuf<uint32_t> d_dense_off;   // ... and each tile's offset in it
+  DBuf<uint32_t> d_bsum;        // compaction block sums (+ total)
   DBuf<uint32_t> d_counters;
   DBuf<unsigned long long> d_counts;   // per (file, top rule) x {PASS, FAIL, SKIP, error}
   DBuf<unsigned long long> d_stats;    // diagnostic counters (stats build variant)
@@ -263,6 +270,7 @@ struct DeviceBufs {
     return d_nodes.bytes() + d_klen.bytes() + d_bytes.bytes() + d_roots.bytes() + d_base.bytes() + d_res_map.bytes() +
            d_tix_off.bytes() + d_tix.bytes() + d_progs.bytes() + d_rx_memo.bytes() + d_heaps.bytes() + d_lane_heaps.bytes() + d_retry.bytes() +
            d_big_heaps.bytes() + d_retry2.bytes() + d_tiles.bytes() + d_rule_status.bytes() + d_recs.bytes() +
+           d_recs_dense.bytes() + d_dense_off.bytes() + d_bsum.bytes() +
            d_counters.bytes() + d_counts.bytes() + d_stats.bytes();
   }
 };
@@ -333,6 +341,7 @@ struct gg_session {
   int32_t mode = 0;               // 0: lane mode + wave-mode retry; 1: wave mode only
   bool verbose = false;           // wave mode recording the EventRecord tree (guard_eval_verbose_kernel)
   size_t rec_cap = 0;
+  uint32_t rec_chunk = 0;         // lane mode: direct record slots per lane per batch (eval_core.inc rec_store)
   size_t rx_memo_words = 0;       // words of the regex is_match memo (0: none)
   bool rx_memo_per_launch = false;   // zero the memo before every launch (bench: no warm memo across steps)
   // results
@@ -571,7 +580,20 @@ void session_upload(gg_session* s) {
   s->dv->d_retry2.alloc(std::max<size_t>(ntiles, 1));
   s->dv->d_tiles.alloc(std::max<size_t>(ntiles, 1));
   s->dv->d_rule_status.alloc(std::max<size_t>(ntiles * s->max_top, 1));
-  s->rec_cap = std::min<size_t>(std::max<size_t>(ntiles * 48, 4096), (size_t)96 * 1024 * 1024);
+  // direct record chunks (lane mode): rec_chunk slots per lane per batch, reserved by every lane batch of a
+  // launch.  GG_REC_CHUNK overrides (0: every record staged in the lane heap, the round-3 path); halved
+  // until the reservations fit kMaxChunkBytes (<= 8 slots: off)
+  s->rec_chunk = 0;
+  size_t reserve = 0;
+  if (s->mode != 1) {
+    size_t ch = getenv("GG_REC_CHUNK") ? (size_t)std::max(0, atoi(getenv("GG_REC_CHUNK"))) : 32;
+    const size_t lane_batches = nbatches;
+    static constexpr size_t kMaxChunkBytes = (size_t)24 << 30;
+    while (ch >= 8 && lane_batches * 64 * ch * sizeof(Rec) > kMaxChunkBytes) ch /= 2;
+    if (ch >= 8 && lane_batches * 64 * ch < 0xC0000000ull) { s->rec_chunk = (uint32_t)ch; reserve = lane_batches * 64 * ch; }
+  }
+  s->rec_cap = reserve + std::min<size_t>(std::max<size_t>(ntiles * 48, 4096), (size_t)96 * 1024 * 1024);
+  s->rec_cap = std::min<size_t>(s->rec_cap, (size_t)0xFFFFFFF0u);
   s->dv->d_recs.alloc(s->rec_cap);
   s->dv->d_counters.alloc(32);   // [0..6] cursors / counts, [16..23] per-XCD lane-mode queues
   s->dv->d_stats.alloc(32);
@@ -607,6 +629,7 @@ void session_launch(gg_session* s) {
   A.heaps = s->dv->d_heaps.p; A.heap_bytes = s->heap_bytes; A.nslots = s->nslots;
   A.tiles = s->dv->d_tiles.p; A.rule_status = s->dv->d_rule_status.p; A.max_top = s->max_top;
   A.recs = s->dv->d_recs.p; A.rec_cap = (uint32_t)s->rec_cap;
+  A.rec_chunk = s->mode == 1 ? 0u : s->rec_chunk;
   A.rec_cursor = s->dv->d_counters.p; A.tile_cursor = s->dv->d_counters.p + 1;   // [1] lane batches, [2] wave tiles
   A.retry_count = s->dv->d_counters.p + 3;
   A.xcd_cursor = s->dv->d_counters.p + 16;
@@ -688,18 +711,36 @@ uint32_t session_records_wanted(gg_session* s) {
 void session_fetch(gg_session* s) {
   bind_device(s);
   // the tally kernel runs after ev1 on a non-blocking stream: wait for the whole launch
-  HIPCHK(hipStreamSynchronize(session_stream(s)));
+  hipStream_t st = session_stream(s);
+  HIPCHK(hipStreamSynchronize(st));
   uint32_t ntiles = (uint32_t)(s->docs.ndocs() * s->progs.size());
   s->tiles.resize(ntiles);
   s->rule_status.resize((size_t)ntiles * s->max_top);
-  uint32_t nrec = session_records_wanted(s);
-  if (nrec > s->rec_cap) nrec = (uint32_t)s->rec_cap;
-  s->recs.resize(nrec);
+  uint32_t total = 0;
   if (ntiles) {
+    // compact every tile's records (direct chunks or contiguous) into one dense array in tile order
+    const uint32_t nb = (ntiles + 1023u) / 1024u;
+    s->dv->d_bsum.alloc((size_t)nb + 1);
+    s->dv->d_dense_off.alloc(ntiles);
+    hipLaunchKernelGGL(rec_block_sums_kernel, dim3(nb), dim3(256), 0, st, s->dv->d_tiles.p, ntiles, s->dv->d_bsum.p);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(rec_scan_sums_kernel, dim3(1), dim3(1024), 0, st, s->dv->d_bsum.p, nb, s->dv->d_bsum.p + nb);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(&total, s->dv->d_bsum.p + nb, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    s->dv->d_recs_dense.alloc(std::max<size_t>(total, 1));
+    hipLaunchKernelGGL(rec_compact_kernel, dim3(nb), dim3(256), 0, st, s->dv->d_tiles.p, ntiles, s->dv->d_bsum.p,
+                       s->dv->d_recs.p, s->dv->d_recs_dense.p, s->dv->d_dense_off.p);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(st));
     HIPCHK(hipMemcpy(s->tiles.data(), s->dv->d_tiles.p, ntiles * sizeof(TileOut), hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(s->rule_status.data(), s->dv->d_rule_status.p, s->rule_status.size(), hipMemcpyDeviceToHost));
+    std::vector<uint32_t> doff(ntiles);
+    HIPCHK(hipMemcpy(doff.data(), s->dv->d_dense_off.p, ntiles * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    for (uint32_t t = 0; t < ntiles; t++) { s->tiles[t].rec_off = doff[t]; s->tiles[t].pad1 = 0; }
   }
-  if (nrec) HIPCHK(hipMemcpy(s->recs.data(), s->dv->d_recs.p, nrec * sizeof(Rec), hipMemcpyDeviceToHost));
+  s->recs.resize(total);
+  if (total) HIPCHK(hipMemcpy(s->recs.data(), s->dv->d_recs_dense.p, (size_t)total * sizeof(Rec), hipMemcpyDeviceToHost));
   s->counts.resize(s->ncounts);
   HIPCHK(hipMemcpy(s->counts.data(), s->ext_counts ? s->ext_counts : s->dv->d_counts.p, s->ncounts * sizeof(unsigned long long),
                    hipMemcpyDeviceToHost));
@@ -709,24 +750,27 @@ void session_fetch(gg_session* s) {
 // one complete evaluation; re-runs when the first pass overflowed the record arena (grown) or left
 // tiles for the large-heap pass before its heaps existed (allocated)
 double session_run(gg_session* s, bool fetch) {
-  session_launch(s);
-  double ms = session_wait(s);
-  uint32_t cnt[5] = {0, 0, 0, 0, 0};
-  HIPCHK(hipStreamSynchronize(session_stream(s)));
-  HIPCHK(hipMemcpy(cnt, s->dv->d_counters.p, sizeof(cnt), hipMemcpyDeviceToHost));
-  bool again = false;
-  if (cnt[0] > s->rec_cap) {
-    s->rec_cap = std::min<size_t>((size_t)cnt[0] + cnt[0] / 8 + 1024, (size_t)0xFFFFFFF0u);
-    s->dv->d_recs.alloc(s->rec_cap);
-    again = true;
-  }
-  if (cnt[4] && !s->dv->d_big_heaps.p) {
-    s->dv->d_big_heaps.alloc((size_t)gg_session::kBigSlots * gg_session::kBigHeap);
-    again = true;
-  }
-  if (again) {
+  double ms = 0;
+  // re-runs while a pass needed what did not exist yet: a larger record arena (the cursor counts every
+  // reservation and allocation, also of tiles that could not write) or the large-heap pass's heaps (its
+  // tiles' records are counted only once it runs, so allocating it can call for a larger arena next)
+  for (int pass = 0; pass < 4; pass++) {
     session_launch(s);
     ms = session_wait(s);
+    uint32_t cnt[5] = {0, 0, 0, 0, 0};
+    HIPCHK(hipStreamSynchronize(session_stream(s)));
+    HIPCHK(hipMemcpy(cnt, s->dv->d_counters.p, sizeof(cnt), hipMemcpyDeviceToHost));
+    bool again = false;
+    if (cnt[0] > s->rec_cap) {
+      s->rec_cap = std::min<size_t>((size_t)cnt[0] + cnt[0] / 8 + 1024, (size_t)0xFFFFFFF0u);
+      s->dv->d_recs.alloc(s->rec_cap);
+      again = true;
+    }
+    if (cnt[4] && !s->dv->d_big_heaps.p) {
+      s->dv->d_big_heaps.alloc((size_t)gg_session::kBigSlots * gg_session::kBigHeap);
+      again = true;
+    }
+    if (!again) break;
   }
   if (fetch) session_fetch(s);
   session_drain(s, nullptr, 0);

@@ -155,6 +155,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
   if (lane == 0) {
     g_wave.heap = heap; g_wave.nodes = A.docs.nodes; g_wave.klen = A.docs.klen; g_wave.db = A.docs.bytes;
     g_wave.tix = A.docs.tix; g_wave.fcap = FRAMES_BYTES; g_wave.rcap = RECS_BYTES; g_wave.type_key = A.docs.type_key;
+    g_wave.recs = A.recs; g_wave.rchunk = A.rec_chunk;
   }
   __syncthreads();
   uint32_t staged = NONE;
@@ -192,6 +193,16 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
       if (active) A.retry_list[atomicAdd(A.retry_count, 1u)] = tile;
       continue;
     }
+    // the batch's direct record chunk: 64 lanes x rec_chunk slots, one atomic per wave (eval_core.inc
+    // rec_store); a reservation past the arena leaves the lanes without a chunk (their tiles then fail
+    // with E_RECORDS if they record anything, and the host re-runs with a larger arena)
+    uint32_t rbase = NONE;
+    if (A.rec_chunk) {
+      if (lane == 0) rbase = atomicAdd(A.rec_cursor, 64u * A.rec_chunk);
+      rbase = __shfl(rbase, 0);
+      if ((uint64_t)rbase + 64ull * A.rec_chunk > A.rec_cap) rbase = NONE;
+    }
+    c.rbase = rbase == NONE ? NONE : rbase + lane;
     if (active) {
       tile_begin<true>(c, A, P, doc, heap, A.lane_heap_bytes, FRAMES_BYTES, RECS_BYTES);
       c.syn_off = alloc_pers(c, 256 * 16);
@@ -211,10 +222,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
       }
       status = fails ? ST_FAIL : (passes ? ST_PASS : ST_SKIP);
       n = c.err ? 0 : c.nrec + c.naux;
+      // records written into a chunk the arena could not hold: the tile is re-run after the host grows it
+      if (n && A.rec_chunk && c.rbase == NONE) { c.err = E_RECORDS; n = 0; }
       tile_stats(c, A);
     }
-    // wave-aggregated record allocation
-    uint32_t incl = n;
+    // a tile whose records fit its chunk is published in place; the others (overflow, or no chunks) get a
+    // contiguous range: wave-aggregated allocation, one atomic per wave
+    const bool in_chunk = active && A.rec_chunk && c.rbase != NONE && n <= A.rec_chunk;
+    const uint32_t need = in_chunk ? 0u : n;
+    uint32_t incl = need;
     for (uint32_t d = 1; d < 64; d <<= 1) {
       uint32_t v = __shfl_up(incl, d);
       if (lane >= d) incl += v;
@@ -224,19 +240,26 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
     if (lane == 0 && total) base = atomicAdd(A.rec_cursor, total);
     base = __shfl(base, 0);
     if (active) {
-      uint32_t off = base + incl - n;
+      uint32_t off = base + incl - need;
       bool retry = c.err == E_HEAP || c.err == E_RECORDS || c.err == E_DEPTH;
       if (retry) A.retry_list[atomicAdd(A.retry_count, 1u)] = tile;
-      if (n && off + n > A.rec_cap) { c.err = E_RECORDS; n = 0; }
+      if (need && off + need > A.rec_cap) { c.err = E_RECORDS; n = 0; }
       const uint32_t naux = n ? c.naux : 0, nrec = n - naux;
-#if GG_AB_NOREC != 1 && GG_AB_NOREC != 3   // diagnostic A/B only (2: staging off; 3: copy-out off)
-      for (uint32_t i = 0; i < nrec; i++) A.recs[off + i] = rec_load(c, i);
-#endif
-      for (uint32_t i = 0; i < naux; i++)
-        A.recs[off + nrec + i] = rec_load(c, RECS_BYTES / (uint32_t)sizeof(Rec) - 1 - i);
       TileOut o;
       o.status = status; o.err = c.err; o.err_a = c.err_a; o.err_b = c.err_b;
-      o.rec_off = off; o.rec_n = nrec; o.pad0 = naux; o.pad1 = 0;
+      o.rec_n = nrec; o.pad0 = naux;
+      if (in_chunk && n) {
+        // side records follow the tile's records in its chunk
+        for (uint32_t i = 0; i < naux; i++) rec_store(c, nrec + i, stage_load(c, RECS_BYTES / (uint32_t)sizeof(Rec) - 1 - i));
+        o.rec_off = c.rbase; o.pad1 = 1;   // slot k at rec_off + 64 k (session_fetch compacts)
+      } else {
+#if GG_AB_NOREC != 1 && GG_AB_NOREC != 3   // diagnostic A/B only (2: staging off; 3: copy-out off)
+        for (uint32_t i = 0; i < nrec; i++) A.recs[off + i] = rec_load(c, i);
+#endif
+        for (uint32_t i = 0; i < naux; i++)
+          A.recs[off + nrec + i] = stage_load(c, RECS_BYTES / (uint32_t)sizeof(Rec) - 1 - i);
+        o.rec_off = n ? off : 0; o.pad1 = 0;
+      }
       A.tiles[tile] = o;
     }
   }
@@ -342,6 +365,75 @@ __global__ void __launch_bounds__(256) rule_count_kernel(const TileOut* tiles, c
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < ncount; i += blockDim.x)
     if (lds_counts[i]) atomicAdd(&counts[i], (unsigned long long)lds_counts[i]);
+}
+
+// Record compaction (session_fetch, outside the evaluation): every tile's records -- in place in its
+// lane's direct chunk (TileOut.pad1 == 1: record k at rec_off + 64 k) or contiguous (pad1 == 0) -- are
+// copied to dst[dense_off[t] ..), dense_off an exclusive scan of the tiles' record counts (rec_n + pad0),
+// so the host receives one dense array in tile order.  Three passes: per-block sums, a one-block scan of
+// the block sums, then per-block scan + copy.  The evaluation's buffers are only read (idempotent).
+static constexpr uint32_t kScanTiles = 1024;   // tiles per block (256 threads x 4)
+__device__ __attribute__((always_inline)) inline uint32_t tile_rec_count(const TileOut* t, uint32_t i, uint32_t n) {
+  return i < n ? t[i].rec_n + t[i].pad0 : 0u;
+}
+__global__ void __launch_bounds__(256) rec_block_sums_kernel(const TileOut* tiles, uint32_t n, uint32_t* bsum) {
+  __shared__ uint32_t part[256];
+  const uint32_t i0 = blockIdx.x * kScanTiles + threadIdx.x * 4u;
+  uint32_t v = 0;
+  for (uint32_t k = 0; k < 4; k++) v += tile_rec_count(tiles, i0 + k, n);
+  part[threadIdx.x] = v;
+  __syncthreads();
+  for (uint32_t st = 128; st; st >>= 1) {
+    if (threadIdx.x < st) part[threadIdx.x] += part[threadIdx.x + st];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) bsum[blockIdx.x] = part[0];
+}
+// one block: bsum[0, nb) -> exclusive offsets in place; total records in *total
+__global__ void __launch_bounds__(1024) rec_scan_sums_kernel(uint32_t* bsum, uint32_t nb, uint32_t* total) {
+  __shared__ uint32_t sh[1024];
+  uint32_t carry = 0;
+  for (uint32_t base = 0; base < nb; base += 1024u) {
+    const uint32_t i = base + threadIdx.x;
+    const uint32_t v = i < nb ? bsum[i] : 0u;
+    sh[threadIdx.x] = v;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024u; d <<= 1) {
+      const uint32_t add = threadIdx.x >= d ? sh[threadIdx.x - d] : 0u;
+      __syncthreads();
+      sh[threadIdx.x] += add;
+      __syncthreads();
+    }
+    if (i < nb) bsum[i] = carry + sh[threadIdx.x] - v;
+    carry += sh[1023];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *total = carry;
+}
+__global__ void __launch_bounds__(256) rec_compact_kernel(const TileOut* tiles, uint32_t n, const uint32_t* bsum,
+                                                          const Rec* src, Rec* dst, uint32_t* dense_off) {
+  __shared__ uint32_t sh[256];
+  const uint32_t i0 = blockIdx.x * kScanTiles + threadIdx.x * 4u;
+  uint32_t c[4], v = 0;
+  for (uint32_t k = 0; k < 4; k++) { c[k] = tile_rec_count(tiles, i0 + k, n); v += c[k]; }
+  sh[threadIdx.x] = v;
+  __syncthreads();
+  for (uint32_t d = 1; d < 256u; d <<= 1) {
+    const uint32_t add = threadIdx.x >= d ? sh[threadIdx.x - d] : 0u;
+    __syncthreads();
+    sh[threadIdx.x] += add;
+    __syncthreads();
+  }
+  uint32_t off = bsum[blockIdx.x] + sh[threadIdx.x] - v;
+  for (uint32_t k = 0; k < 4; k++) {
+    const uint32_t i = i0 + k;
+    if (i >= n) break;
+    dense_off[i] = off;
+    const TileOut t = tiles[i];
+    const uint32_t stride = t.pad1 == 1 ? 64u : 1u;
+    for (uint32_t r = 0; r < c[k]; r++) dst[off + r] = src[t.rec_off + (size_t)r * stride];
+    off += c[k];
+  }
 }
 
 // Packs the host arena (32 B DNode) into the device arena (16 B DNodeP + key-length column).

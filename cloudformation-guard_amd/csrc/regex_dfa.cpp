@@ -20,7 +20,7 @@ struct RxErr { std::string why; bool unsupported; };
 struct Rng { uint32_t lo, hi; };
 
 struct RNode {
-  enum K { Empty, Set, Concat, Alt, Repeat, AssertStart, AssertEnd } k = Empty;
+  enum K { Empty, Set, Concat, Alt, Repeat, AssertStart, AssertEnd, WordB, NotWordB } k = Empty;
   std::vector<Rng> set;                      // code point ranges
   std::vector<std::unique_ptr<RNode>> kids;
   int min = 0, max = -1;                     // Repeat
@@ -83,6 +83,7 @@ struct RxParser {
   size_t i = 0;
   bool icase = false, dotall = false;
   int depth = 0;
+  bool has_word = false;   // \b or \B appears: the DFA tracks whether the previous character was a word one
   explicit RxParser(const std::string& s) : p(s) {}
 
   [[noreturn]] void unsup(const std::string& w) { throw RxErr{w, true}; }
@@ -160,7 +161,7 @@ struct RxParser {
       case 'a': add_literal(s, 7); return s;
       case 'x': case 'u': case 'U': add_literal(s, hex_escape(c)); return s;
       case 'p': case 'P': unsup("unicode property class");
-      case 'b': case 'B': if (in_class) invalid("\\b in class"); unsup("word boundary");
+      case 'b': case 'B': invalid("\\b in class");   // outside a class: atom() (an assertion)
       case 'A': case 'z': unsup("anchor");  // handled by caller at pattern ends
       case 'k': unsup("backreference");
       default:
@@ -379,6 +380,9 @@ struct RxParser {
       i++;
       if (i < p.size() && p[i] == 'A') { i++; return assert_node(RNode::AssertStart); }
       if (i < p.size() && p[i] == 'z') { i++; return end_node(); }
+      // Unicode word boundary / not a word boundary (regex-syntax Look::WordUnicode / WordUnicodeNegate):
+      // \w on one side and not on the other, the text's ends counting as non-word
+      if (i < p.size() && (p[i] == 'b' || p[i] == 'B')) { has_word = true; return assert_node(p[i++] == 'b' ? RNode::WordB : RNode::NotWordB); }
       return set_node(escape(false));
     }
     if (c == '*' || c == '+' || c == '?') invalid("repetition operator missing expression");
@@ -394,7 +398,8 @@ struct RxParser {
 // of classes), so the DFA table is nstates x nclasses and stays small enough for LDS even for the
 // Unicode perl classes.  The matcher decodes UTF-8 and maps a code point to its class through a
 // 128-entry ASCII table, or a binary search over the class boundaries above U+007F.
-// type 0 class set, 1 split, 2 match, 3 epsilon, 4 start-of-text assertion, 5 match at end of text
+// type 0 class set, 1 split, 2 match, 3 epsilon, 4 start-of-text assertion, 5 match at end of text,
+// 6 word boundary (\b), 7 not a word boundary (\B)
 struct NState { int type; int cset; int out, out2; };
 struct Nfa {
   std::vector<NState> s;
@@ -424,6 +429,8 @@ struct Builder {
       case RNode::Set: { int s = nfa.add(0, cset_of.at(&n)); return F{s, {{s, 0}}}; }
       case RNode::AssertStart: { int s = nfa.add(4); return F{s, {{s, 0}}}; }
       case RNode::AssertEnd: { int s = nfa.add(5); return F{s, {}}; }
+      case RNode::WordB: { int s = nfa.add(6); return F{s, {{s, 0}}}; }
+      case RNode::NotWordB: { int s = nfa.add(7); return F{s, {{s, 0}}}; }
       case RNode::Concat: {
         if (n.kids.empty()) return eps();
         F f = build(*n.kids[0]);
@@ -477,12 +484,14 @@ struct Builder {
 };
 
 // epsilon closure, in place; `mark` is a scratch bitmap over NFA states (cleared on return).
-// Start-of-text assertions pass only for the closure taken at offset 0.
-void closure(const Nfa& nfa, std::vector<int>& st, std::vector<uint8_t>& mark, bool at_start) {
+// Start-of-text assertions pass only for the closure taken at offset 0; word-boundary assertions only
+// when `look` says the position satisfies them (bit 0: \b holds, bit 1: \B holds) -- a state's closure
+// stops at them until the next character (or the end of the text) decides.
+void closure(const Nfa& nfa, std::vector<int>& st, std::vector<uint8_t>& mark, bool at_start, uint32_t look = 0) {
   for (int x : st) mark[x] = 1;
   for (size_t k = 0; k < st.size(); k++) {
     const NState& s = nfa.s[st[k]];
-    if (s.type == 1 || s.type == 3 || (s.type == 4 && at_start))
+    if (s.type == 1 || s.type == 3 || (s.type == 4 && at_start) || (s.type == 6 && (look & 1)) || (s.type == 7 && (look & 2)))
       for (int o : {s.out, s.out2}) if (o >= 0 && !mark[o]) { mark[o] = 1; st.push_back(o); }
   }
   for (int x : st) mark[x] = 0;
@@ -522,6 +531,15 @@ CompiledRegex compile_regex(const std::string& pattern) {
   // ---- code-point classes: elementary intervals keyed by the set of Set nodes containing them
   std::vector<const RNode*> sets_n;
   collect_sets(*ast, sets_n);
+  // word assertions: \w is one more partitioning set, so every class is all word or all non-word
+  // characters (it builds no NFA state)
+  RNode word_set;
+  word_set.k = RNode::Set;
+  if (ps.has_word) {
+    word_set.set = table_set(uni::kWord, uni::kWord_N);
+    normalize(word_set.set);
+    sets_n.push_back(&word_set);
+  }
   std::vector<uint32_t> cuts = {0, 128, 0x110000};
   for (auto* n : sets_n) for (auto& r : n->set) { cuts.push_back(r.lo); cuts.push_back(r.hi + 1); }
   for (uint32_t c = 1; c < 128; c++) cuts.push_back(c);   // ASCII: one interval per code point
@@ -562,6 +580,16 @@ CompiledRegex compile_regex(const std::string& pattern) {
   const int nstart = f.start;
 
   // ---- subset construction over the classes (state 0 = dead)
+  // With word assertions (regex-automata's look-behind state) a DFA state is (NFA states closed up to the
+  // word assertions, whether the previous character was a word character; the start state marked apart,
+  // as start-of-text assertions still pass there): a transition on class c first extends the closure
+  // through the assertions the boundary between the previous character and c satisfies -- a match found
+  // there (ending before c) leads to the accepting sink -- then steps on c.  At the end of the text the
+  // closure extends with the end counted as a non-word character (accept flag 2).
+  const bool hw = ps.has_word;
+  std::vector<uint8_t> cls_word(ncls0, 0);
+  if (hw) for (uint32_t c = 0; c < ncls0; c++) cls_word[c] = cls_sig[c][sets_n.size() - 1];
+  static const int kPrevWord = -1, kStartMark = -2, kMatchSink = -3;
   std::vector<uint8_t> mark(nfa.s.size(), 0);
   std::unordered_map<std::vector<int>, uint32_t, VecHash> ids;
   std::vector<std::vector<int>> sets;
@@ -569,6 +597,7 @@ CompiledRegex compile_regex(const std::string& pattern) {
   ids[{}] = 0;
   std::vector<int> s0 = {nstart};
   closure(nfa, s0, mark, true);
+  if (hw) s0.push_back(kStartMark);   // previous "character" = start of text: non-word
   auto intern = [&](std::vector<int>& st) -> uint32_t {
     auto it = ids.find(st);
     if (it != ids.end()) return it->second;
@@ -578,14 +607,39 @@ CompiledRegex compile_regex(const std::string& pattern) {
     return id;
   };
   uint32_t start = intern(s0);
+  uint32_t sink = 0;
+  if (hw) { std::vector<int> m1 = {kMatchSink}; sink = intern(m1); }
+  // split a state key into (NFA states, previous-char-is-word, is-start, is-sink)
+  auto parts = [&](const std::vector<int>& key, std::vector<int>& st, bool& pw, bool& at0, bool& sk) {
+    st.clear(); pw = at0 = sk = false;
+    for (int x : key) {
+      if (x == kPrevWord) pw = true;
+      else if (x == kStartMark) at0 = true;
+      else if (x == kMatchSink) sk = true;
+      else st.push_back(x);
+    }
+  };
   std::vector<std::vector<uint32_t>> table(1, std::vector<uint32_t>(ncls0, 0));
+  std::vector<int> here, ex;
   for (size_t cur = 1; cur < sets.size(); cur++) {
     if (sets.size() > 4000) { out.unsupported = true; out.why = "DFA too large"; return out; }
-    const std::vector<int> here = sets[cur];
+    bool pw, at0, sk;
+    parts(sets[cur], here, pw, at0, sk);
     std::vector<uint32_t> row(ncls0);
     for (uint32_t c = 0; c < ncls0; c++) {
+      if (sk) { row[c] = (uint32_t)cur; continue; }
+      const std::vector<int>* from = &here;
+      if (hw) {
+        ex = here;
+        const bool cw = cls_word[c] != 0;
+        closure(nfa, ex, mark, at0, pw != cw ? 1u : 2u);
+        bool matched = false;
+        for (int x : ex) if (nfa.s[x].type == 2) matched = true;
+        if (matched) { row[c] = sink; continue; }
+        from = &ex;
+      }
       std::vector<int> nx;
-      for (int x : here) {
+      for (int x : *from) {
         const NState& s = nfa.s[x];
         if (s.type == 0 && nfa.csets[s.cset][c]) nx.push_back(s.out);
       }
@@ -593,16 +647,26 @@ CompiledRegex compile_regex(const std::string& pattern) {
       std::sort(nx.begin(), nx.end());
       nx.erase(std::unique(nx.begin(), nx.end()), nx.end());
       closure(nfa, nx, mark, false);
+      if (hw && cls_word[c]) nx.push_back(kPrevWord);
       row[c] = intern(nx);
     }
     table.push_back(row);
   }
   // accept flags: 1 = a match ends here (is_match is decided), 2 = a match ends here if the
-  // haystack ends here (`$`)
+  // haystack ends here (`$`, or a word assertion the end of the text satisfies)
   const size_t nd = sets.size();
   std::vector<uint8_t> acc(nd, 0);
-  for (size_t st = 0; st < nd; st++)
-    for (int x : sets[st]) { if (nfa.s[x].type == 2) acc[st] |= 1; else if (nfa.s[x].type == 5) acc[st] |= 2; }
+  for (size_t st = 1; st < nd; st++) {
+    bool pw, at0, sk;
+    parts(sets[st], here, pw, at0, sk);
+    if (sk) { acc[st] = 1; continue; }
+    for (int x : here) { if (nfa.s[x].type == 2) acc[st] |= 1; else if (nfa.s[x].type == 5) acc[st] |= 2; }
+    if (hw && !(acc[st] & 1)) {
+      ex = here;
+      closure(nfa, ex, mark, at0, pw ? 1u : 2u);   // the end of the text is a non-word position
+      for (int x : ex) if (nfa.s[x].type == 2 || nfa.s[x].type == 5) acc[st] |= 2;
+    }
+  }
   // ---- Moore minimisation (block 0 stays the dead state)
   std::vector<uint32_t> blk(nd);
   for (size_t st = 0; st < nd; st++) blk[st] = st == 0 ? 0 : 1 + acc[st];

@@ -16,6 +16,9 @@ module by translating the syntax differences that matter for ``is_match``:
   ``str.isspace`` (``\\w`` would take No such as "½" and miss combining marks, ``\\s`` would take
   U+001C..U+001F), so they are spelled out as those property classes.
 * ``(?i)`` is simple case folding in both (V0 without FULLCASE).
+* ``\\b`` / ``\\B`` are Unicode word boundaries over that same ``\\w`` (regex-syntax
+  ``Look::WordUnicode`` / ``WordUnicodeNegate``; the text's ends count as non-word); Python's are over
+  its own word definition, so they are spelled out as look-arounds on the spelled-out class.
 """
 import functools
 
@@ -24,6 +27,10 @@ import regex as _re
 
 _WORD = r"\p{Alphabetic}\p{M}\p{Nd}\p{Pc}\p{Join_Control}"
 # perl class -> (outside a class, inside a class); `\W` inside a class has no V0 spelling (kept)
+_W1 = "[" + _WORD + "]"
+# \b / \B outside a class: look-arounds on the UTS #18 word class
+_BOUNDARY = {"b": "(?:(?<=%s)(?!%s)|(?<!%s)(?=%s))" % (_W1, _W1, _W1, _W1),
+             "B": "(?:(?<=%s)(?=%s)|(?<!%s)(?!%s))" % (_W1, _W1, _W1, _W1)}
 _PERL = {
     "d": (r"\p{Nd}", r"\p{Nd}"), "D": (r"\P{Nd}", r"\P{Nd}"),
     "s": (r"\p{White_Space}", r"\p{White_Space}"), "S": (r"\P{White_Space}", r"\P{White_Space}"),
@@ -59,6 +66,8 @@ def translate(pattern: str) -> str:
                 out.append(_re.escape(chr(int(pattern[i + 3:j], 16))))
                 i = j + 1
                 continue
+            elif nxt in _BOUNDARY and not in_class:
+                out.append(_BOUNDARY[nxt])
             elif nxt in _PERL and not (in_class and nxt == "W"):
                 out.append(_PERL[nxt][1 if in_class else 0])
             else:

@@ -260,6 +260,45 @@ def test_unicode_regex_pack_vs_oracle():
         assert (code, out) == (ecode, exp), fmt
 
 
+def _wordb_docs():
+    import random
+    r = random.Random(4242)
+    names = ["prod-eu", "preprod", "prod", "xprodx", "café", "café-prod", "cafés", "a_b-c", "σοφία prod", "日本 prod",
+             "e\u0301-prod", "prod\u0301", "-prod-", ""]
+    serials = ["123", "1 2 3", "١٢٣", "12a", "a1", "x", "", "9"]
+    icons = ["😀", "a", "é", " ", "_", "-", "σ"]
+    envs = ["straße", "STRASSE", "Straße!", "Σοφός", "xσy", "σ", "prod"]
+    docs = []
+    for i in range(60):
+        docs.append(json.dumps({"Resources": {
+            "r%d" % k: {"Type": r.choice(["AWS::S3::Bucket", "AWS::EC2::Volume"]),
+                        "Properties": {"Name": r.choice(names), "Serial": r.choice(serials), "Icon": r.choice(icons),
+                                       "Tags": [{"Key": "env", "Value": r.choice(envs)}]}} for k in range(4)}},
+            ensure_ascii=False))
+    return docs
+
+
+def test_word_boundary_regex_pack_vs_oracle():
+    """\\b / \\B (Unicode word boundaries) on the device: byte-identical with the oracle in every format,
+    lane and wave kernels (tests/golden/wordb_rulepack)"""
+    p = os.path.join(G, "wordb_rulepack")
+    rules = [(f, open(os.path.join(p, f)).read()) for f in sorted(os.listdir(p)) if f.endswith(".guard")]
+    data = [("w%d.json" % i, d) for i, d in enumerate(_wordb_docs())]
+    for fmt in ("json", "yaml", "sarif", "junit"):
+        exp, ecode, _ = oracle_validate(rules, data, output=fmt)
+        out, code = guard_amd.validate_structured(rules, data, output=fmt)
+        assert (code, out) == (ecode, exp), fmt
+    s = guard_amd.Session()
+    s.configure(1, 0)   # wave mode
+    for name, text in rules:
+        s.add_rules(text, name)
+    s.add_docs([t for _, t in data], [n for n, _ in data])
+    s.eval(1)
+    exp, ecode, _ = oracle_validate(rules, data)
+    assert s.report("json") == (exp, ecode)
+    s.close()
+
+
 def test_app_b13_unicode_digit_class_on_gpu():
     rules = [("d.guard", "a == /^\\d+$/")]
     out, code = guard_amd.validate_structured(rules, [("d.json", '{"a": "١٢٣"}')])

@@ -21,6 +21,11 @@ UNICODE_PATTERNS = [
     r"^.$", r"^..$", r"^\w+@\w+\.\w+$", r"[[:alpha:]]+", r"(?i)[[:upper:]]", r"^[α-ω]+$", r"(?i)^[α-ω]+$",
     r"\x{1F600}", r"^é$", r"^[^a]$", r"a$|^b", r"^$", r"(?i)^ǆ$", r"^\w\s\d$", r"(?s)^a.b$", r"^a.b$",
     r"(foo|bar)+baz", r"^(ab){2,3}$", r"x*", r"\.json$", r"^arn:aws:[a-z0-9-]+:\d{12}:", r"(?i)^(true|false)$",
+    # Unicode word boundaries (regex-syntax Look::WordUnicode / WordUnicodeNegate; round 4)
+    r"\bfoo\b", r"\b", r"\B", r"^\b", r"\b$", r"\bab", r"ab\b", r"\Bab\B", r"a\B", r"\B\d", r"\b\w+\b",
+    r"(?i)\bstraße\b", r"\bé", r"é\b", r"\b(ab|ba)+\b", r"^\B$", r"\b\s", r"(?i)\bTRUE\b|\bfalse\b",
+    r"\b[α-ω]+\b", r"x\b|\by", r"\b.\b", r"\B.\B", r"^\bab\b$", r"\b\B", r"(\bfoo)+",
+    r"\bprod\b", r"\B\d\B", r"(?i)\bstraße\b|\bσ\w*", r"^\b.\b$|^\B.\B$", r"^\b\w+\b(?:-\b\w+\b)*$", r"\bcafé\b",
 ]
 
 HAYSTACKS = [
