@@ -194,6 +194,9 @@ def main():
     ap.add_argument("--mode", choices=("auto", "lane", "wave"), default="auto",
                     help="evaluation kernel: one tile per lane (+ wave-mode retry), one tile per wavefront, or the "
                          "library's choice (gg_session_configure)")
+    ap.add_argument("--reporter", choices=("device", "host"), default="device",
+                    help="e2e: the structured JSON report rendered on the MI355X (csrc/report_gpu.hip) and copied to "
+                         "host memory, or rendered by the host writer on host threads")
     ap.add_argument("--rx-memo", choices=("per-launch", "warm"), default="per-launch",
                     help="regex is_match memo: zeroed before every launch, or kept warm across launches")
     ap.add_argument("--no-e2e", action="store_true")
@@ -378,7 +381,11 @@ def main():
         log("e2e: structured report of %d of %d documents" % (rdocs, ndocs))
         t0 = time.time()
         os.environ.setdefault("GG_PROGRESS", "1")   # a block line per 65536 documents (a long render keeps writing)
-        rep_bytes, rep_code = sess.report_bytes("json", rdocs)
+        rep_stats = None
+        if args.reporter == "device":
+            rep_bytes, rep_code, rep_stats = sess.report_json_device(rdocs)
+        else:
+            rep_bytes, rep_code = sess.report_bytes("json", rdocs)
         t_report_sample = time.time() - t0
         # the synthetic documents are alike: the whole report costs ndocs / rdocs times the sample
         t_report = t_report_sample * ndocs / max(1, rdocs)
@@ -394,11 +401,13 @@ def main():
                "upload_s": round(t_upload, 3), "eval_fetch_s": round(t_eval, 3), "report_s": round(t_report, 3),
                "report_docs_rendered": rdocs, "report_s_rendered": round(t_report_sample, 3),
                "report_bytes_rendered": rep_bytes, "report_GBps": round(rep_bytes / t_report_sample / 1e9, 3),
-               "exit_code": rep_code, "report_threads": threads,
+               "exit_code": rep_code, "report_threads": threads, "reporter": args.reporter,
+               "device_reporter": rep_stats,
                "pcie_inclusive_value": round(ntiles / (t_upload + t_eval), 1),
                "note": "one job over input text resident in host memory: load (%s) + upload + one evaluation with "
-                       "statuses/records fetched + structured JSON report rendered on the host and discarded "
-                       "(rendered for report_docs_rendered documents; report_s scaled to all when that is fewer); "
+                       "statuses/records fetched + structured JSON report rendered (reporter: device or host) and discarded "
+                       "(rendered for report_docs_rendered documents; report_s scaled to all when that is fewer; "
+                       "reporter=device: rendered on the MI355X and copied to host memory in blocks); "
                        "synthetic text generation (gen_s) is not part of the job%s"
                        % ("device JSON loader: text H2D, parse, arena D2H for the reporter" if args.loader == "device"
                           else "host loader threads", " (inside load_s with --loader host)" if gen_in_load else "")}

@@ -16,6 +16,7 @@
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -29,6 +30,7 @@
 #include "json_gpu.h"
 #include "eisel_lemire.h"
 #include "program.h"
+#include "report_gpu.h"
 #include "reporter.h"
 #include "synth_corpus.h"
 
@@ -38,7 +40,9 @@ __global__ void guard_eval_verbose_kernel(LaunchArgs A);
 __global__ void guard_eval_lanes_kernel(LaunchArgs A);
 __global__ void resource_type_kernel(DevBatch D);
 __global__ void shape_key_kernel(DevBatch D, const uint32_t* top8, unsigned long long* key);
-__global__ void pack_nodes_kernel(const DNode* in, DNodeP* out, uint32_t* klen, uint64_t n, uint32_t* bad);
+__global__ void pack_nodes_kernel(const DNode* in, DNodeP* out, uint32_t* klen, uint32_t* parent, uint64_t n, uint32_t* bad);
+__global__ void report_size_kernel(RenderArgs A);
+__global__ void report_write_kernel(RenderArgs A);
 __global__ void rec_block_sums_kernel(const TileOut* tiles, uint32_t n, uint32_t* bsum);
 __global__ void rec_scan_sums_kernel(uint32_t* bsum, uint32_t nb, uint32_t* total);
 __global__ void rec_compact_kernel(const TileOut* tiles, uint32_t n, const uint32_t* bsum, const Rec* src, Rec* dst,
@@ -234,6 +238,15 @@ struct GpuProgram {
 struct DeviceBufs {
   DBuf<DNodeP> d_nodes;         // packed device arena
   DBuf<uint32_t> d_klen;        // per node key length (cold)
+  DBuf<uint32_t> d_parent;      // per node parent (device reporter: JSON pointers)
+  DBuf<uint32_t> d_line, d_col; // per node marks (device reporter), uploaded at its first use
+  DBuf<uint8_t> d_rtab;         // device reporter tables (RProg sections, sorted rule names)
+  DBuf<RProg> d_rprogs;
+  DBuf<char> d_rnames;          // the block's document names
+  DBuf<uint64_t> d_rname_off, d_rsizes, d_roffs;
+  DBuf<char> d_rtext;           // the block's rendered text
+  char* pinned = nullptr;       // host staging for report text (kPinnedBytes)
+  static constexpr size_t kPinnedBytes = (size_t)256 << 20;
   DBuf<char> d_bytes;
   DBuf<uint32_t> d_roots;
   DBuf<uint64_t> d_base;
@@ -263,11 +276,13 @@ struct DeviceBufs {
   explicit DeviceBufs(int d) : device(d) { HIPCHK(hipSetDevice(d)); HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking)); }
   ~DeviceBufs() {
     hipSetDevice(device);
+    if (pinned) hipHostFree(pinned);
     for (auto& pr : evq) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
     if (stream) hipStreamDestroy(stream);
   }
   size_t bytes() const {
-    return d_nodes.bytes() + d_klen.bytes() + d_bytes.bytes() + d_roots.bytes() + d_base.bytes() + d_res_map.bytes() +
+    return d_nodes.bytes() + d_klen.bytes() + d_parent.bytes() + d_line.bytes() + d_col.bytes() + d_rtab.bytes() +
+           d_rtext.bytes() + d_bytes.bytes() + d_roots.bytes() + d_base.bytes() + d_res_map.bytes() +
            d_tix_off.bytes() + d_tix.bytes() + d_progs.bytes() + d_rx_memo.bytes() + d_heaps.bytes() + d_lane_heaps.bytes() + d_retry.bytes() +
            d_big_heaps.bytes() + d_retry2.bytes() + d_tiles.bytes() + d_rule_status.bytes() + d_recs.bytes() +
            d_recs_dense.bytes() + d_dense_off.bytes() + d_bsum.bytes() +
@@ -344,6 +359,15 @@ struct gg_session {
   uint32_t rec_chunk = 0;         // lane mode: direct record slots per lane per batch (eval_core.inc rec_store)
   size_t rx_memo_words = 0;       // words of the regex is_match memo (0: none)
   bool rx_memo_per_launch = false;   // zero the memo before every launch (bench: no warm memo across steps)
+  bool marks_on_device = false;   // d_line / d_col hold docs.line / docs.col (device reporter)
+  bool fetched_on_device = false; // the fetched results are the device's (tiles, dense records): it can report them
+  bool rtab_ready = false;        // d_rtab / d_rprogs built for the current programs
+  int32_t device_report = -1;     // 1: JSON reports rendered on the device, 0: host, -1: GG_DEVICE_REPORT (default 1)
+  // device reporter: the sorted rule-name tables inside d_rtab (render_tables)
+  const char* r_sname_text = nullptr;
+  const RStr* r_sname = nullptr;
+  const uint32_t *r_sname_first = nullptr, *r_sname_n = nullptr, *r_sname_fk = nullptr;
+  uint32_t r_nsname = 0;
   // results
   std::vector<TileOut> tiles;
   std::vector<uint8_t> rule_status;
@@ -411,12 +435,17 @@ void session_upload(gg_session* s) {
     }
     s->dv->d_nodes.alloc(std::max<size_t>(n, 1));
     s->dv->d_klen.alloc(std::max<size_t>(n, 1));
+    s->dv->d_parent.alloc(std::max<size_t>(n, 1));
+    s->marks_on_device = false;
+    s->rtab_ready = false;
+    s->fetched_on_device = false;
     DBuf<uint32_t> bad;
     bad.alloc(1);
     HIPCHK(hipMemsetAsync(bad.p, 0, 4, st));
     if (n) {
       const uint32_t blocks = (uint32_t)std::min<size_t>((n + 255) / 256, (size_t)dev_ncu(s->device) * 64);
-      hipLaunchKernelGGL(pack_nodes_kernel, dim3(blocks), dim3(256), 0, st, src, s->dv->d_nodes.p, s->dv->d_klen.p, (uint64_t)n, bad.p);
+      hipLaunchKernelGGL(pack_nodes_kernel, dim3(blocks), dim3(256), 0, st, src, s->dv->d_nodes.p, s->dv->d_klen.p, s->dv->d_parent.p,
+                         (uint64_t)n, bad.p);
       HIPCHK(hipGetLastError());
     }
     uint32_t b = 0;
@@ -745,6 +774,7 @@ void session_fetch(gg_session* s) {
   HIPCHK(hipMemcpy(s->counts.data(), s->ext_counts ? s->ext_counts : s->dv->d_counts.p, s->ncounts * sizeof(unsigned long long),
                    hipMemcpyDeviceToHost));
   s->evaluated = true;
+  s->fetched_on_device = ntiles > 0;
 }
 
 // one complete evaluation; re-runs when the first pass overflowed the record arena (grown) or left
@@ -789,6 +819,269 @@ unsigned report_threads() {
   return std::max(1u, n ? n : 1u);
 }
 
+// ------------------------------------------------------------------ device reporter ---
+// The structured JSON report rendered on the session's device (report_gpu.hip): the reporter's tables
+// (context strings, messages, rule names, remaining-query texts, literal arena, sorted rule names) built
+// once per upload, the marks uploaded at first use, then per block of documents a size pass, offsets, a
+// write pass and the text copied out in document order, with the documents the device writer leaves to
+// the host (floats, Debug-formatted reasons, ...) written by the host writer at their positions.
+bool device_report_on(const gg_session* s) {
+  if (s->device_report >= 0) return s->device_report != 0;
+  const char* e = getenv("GG_DEVICE_REPORT");
+  return !e || atoi(e) != 0;
+}
+
+// where report text goes: reserve(n) gives room for the next n bytes, commit(n) takes them
+struct ReportSink {
+  virtual ~ReportSink() = default;
+  virtual char* reserve(size_t n) = 0;
+  virtual void commit(size_t n) = 0;
+  virtual size_t max_piece() const { return SIZE_MAX; }
+  void write(const char* p, size_t n) {
+    while (n) {
+      const size_t k = std::min(n, max_piece());
+      memcpy(reserve(k), p, k);
+      commit(k);
+      p += k; n -= k;
+    }
+  }
+};
+// the report as one malloc'd NUL-terminated buffer (grown by realloc: glibc moves large blocks by mremap)
+struct BufferSink : ReportSink {
+  char* p = nullptr;
+  size_t n = 0, cap = 0;
+  ~BufferSink() override { free(p); }
+  char* reserve(size_t k) override {
+    if (n + k + 1 > cap) {
+      size_t nc = std::max<size_t>(cap * 2, n + k + 1);
+      nc = std::max<size_t>(nc, 1 << 16);
+      char* q = (char*)realloc(p, nc);
+      if (!q) throw std::bad_alloc();
+      p = q; cap = nc;
+    }
+    return p + n;
+  }
+  void commit(size_t k) override { n += k; }
+  char* take() { reserve(0); p[n] = 0; char* r = p; p = nullptr; n = cap = 0; return r; }
+};
+// counts the bytes and drops them (end-to-end measurement: the text reaches host memory, then is discarded)
+struct CountingSink : ReportSink {
+  char* stage;
+  size_t stage_bytes;
+  uint64_t n = 0;
+  CountingSink(char* st, size_t sb) : stage(st), stage_bytes(sb) {}
+  char* reserve(size_t) override { return stage; }
+  void commit(size_t k) override { n += k; }
+  size_t max_piece() const override { return stage_bytes; }
+};
+
+struct DevReportStats { uint64_t device_docs = 0, host_docs = 0, bytes = 0; double size_ms = 0, write_ms = 0, d2h_ms = 0, host_ms = 0; };
+
+void render_tables(gg_session* s) {
+  if (s->rtab_ready) return;
+  std::vector<uint8_t> blob;
+  auto put = [&](const void* p, size_t n) -> size_t {
+    size_t o = (blob.size() + 15) & ~(size_t)15;
+    blob.resize(o + std::max<size_t>(n, 1), 0);
+    if (n) memcpy(blob.data() + o, p, n);
+    return o;
+  };
+  struct Offs { size_t text, ctx, msgs, rnames, rem_first, rem, pkey, pidx, clauses, lit, lit_bytes, lit_line, lit_col; uint32_t nc, nl, nr, nq, nx, nm; };
+  std::vector<Offs> offs;
+  for (auto& gp : s->progs) {
+    const Program& P = gp->prog;
+    std::string text;
+    auto add = [&](const std::string& x) { RStr r{(uint32_t)text.size(), (uint32_t)x.size()}; text += x; return r; };
+    std::vector<RStr> ctx, msgs, rn, rem, pkey;
+    std::vector<uint32_t> rem_first;
+    std::vector<int32_t> pidx;
+    for (auto& x : P.ctx) ctx.push_back(add(x));
+    for (auto& x : P.msgs) msgs.push_back(add(x));
+    for (auto& x : P.rule_names) rn.push_back(add(x));
+    for (size_t q = 0; q < P.queries.size(); q++) {
+      rem_first.push_back((uint32_t)rem.size());
+      const auto& parts = P.queries[q];
+      for (size_t st = 0; st <= parts.size(); st++) {
+        rem.push_back(add(P.query_remaining((uint32_t)q, (uint32_t)st)));
+        pkey.push_back(st < parts.size() ? add(parts[st].key) : RStr{0, 0});
+        pidx.push_back(st < parts.size() ? parts[st].index : 0);
+      }
+    }
+    rem_first.push_back((uint32_t)rem.size());
+    Offs o;
+    o.text = put(text.data(), text.size());
+    o.ctx = put(ctx.data(), ctx.size() * sizeof(RStr));
+    o.msgs = put(msgs.data(), msgs.size() * sizeof(RStr));
+    o.rnames = put(rn.data(), rn.size() * sizeof(RStr));
+    o.rem_first = put(rem_first.data(), rem_first.size() * 4);
+    o.rem = put(rem.data(), rem.size() * sizeof(RStr));
+    o.pkey = put(pkey.data(), pkey.size() * sizeof(RStr));
+    o.pidx = put(pidx.data(), pidx.size() * 4);
+    o.clauses = put(P.clauses.data(), P.clauses.size() * sizeof(PClause));
+    o.lit = put(P.lit.nodes.data(), P.lit.nodes.size() * sizeof(DNode));
+    o.lit_bytes = put(P.lit.bytes.data(), P.lit.bytes.size());
+    o.lit_line = put(P.lit.line.data(), P.lit.line.size() * 4);
+    o.lit_col = put(P.lit.col.data(), P.lit.col.size() * 4);
+    o.nc = (uint32_t)P.clauses.size(); o.nl = (uint32_t)P.lit.nodes.size(); o.nr = (uint32_t)P.rule_names.size();
+    o.nq = (uint32_t)P.queries.size(); o.nx = (uint32_t)P.ctx.size(); o.nm = (uint32_t)P.msgs.size();
+    offs.push_back(o);
+  }
+  // not_applicable / compliant: the distinct top-level rule names, sorted as std::set<std::string> sorts them
+  std::map<std::string, std::vector<uint32_t>> names;
+  for (size_t f = 0; f < s->progs.size(); f++) {
+    const Program& P = s->progs[f]->prog;
+    for (uint32_t k = 0; k < P.n_rules; k++) names[P.rule_names[P.rule_names.size() - P.n_rules + k]].push_back((uint32_t)(f << 16 | k));
+  }
+  std::string stext;
+  std::vector<RStr> sname;
+  std::vector<uint32_t> sfirst, sn, sfk;
+  for (auto& kv : names) {
+    sname.push_back(RStr{(uint32_t)stext.size(), (uint32_t)kv.first.size()});
+    stext += kv.first;
+    sfirst.push_back((uint32_t)sfk.size());
+    sn.push_back((uint32_t)kv.second.size());
+    for (uint32_t x : kv.second) sfk.push_back(x);
+  }
+  const size_t o_stext = put(stext.data(), stext.size()), o_sname = put(sname.data(), sname.size() * sizeof(RStr)),
+               o_sfirst = put(sfirst.data(), sfirst.size() * 4), o_sn = put(sn.data(), sn.size() * 4), o_sfk = put(sfk.data(), sfk.size() * 4);
+  hipStream_t st = s->dv->stream;
+  s->dv->d_rtab.upload(blob.data(), blob.size(), st);
+  const uint8_t* b = s->dv->d_rtab.p;
+  std::vector<RProg> rp;
+  for (auto& o : offs) {
+    RProg r{};
+    r.text = (const char*)(b + o.text); r.ctx = (const RStr*)(b + o.ctx); r.msgs = (const RStr*)(b + o.msgs);
+    r.rule_names = (const RStr*)(b + o.rnames); r.rem_first = (const uint32_t*)(b + o.rem_first); r.rem = (const RStr*)(b + o.rem);
+    r.pkey = (const RStr*)(b + o.pkey); r.pidx = (const int32_t*)(b + o.pidx); r.clauses = (const PClause*)(b + o.clauses);
+    r.lit = (const DNode*)(b + o.lit); r.lit_bytes = (const char*)(b + o.lit_bytes);
+    r.lit_line = (const uint32_t*)(b + o.lit_line); r.lit_col = (const uint32_t*)(b + o.lit_col);
+    r.n_clauses = o.nc; r.n_lit = o.nl; r.n_rule_names = o.nr; r.n_queries = o.nq; r.n_ctx = o.nx; r.n_msgs = o.nm;
+    rp.push_back(r);
+  }
+  s->dv->d_rprogs.upload(rp.data(), std::max<size_t>(rp.size(), 1), st);
+  s->r_sname_text = (const char*)(b + o_stext); s->r_sname = (const RStr*)(b + o_sname);
+  s->r_sname_first = (const uint32_t*)(b + o_sfirst); s->r_sname_n = (const uint32_t*)(b + o_sn);
+  s->r_sname_fk = (const uint32_t*)(b + o_sfk); s->r_nsname = (uint32_t)sname.size();
+  if (!s->marks_on_device) {
+    const size_t n = s->docs.nodes.size();
+    s->dv->d_line.upload(s->docs.line.data(), std::max<size_t>(n, 1), st);
+    s->dv->d_col.upload(s->docs.col.data(), std::max<size_t>(n, 1), st);
+    s->marks_on_device = true;
+  }
+  if (!s->dv->pinned) HIPCHK(hipHostMalloc((void**)&s->dv->pinned, DeviceBufs::kPinnedBytes, hipHostMallocDefault));
+  HIPCHK(hipStreamSynchronize(st));
+  s->rtab_ready = true;
+}
+
+// JSON FileReports of documents [first, first + count) into `sink` (each preceded by ",\n" unless it is
+// report_first, and by two spaces); the session was evaluated and fetched on its device.  false + err when
+// a document's report aborts (the host writer's Fatal; the first such document in order).
+bool device_report_json(gg_session* s, size_t first, size_t count, size_t report_first, ReportSink& sink, ReportError& err,
+                        DevReportStats* stats) {
+  bind_device(s);
+  render_tables(s);
+  hipStream_t st = s->dv->stream;
+  std::vector<const Program*> progs;
+  for (auto& p : s->progs) progs.push_back(&p->prog);
+  const size_t nf = progs.size();
+  size_t kBlock = getenv("GG_DREPORT_BLOCK") ? (size_t)std::max(1, atoi(getenv("GG_DREPORT_BLOCK"))) : 32768;
+  DevReportStats local;
+  DevReportStats& S = stats ? *stats : local;
+  std::vector<uint64_t> sizes, offs;
+  std::vector<char> names;
+  std::vector<uint64_t> name_off;
+  hipEvent_t e0, e1, e2;
+  HIPCHK(hipEventCreate(&e0)); HIPCHK(hipEventCreate(&e1)); HIPCHK(hipEventCreate(&e2));
+  struct EvFree { hipEvent_t a, b, c; ~EvFree() { hipEventDestroy(a); hipEventDestroy(b); hipEventDestroy(c); } } evf{e0, e1, e2};
+  for (size_t d0 = first; d0 < first + count; d0 += kBlock) {
+    const size_t nb = std::min(kBlock, first + count - d0);
+    names.clear(); name_off.assign(1, 0);
+    for (size_t k = 0; k < nb; k++) {
+      const std::string& nm = s->docs.names[d0 + k];
+      names.insert(names.end(), nm.begin(), nm.end());
+      name_off.push_back(names.size());
+    }
+    s->dv->d_rnames.upload(names.data(), std::max<size_t>(names.size(), 1), st);
+    s->dv->d_rname_off.upload(name_off.data(), name_off.size(), st);
+    s->dv->d_rsizes.alloc(nb);
+    RenderArgs A{};
+    A.nodes = s->dv->d_nodes.p; A.klen = s->dv->d_klen.p; A.pool = s->dv->d_bytes.p; A.parent = s->dv->d_parent.p;
+    A.line = s->dv->d_line.p; A.col = s->dv->d_col.p; A.base = s->dv->d_base.p; A.n_nodes = s->docs.nodes.size();
+    A.progs = s->dv->d_rprogs.p; A.nfiles = (uint32_t)nf; A.max_top = s->max_top;
+    A.tiles = s->dv->d_tiles.p; A.rule_status = s->dv->d_rule_status.p; A.recs = s->dv->d_recs_dense.p; A.rec_off = s->dv->d_dense_off.p;
+    A.sname_text = s->r_sname_text; A.sname = s->r_sname; A.sname_first = s->r_sname_first; A.sname_n = s->r_sname_n;
+    A.sname_fk = s->r_sname_fk; A.n_sname = s->r_nsname;
+    A.doc0 = (uint32_t)d0; A.ndocs = (uint32_t)nb; A.report_first = (uint32_t)report_first;
+    A.names = s->dv->d_rnames.p; A.name_off = s->dv->d_rname_off.p; A.sizes = s->dv->d_rsizes.p;
+    const uint32_t blocks = (uint32_t)std::min<size_t>((nb + 255) / 256, (size_t)dev_ncu(s->device) * 8);
+    HIPCHK(hipEventRecord(e0, st));
+    hipLaunchKernelGGL(report_size_kernel, dim3(blocks), dim3(256), 0, st, A);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(e1, st));
+    sizes.resize(nb);
+    HIPCHK(hipMemcpyAsync(sizes.data(), s->dv->d_rsizes.p, nb * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, e0, e1)); S.size_ms += ms;
+    offs.resize(nb);
+    uint64_t total = 0;
+    for (size_t k = 0; k < nb; k++) {
+      offs[k] = total;
+      if (!(sizes[k] & kHostDoc)) total += sizes[k];
+    }
+    s->dv->d_rtext.alloc(std::max<uint64_t>(total, 1));
+    s->dv->d_roffs.upload(offs.data(), nb, st);
+    A.offsets = s->dv->d_roffs.p; A.out = s->dv->d_rtext.p;
+    HIPCHK(hipEventRecord(e1, st));
+    hipLaunchKernelGGL(report_write_kernel, dim3(blocks), dim3(256), 0, st, A);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(e2, st));
+    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(hipEventElapsedTime(&ms, e1, e2)); S.write_ms += ms;
+    // copy out in document order: runs of device documents, host documents between them
+    size_t k = 0;
+    while (k < nb) {
+      if (sizes[k] & kHostDoc) {
+        const auto h0 = std::chrono::steady_clock::now();
+        const size_t d = d0 + k;
+        TextBuf t;
+        if (d != report_first) t.append(",\n", 2);
+        t.append(2, ' ');
+        std::vector<TileResult> trs(nf);
+        std::vector<const TileResult*> tp(nf);
+        for (size_t f = 0; f < nf; f++) {
+          trs[f] = tile_view(s->tiles.data(), s->rule_status.data(), s->max_top, s->recs.data(), d * nf + f);
+          tp[f] = &trs[f];
+        }
+        if (!report_json_doc(s->docs, (uint32_t)d, progs, tp, t, err)) return false;
+        sink.write(t.data(), t.size());
+        S.bytes += t.size();
+        S.host_docs++;
+        S.host_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count();
+        k++;
+        continue;
+      }
+      size_t k1 = k;
+      uint64_t bytes = 0;
+      while (k1 < nb && !(sizes[k1] & kHostDoc)) { bytes += sizes[k1]; k1++; }
+      const auto c0 = std::chrono::steady_clock::now();
+      uint64_t at = offs[k];
+      while (bytes) {
+        const size_t piece = (size_t)std::min<uint64_t>(bytes, sink.max_piece());
+        HIPCHK(hipMemcpyAsync(sink.reserve(piece), s->dv->d_rtext.p + at, piece, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        sink.commit(piece);
+        at += piece; bytes -= piece; S.bytes += piece;
+      }
+      S.d2h_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - c0).count();
+      S.device_docs += k1 - k;
+      k = k1;
+    }
+    if (getenv("GG_PROGRESS")) fprintf(stderr, "[device report] %zu / %zu documents, %llu bytes\n", d0 + nb - first, count, (unsigned long long)S.bytes);
+  }
+  return true;
+}
+
 // One shard of a structured report: documents [first, first + count) of a fetched session.
 struct ShardView {
   gg_session* s;
@@ -818,10 +1111,32 @@ bool shards_report(const std::vector<ShardView>& sh, std::string& out, int32_t& 
     }
   }
   out.clear();
+  bool anyfail = false;
+  bool on_device = fmt == OUT_JSON && cstr && !sh.empty();
+  for (const ShardView& v : sh) on_device = on_device && (v.count == 0 || (device_report_on(v.s) && v.s->fetched_on_device));
+  if (on_device) {
+    // the FileReports rendered on the shards' devices (report_gpu.hip), joined in document order
+    BufferSink sink;
+    size_t ndocs = 0;
+    bool firstdoc = true;
+    sink.write("[\n", 2);
+    for (const ShardView& v : sh) {
+      if (!v.count) continue;
+      if (!device_report_json(v.s, v.first, v.count, firstdoc ? v.first : SIZE_MAX, sink, err, nullptr)) { exit_code = -1; return false; }
+      firstdoc = false;
+      ndocs += v.count;
+      const size_t nf = v.s->progs.size();
+      for (size_t t = v.first * nf; t < (v.first + v.count) * nf; t++) if (v.s->tiles[t].status == ST_FAIL) anyfail = true;
+    }
+    if (ndocs) sink.write("\n]", 2);
+    else { sink.n = 0; sink.write("[]", 2); }
+    *cstr = sink.take();
+    if (anyfail && !(fmt == OUT_JUNIT && exit_code == 5)) exit_code = 19;
+    return true;
+  }
   std::vector<TextBuf> all_parts;
   std::vector<std::unique_ptr<ReportWriter>> writers;
   std::vector<std::string> yaml_parts;
-  bool anyfail = false;
   for (const ShardView& v : sh) {
     gg_session* s = v.s;
     std::vector<const Program*> progs;
@@ -1808,6 +2123,45 @@ int64_t gg_session_report_bytes(gg_session* s, int32_t output_format, size_t max
 
 size_t gg_session_ncounts(gg_session* s) { return s->ncounts; }
 void* gg_session_counts_device(gg_session* s) { return s->ext_counts ? (void*)s->ext_counts : s->dv ? (void*)s->dv->d_counts.p : nullptr; }
+int64_t gg_session_report_json_device(gg_session* s, size_t max_docs, int32_t* exit_code, double* stats, extern_err_t* err) {
+  set_err(err, 0, "");
+  if (!s->evaluated || !s->fetched_on_device) { set_err(err, -1, "session not evaluated and fetched on a device"); return -1; }
+  try {
+    std::vector<const Program*> progs;
+    for (auto& p : s->progs) progs.push_back(&p->prog);
+    const size_t nf = progs.size(), nd = max_docs ? std::min(max_docs, s->docs.ndocs()) : s->docs.ndocs();
+    for (size_t t = 0; t < nd * nf; t++)
+      if (s->tiles[t].err) {
+        ReportError re;
+        tile_error(s->docs, (uint32_t)(t / nf), *progs[t % nf], s->tiles[t], re);
+        set_err(err, ffi_code(re.kind), error_display(re.kind, re.msg));
+        if (exit_code) *exit_code = -1;
+        return -1;
+      }
+    bind_device(s);
+    render_tables(s);
+    CountingSink sink(s->dv->pinned, DeviceBufs::kPinnedBytes);
+    DevReportStats st;
+    ReportError re;
+    if (!device_report_json(s, 0, nd, 0, sink, re, &st)) {
+      set_err(err, ffi_code(re.kind), error_display(re.kind, re.msg));
+      if (exit_code) *exit_code = -1;
+      return -1;
+    }
+    const int64_t bytes = (int64_t)sink.n + (nd ? 4 : 2);   // "[\n" ... "\n]" or "[]"
+    bool anyfail = false;
+    for (size_t t = 0; t < nd * nf; t++) if (s->tiles[t].status == ST_FAIL) anyfail = true;
+    if (exit_code) *exit_code = anyfail ? 19 : (s->parse_errors.empty() ? 0 : 5);
+    if (stats) {
+      stats[0] = (double)st.device_docs; stats[1] = (double)st.host_docs; stats[2] = st.size_ms; stats[3] = st.write_ms;
+      stats[4] = st.d2h_ms; stats[5] = st.host_ms; stats[6] = (double)st.bytes; stats[7] = 0;
+    }
+    return bytes;
+  } catch (std::exception& e) { set_err(err, -1, e.what()); return -1; }
+}
+
+int32_t gg_session_set_device_report(gg_session* s, int32_t on) { s->device_report = on < 0 ? -1 : (on ? 1 : 0); return 0; }
+
 void gg_session_bind_counts(gg_session* s, void* dev, size_t n) {
   s->ext_counts = (dev && n >= s->ncounts) ? (unsigned long long*)dev : nullptr;
 }
@@ -2279,6 +2633,7 @@ int32_t gg_session_load_results(gg_session* s, const char* path, extern_err_t* e
   fclose(f);
   if (!ok) { set_err(err, -1, "results file does not match this session"); return -1; }
   s->evaluated = true;
+  s->fetched_on_device = false;   // host results only: the host writer reports them
   return 0;
 }
 

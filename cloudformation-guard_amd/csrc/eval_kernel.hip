@@ -436,10 +436,11 @@ __global__ void __launch_bounds__(256) rec_compact_kernel(const TileOut* tiles, 
   }
 }
 
-// Packs the host arena (32 B DNode) into the device arena (16 B DNodeP + key-length column).
+// Packs the host arena (32 B DNode) into the device arena (16 B DNodeP + key-length column) and the
+// parent column the device reporter walks.
 // bad[0] = 1: a count past 2^28; 2: a map entry whose key offset is not its key id.
-__global__ void __launch_bounds__(256) pack_nodes_kernel(const DNode* in, DNodeP* out, uint32_t* klen, uint64_t n,
-                                                         uint32_t* bad) {
+__global__ void __launch_bounds__(256) pack_nodes_kernel(const DNode* in, DNodeP* out, uint32_t* klen, uint32_t* parent,
+                                                         uint64_t n, uint32_t* bad) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const DNode d = in[i];
     if (d.count > kMaxPackedCount) atomicOr(bad, 1u);
@@ -448,6 +449,7 @@ __global__ void __launch_bounds__(256) pack_nodes_kernel(const DNode* in, DNodeP
     p.kc = d.kind | (d.count << 4); p.a = d.a; p.b = d.b; p.key_hash = d.key_off != NONE ? d.key_hash : 0u;
     out[i] = p;
     klen[i] = d.key_off != NONE ? d.key_len : 0u;
+    parent[i] = d.parent;   // the device reporter's JSON pointers (report_gpu.hip)
   }
 }
 

@@ -1143,6 +1143,15 @@ bool write_file_report(const DocBatch& docs, uint32_t doc, const std::vector<con
   }
 }
 
+}  // namespace
+
+bool report_json_doc(const DocBatch& docs, uint32_t doc, const std::vector<const Program*>& progs,
+                     const std::vector<const TileResult*>& tiles, TextBuf& out, ReportError& err) {
+  return write_file_report(docs, doc, progs, tiles, 1, out, err);
+}
+
+namespace {
+
 const J* field(const J& o, const char* k) {
   for (auto& kv : o.o) if (kv.first == k) return &kv.second;
   return nullptr;

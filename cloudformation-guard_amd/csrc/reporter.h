@@ -261,6 +261,10 @@ bool report_batch_json_parts(const DocBatch& docs, const std::vector<const Progr
                              const std::function<TileResult(size_t doc, size_t file)>& tile, unsigned nthreads,
                              std::vector<TextBuf>& parts, ReportError& err);
 size_t json_parts_size(const std::vector<TextBuf>& parts);
+// one document's FileReport, streamed JSON at indent 1 (what report_batch_json_parts writes per document,
+// without the separator and the two leading spaces); false + err on an abort
+bool report_json_doc(const DocBatch& docs, uint32_t doc, const std::vector<const Program*>& progs,
+                     const std::vector<const TileResult*>& tiles, TextBuf& out, ReportError& err);
 size_t json_parts_count(const std::vector<TextBuf>& parts);   // non-empty parts
 char* json_parts_join(const std::vector<TextBuf>& parts);
 

@@ -73,6 +73,11 @@ def lib():
                                            ctypes.c_size_t, ctypes.POINTER(ctypes.c_int32),
                                            ctypes.POINTER(ExternError)]
     L.gg_session_report_shards.restype = ctypes.c_void_p
+    L.gg_session_report_json_device.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int32),
+                                                ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ExternError)]
+    L.gg_session_report_json_device.restype = ctypes.c_int64
+    L.gg_session_set_device_report.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+    L.gg_session_set_device_report.restype = ctypes.c_int32
     L.gg_session_set_device.argtypes = [ctypes.c_void_p, ctypes.c_int32]
     L.gg_session_set_device.restype = ctypes.c_int32
     L.cfn_guard_validate_console.argtypes = [ctypes.POINTER(ValidateInput), ctypes.c_size_t,
@@ -516,6 +521,22 @@ class Session:
         if err.code != 0:
             _raise(err)
         return _owned_bytes(p, ln.value), code.value
+
+    def report_json_device(self, max_docs=0):
+        """the JSON report of the first max_docs documents (0: all) rendered on the device, copied to host
+        memory and discarded: (bytes, exit code, stats)"""
+        code = ctypes.c_int32(0)
+        st = (ctypes.c_double * 8)()
+        err = ExternError()
+        n = lib().gg_session_report_json_device(self.s, max_docs, ctypes.byref(code), st, ctypes.byref(err))
+        if err.code != 0:
+            _raise(err)
+        keys = ("device_docs", "host_docs", "size_ms", "write_ms", "d2h_ms", "host_ms", "body_bytes")
+        return n, code.value, dict(zip(keys, list(st)[:7]))
+
+    def set_device_report(self, on):
+        """JSON reports rendered on the device (True), on host threads (False), or per GG_DEVICE_REPORT (None)"""
+        lib().gg_session_set_device_report(self.s, -1 if on is None else int(bool(on)))
 
     def report_shards(self, output="json", cuts=()):
         """the report rendered as the shards [0, cuts[0]), [cuts[0], cuts[1]), ... and joined as the

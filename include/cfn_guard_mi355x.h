@@ -196,6 +196,17 @@ int32_t gg_session_counts(gg_session *s, uint64_t *out, size_t n);
  * text would not fit in memory) */
 int64_t gg_session_report_bytes(gg_session *s, int32_t output_format, size_t max_docs, int32_t *exit_code,
                                 extern_err_t *err);
+/* The structured JSON report of the first max_docs documents (0: all) rendered on the session's device
+ * (csrc/report_gpu.hip: a size pass and a write pass per block of documents, one lane per document), copied
+ * to host memory block by block and discarded; documents the device writer leaves to the host writer
+ * (floats, Debug-formatted reasons, map keys / count() values as values) are written by it in place.
+ * Returns the report's size in bytes (gg_session_report_bytes' end-to-end measurement, reporter on the
+ * device); stats (may be NULL, 8 doubles): device documents, host documents, size-pass ms, write-pass ms,
+ * copy-out ms, host-writer ms, body bytes, 0. */
+int64_t gg_session_report_json_device(gg_session *s, size_t max_docs, int32_t *exit_code, double *stats, extern_err_t *err);
+/* JSON reports of this session (gg_session_report*, the batch entry points): 1 rendered on the device
+ * (default, GG_DEVICE_REPORT=0 turns it off), 0 on host threads, -1 back to the environment's choice. */
+int32_t gg_session_set_device_report(gg_session *s, int32_t on);
 /* diagnostic evaluator counters (nonzero only in the GG_STATS build variant) */
 int32_t gg_session_kernel_stats(gg_session *s, uint64_t *out, size_t n);
 
