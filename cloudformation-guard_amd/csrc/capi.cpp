@@ -351,6 +351,8 @@ struct gg_session {
   // large-heap pass (rare: documents with thousands of failing clause values or deep nesting)
   static constexpr uint32_t kBigHeap = 32u << 20, kBigFrames = 1u << 20, kBigRecs = 16u << 20, kBigSlots = 8;
   uint32_t lane_heap_bytes = 64 * 1024;
+  uint32_t lane_heap_set = 0;     // gg_session_configure's lane heap (0: sized at upload)
+  uint32_t lane_recs_bytes = 24576;   // record staging per lane (eval_core.inc RECS_BYTES by default)
   uint32_t lds_prog_words = 2048;              // per-launch program staging window (words)
   static constexpr uint32_t kMaxLdsProgWords = 4096;   // 16 KB
   int32_t mode = 0;               // 0: lane mode + wave-mode retry; 1: wave mode only
@@ -604,6 +606,18 @@ void session_upload(gg_session* s) {
   s->lane_slots = s->mode == 1 ? 0 : (uint32_t)std::min<size_t>(std::max<size_t>(nbatches, 1), (size_t)dev_ncu(s->device) * lane_waves_per_cu);
   // every one of the 8 per-XCD queues needs waves (block b serves queue b % 8)
   if (s->lane_slots) s->lane_slots = (std::max<uint32_t>(s->lane_slots, 8u) + 7u) & ~7u;
+  // Few lane batches (a corpus of few, large documents: cfg4's plans) leave most of the lane heaps' memory
+  // budget unused while their tiles outgrow 64 KB (hundreds of records, long QR lists) and fall back to
+  // the wave kernel one tile per wave: such launches get 256 KB lane heaps with 96 KB of record staging
+  // while the heaps stay within kLaneHeapBudget
+  static constexpr size_t kLaneHeapBudget = (size_t)8 << 30;
+  s->lane_heap_bytes = s->lane_heap_set ? s->lane_heap_set : 64u * 1024u;
+  s->lane_recs_bytes = 24576;
+  const bool large_docs = s->docs.ndocs() && s->docs.nodes.size() / s->docs.ndocs() > 4096;
+  if (!s->lane_heap_set && large_docs && s->lane_slots && (size_t)s->lane_slots * 64 * (256u << 10) <= kLaneHeapBudget) {
+    s->lane_heap_bytes = 256u << 10;
+    s->lane_recs_bytes = 2048u * (uint32_t)sizeof(Rec);
+  }
   s->dv->d_lane_heaps.alloc((size_t)s->lane_slots * 64 * s->lane_heap_bytes);
   s->dv->d_retry.alloc(std::max<size_t>(ntiles, 1));
   s->dv->d_retry2.alloc(std::max<size_t>(ntiles, 1));
@@ -615,8 +629,14 @@ void session_upload(gg_session* s) {
   s->rec_chunk = 0;
   size_t reserve = 0;
   if (s->mode != 1) {
-    size_t ch = getenv("GG_REC_CHUNK") ? (size_t)std::max(0, atoi(getenv("GG_REC_CHUNK"))) : 32;
     const size_t lane_batches = nbatches;
+    size_t ch = 32;
+    // few batches (large documents, hundreds of records per tile): chunks as large as 2 GB of
+    // reservations allows, up to 1024 records per lane
+    static constexpr size_t kSmallChunkBytes = (size_t)2 << 30;
+    if (large_docs && lane_batches && lane_batches * 64 * 32 * sizeof(Rec) < kSmallChunkBytes)
+      ch = std::min<size_t>(1024, kSmallChunkBytes / (lane_batches * 64 * sizeof(Rec)));
+    if (getenv("GG_REC_CHUNK")) ch = (size_t)std::max(0, atoi(getenv("GG_REC_CHUNK")));
     static constexpr size_t kMaxChunkBytes = (size_t)24 << 30;
     while (ch >= 8 && lane_batches * 64 * ch * sizeof(Rec) > kMaxChunkBytes) ch /= 2;
     if (ch >= 8 && lane_batches * 64 * ch < 0xC0000000ull) { s->rec_chunk = (uint32_t)ch; reserve = lane_batches * 64 * ch; }
@@ -662,7 +682,7 @@ void session_launch(gg_session* s) {
   A.rec_cursor = s->dv->d_counters.p; A.tile_cursor = s->dv->d_counters.p + 1;   // [1] lane batches, [2] wave tiles
   A.retry_count = s->dv->d_counters.p + 3;
   A.xcd_cursor = s->dv->d_counters.p + 16;
-  A.lane_heaps = s->dv->d_lane_heaps.p; A.lane_heap_bytes = s->lane_heap_bytes;
+  A.lane_heaps = s->dv->d_lane_heaps.p; A.lane_heap_bytes = s->lane_heap_bytes; A.lane_recs_bytes = s->lane_recs_bytes;
   A.retry_list = s->mode == 1 ? nullptr : s->dv->d_retry.p;
   A.wave_frames_bytes = gg_session::kWaveFrames; A.wave_recs_bytes = gg_session::kWaveRecs;
   A.retry2_list = s->dv->d_retry2.p; A.retry2_count = s->dv->d_counters.p + 4;
@@ -2022,7 +2042,7 @@ int32_t gg_session_configure(gg_session* s, int32_t mode, uint32_t lane_heap_byt
   if (mode != 0 && mode != 1) return -1;
   if (lane_heap_bytes && lane_heap_bytes < 32 * 1024) return -1;   // frames + record staging + tables
   s->mode = mode;
-  if (lane_heap_bytes) s->lane_heap_bytes = lane_heap_bytes;
+  if (lane_heap_bytes) { s->lane_heap_bytes = lane_heap_bytes; s->lane_heap_set = lane_heap_bytes; }
   s->uploaded = false;
   return 0;
 }
@@ -2417,6 +2437,20 @@ int32_t gg_session_add_docs_device(gg_session* s, const char* const* texts, cons
     if (!ensure_device(why, s->device, &s->device)) { set_err(err, -1, why); return -1; }
     if (s->docs.ndocs()) { set_err(err, 18, "IllegalArguments: the device loader fills an empty session"); return -1; }
     if (s->params) { set_note(err, "input parameters are merged by the host loader (gg_session_add_docs)"); return 1; }
+    // the device parse is one lane per document: a batch of few, large documents (Terraform plans of
+    // thousands of resources) leaves the device nearly idle -- 2048 plans parsed at 0.3 GB/s of text
+    // (profiles/r04a_bench_cfg4_lane_2048.json) against ~1 GB/s on 16 host threads -- so such a batch is
+    // refused as a whole and the caller loads it on host threads (GG_JSON_FEW_DOCS=0 keeps it on the device)
+    {
+      uint64_t total = 0;
+      for (size_t i = 0; i < n; i++) total += lens[i];
+      const bool force = getenv("GG_JSON_FEW_DOCS") && atoi(getenv("GG_JSON_FEW_DOCS")) == 0;
+      if (!force && n < (size_t)dev_ncu(s->device) * 64 && n && total / n > (64u << 10)) {
+        set_note(err, "too few documents for the lane-per-document device parse (" + std::to_string(n) + " documents of " +
+                          std::to_string(total / n) + " bytes on average): load them on host threads");
+        return 1;
+      }
+    }
     std::vector<std::string> nm(n);
     for (size_t i = 0; i < n; i++) nm[i] = names ? names[i] : std::string();
     GpuLoadStats st;

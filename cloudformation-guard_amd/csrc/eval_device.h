@@ -93,6 +93,7 @@ struct LaunchArgs {
   uint32_t* xcd_cursor;       // lane mode: one batch queue per XCD ([8])
   uint32_t lds_prog_words;    // program staging window (dynamic LDS, words; multiple of 4)
   uint32_t rec_chunk;         // lane mode: record slots per lane reserved per batch (direct writes; 0: off)
+  uint32_t lane_recs_bytes;   // lane mode: record staging bytes per lane (a multiple of 48; after the 4 KB frames)
   unsigned long long* stats;   // stats build variant: [0,8) counters, [8] tiles, [9,18) cycles per category
 };
 

@@ -154,7 +154,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
   LCtx& c = *(LCtx*)&s_ctx[lane];
   if (lane == 0) {
     g_wave.heap = heap; g_wave.nodes = A.docs.nodes; g_wave.klen = A.docs.klen; g_wave.db = A.docs.bytes;
-    g_wave.tix = A.docs.tix; g_wave.fcap = FRAMES_BYTES; g_wave.rcap = RECS_BYTES; g_wave.type_key = A.docs.type_key;
+    g_wave.tix = A.docs.tix; g_wave.fcap = FRAMES_BYTES; g_wave.rcap = A.lane_recs_bytes; g_wave.type_key = A.docs.type_key;
     g_wave.recs = A.recs; g_wave.rchunk = A.rec_chunk;
   }
   __syncthreads();
@@ -204,7 +204,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
     }
     c.rbase = rbase == NONE ? NONE : rbase + lane;
     if (active) {
-      tile_begin<true>(c, A, P, doc, heap, A.lane_heap_bytes, FRAMES_BYTES, RECS_BYTES);
+      tile_begin<true>(c, A, P, doc, heap, A.lane_heap_bytes, FRAMES_BYTES, A.lane_recs_bytes);
       c.syn_off = alloc_pers(c, 256 * 16);
       c.wbase = alloc_pers(c, WLEVELS * (uint32_t)sizeof(WLevel)); c.wdepth = 0;
       c.memo = alloc_pers(c, (P->n_slots ? P->n_slots : 1) * 4);
@@ -250,14 +250,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
       o.rec_n = nrec; o.pad0 = naux;
       if (in_chunk && n) {
         // side records follow the tile's records in its chunk
-        for (uint32_t i = 0; i < naux; i++) rec_store(c, nrec + i, stage_load(c, RECS_BYTES / (uint32_t)sizeof(Rec) - 1 - i));
+        for (uint32_t i = 0; i < naux; i++) rec_store(c, nrec + i, stage_load(c, rec_slots(c) - 1 - i));
         o.rec_off = c.rbase; o.pad1 = 1;   // slot k at rec_off + 64 k (session_fetch compacts)
       } else {
 #if GG_AB_NOREC != 1 && GG_AB_NOREC != 3   // diagnostic A/B only (2: staging off; 3: copy-out off)
         for (uint32_t i = 0; i < nrec; i++) A.recs[off + i] = rec_load(c, i);
 #endif
         for (uint32_t i = 0; i < naux; i++)
-          A.recs[off + nrec + i] = stage_load(c, RECS_BYTES / (uint32_t)sizeof(Rec) - 1 - i);
+          A.recs[off + nrec + i] = stage_load(c, rec_slots(c) - 1 - i);
         o.rec_off = n ? off : 0; o.pad1 = 0;
       }
       A.tiles[tile] = o;
