@@ -13,6 +13,7 @@
 #include <sched.h>
 
 #include <atomic>
+#include <condition_variable>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -41,8 +42,7 @@ __global__ void guard_eval_lanes_kernel(LaunchArgs A);
 __global__ void resource_type_kernel(DevBatch D);
 __global__ void shape_key_kernel(DevBatch D, const uint32_t* top8, unsigned long long* key);
 __global__ void pack_nodes_kernel(const DNode* in, DNodeP* out, uint32_t* klen, uint32_t* parent, uint64_t n, uint32_t* bad);
-__global__ void report_size_kernel(RenderArgs A);
-__global__ void report_write_kernel(RenderArgs A);
+__global__ void report_kernel(RenderArgs A, uint32_t write);
 __global__ void rec_block_sums_kernel(const TileOut* tiles, uint32_t n, uint32_t* bsum);
 __global__ void rec_scan_sums_kernel(uint32_t* bsum, uint32_t nb, uint32_t* total);
 __global__ void rec_compact_kernel(const TileOut* tiles, uint32_t n, const uint32_t* bsum, const Rec* src, Rec* dst,
@@ -147,6 +147,13 @@ struct DBuf {
     cap = count;
     if (count) HIPCHK(hipMalloc((void**)&p, count * sizeof(T)));
   }
+  // alloc with headroom: a growing buffer is reallocated rarely (hipFree synchronises the whole device,
+  // which would serialise the device reporter's overlapped render and copy-out)
+  void alloc_grow(size_t count) {
+    if (count <= cap && p) { n = count; return; }
+    alloc(count + count / 4 + 64);
+    n = count;
+  }
   void upload(const T* src, size_t count, hipStream_t s) {
     alloc(count);
     if (count) HIPCHK(hipMemcpyAsync(p, src, count * sizeof(T), hipMemcpyHostToDevice, s));
@@ -242,9 +249,13 @@ struct DeviceBufs {
   DBuf<uint32_t> d_line, d_col; // per node marks (device reporter), uploaded at its first use
   DBuf<uint8_t> d_rtab;         // device reporter tables (RProg sections, sorted rule names)
   DBuf<RProg> d_rprogs;
-  DBuf<char> d_rnames;          // the block's document names
-  DBuf<uint64_t> d_rname_off, d_rsizes, d_roffs;
-  DBuf<char> d_rtext;           // the block's rendered text
+  // per block set (two: one renders while the other is copied out): names, sizes, offsets, slots,
+  // overflow area, contiguous text
+  struct RenderSet {
+    DBuf<char> names, text;
+    DBuf<uint64_t> name_off, sizes, offs;
+  } rset[2];
+  hipStream_t copy_stream = nullptr;
   char* pinned = nullptr;       // host staging for report text (kPinnedBytes)
   static constexpr size_t kPinnedBytes = (size_t)256 << 20;
   DBuf<char> d_bytes;
@@ -277,12 +288,13 @@ struct DeviceBufs {
   ~DeviceBufs() {
     hipSetDevice(device);
     if (pinned) hipHostFree(pinned);
+    if (copy_stream) hipStreamDestroy(copy_stream);
     for (auto& pr : evq) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
     if (stream) hipStreamDestroy(stream);
   }
   size_t bytes() const {
     return d_nodes.bytes() + d_klen.bytes() + d_parent.bytes() + d_line.bytes() + d_col.bytes() + d_rtab.bytes() +
-           d_rtext.bytes() + d_bytes.bytes() + d_roots.bytes() + d_base.bytes() + d_res_map.bytes() +
+           rset[0].text.bytes() + rset[1].text.bytes() + d_bytes.bytes() + d_roots.bytes() + d_base.bytes() + d_res_map.bytes() +
            d_tix_off.bytes() + d_tix.bytes() + d_progs.bytes() + d_rx_memo.bytes() + d_heaps.bytes() + d_lane_heaps.bytes() + d_retry.bytes() +
            d_big_heaps.bytes() + d_retry2.bytes() + d_tiles.bytes() + d_rule_status.bytes() + d_recs.bytes() +
            d_recs_dense.bytes() + d_dense_off.bytes() + d_bsum.bytes() +
@@ -996,34 +1008,146 @@ void render_tables(gg_session* s) {
 // JSON FileReports of documents [first, first + count) into `sink` (each preceded by ",\n" unless it is
 // report_first, and by two spaces); the session was evaluated and fetched on its device.  false + err when
 // a document's report aborts (the host writer's Fatal; the first such document in order).
+//
+// Per block of documents (two block sets in flight): the size pass, then the write pass at the offsets;
+// a copy thread moves each block to the sink in document order -- device runs by D2H, host-writer
+// documents between them -- while the device renders the next block.
 bool device_report_json(gg_session* s, size_t first, size_t count, size_t report_first, ReportSink& sink, ReportError& err,
                         DevReportStats* stats) {
   bind_device(s);
   render_tables(s);
   hipStream_t st = s->dv->stream;
+  if (!s->dv->copy_stream) HIPCHK(hipStreamCreateWithFlags(&s->dv->copy_stream, hipStreamNonBlocking));
+  hipStream_t cst = s->dv->copy_stream;
+  const int dev = s->device;
   std::vector<const Program*> progs;
   for (auto& p : s->progs) progs.push_back(&p->prog);
   const size_t nf = progs.size();
-  size_t kBlock = getenv("GG_DREPORT_BLOCK") ? (size_t)std::max(1, atoi(getenv("GG_DREPORT_BLOCK"))) : 32768;
+  const size_t kBlock = getenv("GG_DREPORT_BLOCK") ? (size_t)std::max(1, atoi(getenv("GG_DREPORT_BLOCK"))) : 65536;
   DevReportStats local;
   DevReportStats& S = stats ? *stats : local;
-  std::vector<uint64_t> sizes, offs;
+
+  struct Block {
+    size_t d0 = 0, nb = 0;
+    std::vector<uint64_t> sizes, offs;
+    hipEvent_t done = nullptr;   // compaction finished
+  };
+  Block blk[2];
+  for (auto& b : blk) HIPCHK(hipEventCreateWithFlags(&b.done, hipEventDisableTiming));
+  // copy thread state
+  std::mutex mu;
+  std::condition_variable cv;
+  bool busy[2] = {false, false};    // set i holds a block not yet copied out
+  int queued = -1;                  // set index handed to the copy thread (-1: none)
+  bool finished = false, failed = false;
+  ReportError cerr;
+  std::exception_ptr cex;
+  std::thread copier([&]() {
+    try {
+      HIPCHK(hipSetDevice(dev));
+      for (;;) {
+        int set;
+        {
+          std::unique_lock<std::mutex> lk(mu);
+          cv.wait(lk, [&] { return queued >= 0 || finished; });
+          if (queued < 0) return;
+          set = queued;
+          queued = -1;
+        }
+        Block& b = blk[set];
+        DeviceBufs::RenderSet& R = s->dv->rset[set];
+        HIPCHK(hipEventSynchronize(b.done));
+        size_t k = 0;
+        while (k < b.nb && !failed) {
+          if (b.sizes[k] & kHostDoc) {
+            const auto h0 = std::chrono::steady_clock::now();
+            const size_t d = b.d0 + k;
+            TextBuf t;
+            if (d != report_first) t.append(",\n", 2);
+            t.append(2, ' ');
+            std::vector<TileResult> trs(nf);
+            std::vector<const TileResult*> tp(nf);
+            for (size_t f = 0; f < nf; f++) {
+              trs[f] = tile_view(s->tiles.data(), s->rule_status.data(), s->max_top, s->recs.data(), d * nf + f);
+              tp[f] = &trs[f];
+            }
+            if (!report_json_doc(s->docs, (uint32_t)d, progs, tp, t, cerr)) { failed = true; break; }
+            sink.write(t.data(), t.size());
+            S.bytes += t.size();
+            S.host_docs++;
+            S.host_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count();
+            k++;
+            continue;
+          }
+          size_t k1 = k;
+          uint64_t bytes = 0;
+          while (k1 < b.nb && !(b.sizes[k1] & kHostDoc)) { bytes += b.sizes[k1]; k1++; }
+          const auto c0 = std::chrono::steady_clock::now();
+          uint64_t at = b.offs[k];
+          while (bytes) {
+            const size_t piece = (size_t)std::min<uint64_t>(bytes, sink.max_piece());
+            HIPCHK(hipMemcpyAsync(sink.reserve(piece), R.text.p + at, piece, hipMemcpyDeviceToHost, cst));
+            HIPCHK(hipStreamSynchronize(cst));
+            sink.commit(piece);
+            at += piece; bytes -= piece; S.bytes += piece;
+          }
+          S.d2h_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - c0).count();
+          S.device_docs += k1 - k;
+          k = k1;
+        }
+        {
+          std::lock_guard<std::mutex> lk(mu);
+          busy[set] = false;
+        }
+        cv.notify_all();
+        if (getenv("GG_PROGRESS"))
+          fprintf(stderr, "[device report] %zu / %zu documents, %llu bytes\n", b.d0 + b.nb - first, count, (unsigned long long)S.bytes);
+      }
+    } catch (...) {
+      cex = std::current_exception();
+      std::lock_guard<std::mutex> lk(mu);
+      failed = true;
+      busy[0] = busy[1] = false;
+      cv.notify_all();
+    }
+  });
+  struct Join {
+    std::thread& t; std::mutex& mu; std::condition_variable& cv; bool& finished; Block* blk;
+    ~Join() {
+      { std::lock_guard<std::mutex> lk(mu); finished = true; }
+      cv.notify_all();
+      if (t.joinable()) t.join();
+      for (int i = 0; i < 2; i++) if (blk[i].done) hipEventDestroy(blk[i].done);
+    }
+  } join{copier, mu, cv, finished, blk};
+
+  hipEvent_t e0, e1;
+  HIPCHK(hipEventCreate(&e0)); HIPCHK(hipEventCreate(&e1));
+  struct EvFree { hipEvent_t a, b; ~EvFree() { hipEventDestroy(a); hipEventDestroy(b); } } evf{e0, e1};
   std::vector<char> names;
   std::vector<uint64_t> name_off;
-  hipEvent_t e0, e1, e2;
-  HIPCHK(hipEventCreate(&e0)); HIPCHK(hipEventCreate(&e1)); HIPCHK(hipEventCreate(&e2));
-  struct EvFree { hipEvent_t a, b, c; ~EvFree() { hipEventDestroy(a); hipEventDestroy(b); hipEventDestroy(c); } } evf{e0, e1, e2};
-  for (size_t d0 = first; d0 < first + count; d0 += kBlock) {
+  int set = 0;
+  for (size_t d0 = first; d0 < first + count; d0 += kBlock, set ^= 1) {
+    {
+      std::unique_lock<std::mutex> lk(mu);
+      cv.wait(lk, [&] { return (!busy[set] && queued < 0) || failed; });
+      if (failed) break;
+    }
+    Block& b = blk[set];
+    DeviceBufs::RenderSet& R = s->dv->rset[set];
     const size_t nb = std::min(kBlock, first + count - d0);
+    b.d0 = d0; b.nb = nb;
     names.clear(); name_off.assign(1, 0);
     for (size_t k = 0; k < nb; k++) {
       const std::string& nm = s->docs.names[d0 + k];
       names.insert(names.end(), nm.begin(), nm.end());
       name_off.push_back(names.size());
     }
-    s->dv->d_rnames.upload(names.data(), std::max<size_t>(names.size(), 1), st);
-    s->dv->d_rname_off.upload(name_off.data(), name_off.size(), st);
-    s->dv->d_rsizes.alloc(nb);
+    R.names.alloc_grow(std::max<size_t>(names.size(), 1));
+    HIPCHK(hipMemcpyAsync(R.names.p, names.data(), names.size(), hipMemcpyHostToDevice, st));
+    R.name_off.alloc_grow(name_off.size());
+    HIPCHK(hipMemcpyAsync(R.name_off.p, name_off.data(), name_off.size() * 8, hipMemcpyHostToDevice, st));
+    R.sizes.alloc_grow(nb);
     RenderArgs A{};
     A.nodes = s->dv->d_nodes.p; A.klen = s->dv->d_klen.p; A.pool = s->dv->d_bytes.p; A.parent = s->dv->d_parent.p;
     A.line = s->dv->d_line.p; A.col = s->dv->d_col.p; A.base = s->dv->d_base.p; A.n_nodes = s->docs.nodes.size();
@@ -1031,74 +1155,46 @@ bool device_report_json(gg_session* s, size_t first, size_t count, size_t report
     A.tiles = s->dv->d_tiles.p; A.rule_status = s->dv->d_rule_status.p; A.recs = s->dv->d_recs_dense.p; A.rec_off = s->dv->d_dense_off.p;
     A.sname_text = s->r_sname_text; A.sname = s->r_sname; A.sname_first = s->r_sname_first; A.sname_n = s->r_sname_n;
     A.sname_fk = s->r_sname_fk; A.n_sname = s->r_nsname;
-    A.doc0 = (uint32_t)d0; A.ndocs = (uint32_t)nb; A.report_first = (uint32_t)report_first;
-    A.names = s->dv->d_rnames.p; A.name_off = s->dv->d_rname_off.p; A.sizes = s->dv->d_rsizes.p;
+    A.doc0 = (uint32_t)d0; A.ndocs = (uint32_t)nb; A.report_first = (uint32_t)std::min<size_t>(report_first, 0xFFFFFFFFu);
+    A.names = R.names.p; A.name_off = R.name_off.p; A.sizes = R.sizes.p;
     const uint32_t blocks = (uint32_t)std::min<size_t>((nb + 255) / 256, (size_t)dev_ncu(s->device) * 8);
     HIPCHK(hipEventRecord(e0, st));
-    hipLaunchKernelGGL(report_size_kernel, dim3(blocks), dim3(256), 0, st, A);
+    hipLaunchKernelGGL(report_kernel, dim3(blocks), dim3(256), 0, st, A, 0u);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(e1, st));
-    sizes.resize(nb);
-    HIPCHK(hipMemcpyAsync(sizes.data(), s->dv->d_rsizes.p, nb * 8, hipMemcpyDeviceToHost, st));
+    b.sizes.resize(nb);
+    HIPCHK(hipMemcpyAsync(b.sizes.data(), R.sizes.p, nb * 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
-    float ms = 0;
-    HIPCHK(hipEventElapsedTime(&ms, e0, e1)); S.size_ms += ms;
-    offs.resize(nb);
-    uint64_t total = 0;
+    b.offs.resize(nb);
+    uint64_t dev_bytes = 0;
     for (size_t k = 0; k < nb; k++) {
-      offs[k] = total;
-      if (!(sizes[k] & kHostDoc)) total += sizes[k];
+      b.offs[k] = dev_bytes;
+      if (!(b.sizes[k] & kHostDoc)) dev_bytes += b.sizes[k];
     }
-    s->dv->d_rtext.alloc(std::max<uint64_t>(total, 1));
-    s->dv->d_roffs.upload(offs.data(), nb, st);
-    A.offsets = s->dv->d_roffs.p; A.out = s->dv->d_rtext.p;
-    HIPCHK(hipEventRecord(e1, st));
-    hipLaunchKernelGGL(report_write_kernel, dim3(blocks), dim3(256), 0, st, A);
+    R.text.alloc_grow(std::max<uint64_t>(dev_bytes, 1));
+    R.offs.alloc_grow(nb);
+    HIPCHK(hipMemcpyAsync(R.offs.p, b.offs.data(), nb * 8, hipMemcpyHostToDevice, st));
+    A.out = R.text.p; A.offsets = R.offs.p;
+    hipLaunchKernelGGL(report_kernel, dim3(blocks), dim3(256), 0, st, A, 1u);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(e2, st));
-    HIPCHK(hipStreamSynchronize(st));
-    HIPCHK(hipEventElapsedTime(&ms, e1, e2)); S.write_ms += ms;
-    // copy out in document order: runs of device documents, host documents between them
-    size_t k = 0;
-    while (k < nb) {
-      if (sizes[k] & kHostDoc) {
-        const auto h0 = std::chrono::steady_clock::now();
-        const size_t d = d0 + k;
-        TextBuf t;
-        if (d != report_first) t.append(",\n", 2);
-        t.append(2, ' ');
-        std::vector<TileResult> trs(nf);
-        std::vector<const TileResult*> tp(nf);
-        for (size_t f = 0; f < nf; f++) {
-          trs[f] = tile_view(s->tiles.data(), s->rule_status.data(), s->max_top, s->recs.data(), d * nf + f);
-          tp[f] = &trs[f];
-        }
-        if (!report_json_doc(s->docs, (uint32_t)d, progs, tp, t, err)) return false;
-        sink.write(t.data(), t.size());
-        S.bytes += t.size();
-        S.host_docs++;
-        S.host_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count();
-        k++;
-        continue;
-      }
-      size_t k1 = k;
-      uint64_t bytes = 0;
-      while (k1 < nb && !(sizes[k1] & kHostDoc)) { bytes += sizes[k1]; k1++; }
-      const auto c0 = std::chrono::steady_clock::now();
-      uint64_t at = offs[k];
-      while (bytes) {
-        const size_t piece = (size_t)std::min<uint64_t>(bytes, sink.max_piece());
-        HIPCHK(hipMemcpyAsync(sink.reserve(piece), s->dv->d_rtext.p + at, piece, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
-        sink.commit(piece);
-        at += piece; bytes -= piece; S.bytes += piece;
-      }
-      S.d2h_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - c0).count();
-      S.device_docs += k1 - k;
-      k = k1;
+    HIPCHK(hipEventRecord(e1, st));
+    HIPCHK(hipEventRecord(b.done, st));
+    HIPCHK(hipEventSynchronize(e1));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, e0, e1)); S.write_ms += ms;
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      busy[set] = true;
+      queued = set;
     }
-    if (getenv("GG_PROGRESS")) fprintf(stderr, "[device report] %zu / %zu documents, %llu bytes\n", d0 + nb - first, count, (unsigned long long)S.bytes);
+    cv.notify_all();
   }
+  {
+    // wait for the copy thread to drain both sets
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [&] { return (!busy[0] && !busy[1] && queued < 0) || failed; });
+  }
+  if (cex) std::rethrow_exception(cex);
+  if (failed) { err = cerr; return false; }
   return true;
 }
 

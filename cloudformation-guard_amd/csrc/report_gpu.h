@@ -6,8 +6,8 @@
 // (reporters/validate/structured.rs:99-133), its not_compliant ClauseReports from the failure records
 // (eval_context.rs:1965-2435 report_all_failed_clauses_for_rules / simplified_json_from_root), serde's
 // pretty layout (2-space indent, "[]" / "{}" when empty) and the message texts (Display of
-// PathAwareValue / UnResolved, display.rs:33-107).  One lane renders one document, twice: a size pass and
-// a write pass at the offsets their scan gives.  A document the device writer does not cover (a float,
+// PathAwareValue / UnResolved, display.rs:33-107).  One lane renders one document, twice: a size pass
+// and a write pass at the offsets their scan gives (pool strings read 16 bytes at a time).  A document the device writer does not cover (a float,
 // Debug-formatted reasons, map keys or count() values as values, ranges / chars, nesting past 48) is
 // flagged in the size pass and written by the host writer at its position, so the bytes never depend on
 // which writer ran.
@@ -68,8 +68,8 @@ struct RenderArgs {
   uint32_t doc0, ndocs, report_first, pad;
   const char* names;             // the block's document names, concatenated
   const uint64_t* name_off;      // [ndocs + 1]
-  uint64_t* sizes;               // size pass: bytes per document, kHostDoc for the host writer
-  const uint64_t* offsets;       // write pass: each document's offset in out
+  uint64_t* sizes;               // size pass: bytes per document, kHostDoc | reason for the host writer
+  const uint64_t* offsets;       // write pass: each device document's offset in the block's text
   char* out;
 };
 

@@ -25,20 +25,27 @@ enum : uint32_t { FB_NONE = 0, FB_FLOAT = 1, FB_DEBUG = 2, FB_REF = 3, FB_KIND =
 // i has no item yet; container i is indented base + i.  Text inside a JSON string goes through the
 // dot-bracket filter (REC_IN's message) and serde's escaping.
 struct W {
-  char* p;
-  uint64_t n;
+  char* p;          // the document's text, or null: the size pass (count only)
+  uint64_t n;       // bytes produced
   uint32_t fb;
   uint32_t depth, base;
   uint64_t first;
   bool esc, dotf, held;
 };
 
+// (every writer function is inlined into the kernels: a W passed to a real call would live in scratch and
+// every byte would become scratch traffic; the byte-level functions stay trivial so the inlined kernels
+// compile in reasonable time)
+#define RN RD
 RD void raw(W& w, char c) {
   if (w.p) w.p[w.n] = c;
   w.n++;
 }
 RD void raws(W& w, const char* s) { for (; *s; s++) raw(w, *s); }
-RD void spaces(W& w, uint32_t k) { for (uint32_t i = 0; i < k; i++) raw(w, ' '); }
+RD void spaces(W& w, uint32_t k) {
+  if (w.p) for (uint32_t i = 0; i < k; i++) w.p[w.n + i] = ' ';
+  w.n += k;
+}
 // serde_json's string escaping of one byte
 RD void esc1(W& w, unsigned char c) {
   if (c >= 0x20 && c != '"' && c != '\\') { raw(w, (char)c); return; }
@@ -57,6 +64,34 @@ RD void esc1(W& w, unsigned char c) {
     }
   }
 }
+// 8 bytes none of which serde escapes (< 0x20, '"', '\\'); bytes >= 0x80 (UTF-8) pass
+RD bool plain8(uint64_t x) {
+  const uint64_t ones = 0x0101010101010101ull, highs = 0x8080808080808080ull;
+  const uint64_t lt = (x - ones * 0x20u) & ~x & highs;
+  const uint64_t q = x ^ (ones * (uint64_t)'"'), b = x ^ (ones * (uint64_t)'\\');
+  return !(lt | ((q - ones) & ~q & highs) | ((b - ones) & ~b & highs));
+}
+// n bytes at s, escaped or not; a 16-byte aligned source (the interned string pool: strings start
+// 16-byte aligned and are zero-padded) is read 16 bytes at a time
+RD void bulk(W& w, const char* s, uint32_t n, bool escape) {
+  uint32_t i = 0;
+  if ((((uintptr_t)s) & 15u) == 0) {
+    for (; i < n; i += 16) {
+      const uint4 q = *(const uint4*)(s + i);
+      const uint64_t lo = (uint64_t)q.x | ((uint64_t)q.y << 32), hi = (uint64_t)q.z | ((uint64_t)q.w << 32);
+      const uint32_t m = n - i < 16 ? n - i : 16;
+      const bool plain = !escape || (plain8(lo) && plain8(hi));
+#pragma unroll 1
+      for (uint32_t k = 0; k < m; k++) {
+        const char c = (char)((k < 8 ? lo >> (8 * k) : hi >> (8 * (k - 8))) & 0xFF);
+        if (plain) raw(w, c); else esc1(w, (unsigned char)c);
+      }
+    }
+    return;
+  }
+#pragma unroll 1
+  for (; i < n; i++) { if (escape) esc1(w, (unsigned char)s[i]); else raw(w, s[i]); }
+}
 RD void emit(W& w, char c) { if (w.esc) esc1(w, (unsigned char)c); else raw(w, c); }
 // a text character: through the dot filter ('.' dropped before '['), then the escaping
 RD void tput(W& w, char c) {
@@ -66,9 +101,12 @@ RD void tput(W& w, char c) {
   }
   emit(w, c);
 }
-RD void tlit(W& w, const char* s) { for (; *s; s++) tput(w, *s); }
-RD void tstr(W& w, const char* s, uint32_t n) { for (uint32_t i = 0; i < n; i++) tput(w, s[i]); }
-RD void tu64(W& w, uint64_t v) {
+RN void tlit(W& w, const char* s) { for (; *s; s++) tput(w, *s); }
+RD void tstr(W& w, const char* s, uint32_t n) {
+  if (!w.dotf) { bulk(w, s, n, w.esc); return; }
+  for (uint32_t i = 0; i < n; i++) tput(w, s[i]);
+}
+RN void tu64(W& w, uint64_t v) {
   char b[24];
   int k = 0;
   do { b[k++] = (char)('0' + v % 10); v /= 10; } while (v);
@@ -84,8 +122,8 @@ RD void send(W& w) {
   w.esc = false;
   raw(w, '"');
 }
-RD void jstr(W& w, const char* s, uint32_t n) { raw(w, '"'); for (uint32_t i = 0; i < n; i++) esc1(w, (unsigned char)s[i]); raw(w, '"'); }
-RD void jlit(W& w, const char* s) { raw(w, '"'); for (; *s; s++) esc1(w, (unsigned char)*s); raw(w, '"'); }
+RD void jstr(W& w, const char* s, uint32_t n) { raw(w, '"'); bulk(w, s, n, true); raw(w, '"'); }
+RN void jlit(W& w, const char* s) { raw(w, '"'); for (; *s; s++) esc1(w, (unsigned char)*s); raw(w, '"'); }
 
 // JW (reporter.cpp): open / close / item / key
 RD void open(W& w, char c) {
@@ -111,7 +149,7 @@ RD void key(W& w, const char* k) { item(w); raw(w, '"'); raws(w, k); raw(w, '"')
 RD void jnull(W& w) { raws(w, "null"); }
 __device__ const char* const kCmp[] = {"Eq", "In", "Gt", "Lt", "Le", "Ge", "Exists", "Empty", "IsString", "IsList", "IsMap",
                                       "IsBool", "IsInt", "IsFloat", "IsNull"};
-RD void cmp(W& w, uint32_t op, bool neg) {
+RN void cmp(W& w, uint32_t op, bool neg) {
   open(w, '[');
   item(w); raw(w, '"'); raws(w, op < 15 ? kCmp[op] : "Eq"); raw(w, '"');
   item(w); raws(w, neg ? "true" : "false");
@@ -167,7 +205,7 @@ RD const char* type_info(uint32_t k) {
 }
 
 // JSON pointer of `ref` (DocBatch::path): the ancestors' keys / indices, root first
-RD void path(W& w, const Ctx& c, uint32_t ref) {
+RN void path(W& w, const Ctx& c, uint32_t ref) {
   uint32_t chain[64];
   uint32_t n = 0;
   NV v;
@@ -189,13 +227,13 @@ RD void path(W& w, const Ctx& c, uint32_t ref) {
   }
 }
 RD void loc(W& w, uint32_t l, uint32_t col) { tlit(w, "[L:"); tu64(w, l); tlit(w, ",C:"); tu64(w, col); tput(w, ']'); }
-RD void path_display(W& w, const Ctx& c, uint32_t ref) {
+RN void path_display(W& w, const Ctx& c, uint32_t ref) {
   path(w, c, ref);
   if (!w.fb) loc(w, line_of(c, ref), col_of(c, ref));
 }
 
 // serde of a value (R::value_json / write_value): pretty JSON through the JW state
-RD void write_value(W& w, const Ctx& c, uint32_t ref) {
+RN void write_value(W& w, const Ctx& c, uint32_t ref) {
   uint32_t sref[kMaxDepth], sj[kMaxDepth];
   uint32_t sp = 0;
   uint32_t cur = ref;
@@ -246,7 +284,7 @@ RD void write_value(W& w, const Ctx& c, uint32_t ref) {
 }
 
 // ValueOnlyDisplay (display.rs:33-107) into the current text
-RD void value_only(W& w, const Ctx& c, uint32_t ref) {
+RN void value_only(W& w, const Ctx& c, uint32_t ref) {
   uint32_t sref[kMaxDepth], sj[kMaxDepth];
   uint32_t sp = 0;
   uint32_t cur = ref;
@@ -302,16 +340,16 @@ RD void q_path_display(W& w, const Ctx& c, const QR& q) {
   if (qkind(q) == QR_SYNTH_INT && q.node == NONE) { tlit(w, "[L:0,C:0]"); return; }
   path_display(w, c, q.node);
 }
-RD void pav_display(W& w, const Ctx& c, const QR& q) {
+RN void pav_display(W& w, const Ctx& c, const QR& q) {
   tlit(w, "Path="); q_path_display(w, c, q);
   tlit(w, " Value=");
   if (qkind(q) == QR_SYNTH_INT) ti64(w, synth_val(q)); else value_only(w, c, q.node);
 }
-RD void unresolved_display(W& w, const Ctx& c, const QR& q) {
+RN void unresolved_display(W& w, const Ctx& c, const QR& q) {
   tlit(w, "Path="); path_display(w, c, q.node);
   tlit(w, " Value="); value_only(w, c, q.node);
 }
-RD void remaining(W& w, const Ctx& c, const QR& q) {
+RN void remaining(W& w, const Ctx& c, const QR& q) {
   const uint32_t qid = q.uref >> 12, step = q.uref & 0xFFFu;
   if (qid >= c.P->n_queries) { w.fb = FB_REF; return; }
   const uint32_t f = c.P->rem_first[qid], last = c.P->rem_first[qid + 1] - 1;   // entries: steps 0 .. nparts
@@ -319,7 +357,7 @@ RD void remaining(W& w, const Ctx& c, const QR& q) {
   tstr(w, c.P->text + r.off, r.len);
 }
 // the unresolved reasons the device writer covers (R::reason); Debug-formatted ones go to the host
-RD void reason(W& w, const Ctx& c, const QR& q) {
+RN void reason(W& w, const Ctx& c, const QR& q) {
   const uint32_t code = (q.meta >> 8) & 0xFFu;
   const uint32_t qid = q.uref >> 12, step = q.uref & 0xFFFu;
   const uint32_t cur = q.node;
@@ -373,14 +411,14 @@ RD void reason(W& w, const Ctx& c, const QR& q) {
   }
 }
 
-RD void write_pav(W& w, const Ctx& c, const QR& q) {
+RN void write_pav(W& w, const Ctx& c, const QR& q) {
   open(w, '{');
   key(w, "path"); sbeg(w); q_path(w, c, q); send(w);
   key(w, "value");
   if (qkind(q) == QR_SYNTH_INT) ti64(w, synth_val(q)); else write_value(w, c, q.node);
   close(w, '}');
 }
-RD void write_unresolved(W& w, const Ctx& c, const QR& q) {
+RN void write_unresolved(W& w, const Ctx& c, const QR& q) {
   open(w, '{');
   key(w, "traversed_to");
   open(w, '{');
@@ -432,7 +470,7 @@ RD const char* op_msg(uint32_t op, bool neg) {
 RD void custom_text(W& w, const Ctx& c, const PClause& pc) { if (pc.e != NONE) tstr_tab(w, c, c.P->msgs, pc.e); }
 
 // NotComparable reason of a REC_CMP (R::nc_reason)
-RD void nc_reason(W& w, const Ctx& c, const Rec& rc) {
+RN void nc_reason(W& w, const Ctx& c, const Rec& rc) {
   if (rc.x == NC_TYPES) {
     tlit(w, "PathAwareValues are not comparable "); tlit(w, type_info(rc.y >> 8)); tlit(w, ", "); tlit(w, type_info(rc.y & 0xFFu));
   } else if (rc.x == NC_FLOAT) {
@@ -445,7 +483,7 @@ RD void nc_reason(W& w, const Ctx& c, const Rec& rc) {
 
 // ------------------------------------------------------------------------------- records ---
 // one tile's ClauseReports (StreamWalker::items over its records), into the open not_compliant array
-RD void tile_items(W& w, const Ctx& c, const Rec* recs, uint32_t nrec) {
+RN void tile_items(W& w, const Ctx& c, const Rec* recs, uint32_t nrec) {
   uint32_t closes[kMaxDepth];
   uint32_t sp = 0;
   uint32_t i = 0;
@@ -668,7 +706,7 @@ RD void tile_items(W& w, const Ctx& c, const Rec* recs, uint32_t nrec) {
 
 // one document's FileReport (write_file_report), preceded by ",\n" after the report's first document and
 // the array's two-space indent
-RD void file_report(W& w, const RenderArgs& A, uint32_t doc) {
+RN void file_report(W& w, const RenderArgs& A, uint32_t doc) {
   const uint32_t k = doc - A.doc0;
   if (doc != A.report_first) { raw(w, ','); raw(w, '\n'); }
   spaces(w, 2);
@@ -713,23 +751,19 @@ RD void file_report(W& w, const RenderArgs& A, uint32_t doc) {
 
 }  // namespace rg
 
-// size pass: bytes of each document's text (kHostDoc | reason: the host writer takes it)
-__global__ void __launch_bounds__(256) report_size_kernel(RenderArgs A) {
+// One kernel for both passes (one instantiation of the inlined writer: it is large).  Size pass (write 0):
+// the bytes of each document of the block, or kHostDoc | reason for the host writer.  Write pass (write 1):
+// each device document at offsets[k] of the block's contiguous text.  Capped at 128 VGPRs (4 waves per
+// SIMD): the lanes wait on scattered arena loads, so resident waves matter more than registers.
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) report_kernel(RenderArgs A, uint32_t write) {
   for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < A.ndocs; k += gridDim.x * blockDim.x) {
     rg::W w{};
-    w.p = nullptr;
+    if (write) {
+      if (A.sizes[k] & kHostDoc) continue;
+      w.p = A.out + A.offsets[k];
+    }
     rg::file_report(w, A, A.doc0 + k);
-    A.sizes[k] = w.fb ? (kHostDoc | w.fb) : w.n;
-  }
-}
-
-// write pass: each device document at its offset
-__global__ void __launch_bounds__(256) report_write_kernel(RenderArgs A) {
-  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < A.ndocs; k += gridDim.x * blockDim.x) {
-    if (A.sizes[k] & kHostDoc) continue;
-    rg::W w{};
-    w.p = A.out + A.offsets[k];
-    rg::file_report(w, A, A.doc0 + k);
+    if (!write) A.sizes[k] = w.fb ? (kHostDoc | w.fb) : w.n;
   }
 }
 
