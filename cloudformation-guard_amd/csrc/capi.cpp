@@ -39,6 +39,10 @@ namespace gg {
 __global__ void guard_eval_kernel(LaunchArgs A);
 __global__ void guard_eval_verbose_kernel(LaunchArgs A);
 __global__ void guard_eval_lanes_kernel(LaunchArgs A);
+// the same kernels with the regex NFA simulation (eval_kernel_nfa.hip), for programs that need it
+__global__ void guard_eval_kernel_nfa(LaunchArgs A);
+__global__ void guard_eval_verbose_kernel_nfa(LaunchArgs A);
+__global__ void guard_eval_lanes_kernel_nfa(LaunchArgs A);
 __global__ void resource_type_kernel(DevBatch D);
 __global__ void shape_key_kernel(DevBatch D, const uint32_t* top8, unsigned long long* key);
 __global__ void pack_nodes_kernel(const DNode* in, DNodeP* out, uint32_t* klen, uint32_t* parent, uint64_t n, uint32_t* bad);
@@ -95,6 +99,7 @@ static constexpr int kMaxDevices = 64;
 struct DeviceState {
   bool ready = false;
   int ncu = 256;
+  bool big_stack = false;   // lane stack raised to 32 KB for the NFA kernel variant
 };
 struct Devices {
   std::mutex mu;
@@ -709,11 +714,22 @@ void session_launch(gg_session* s) {
   }
   s->ev0 = s->dv->evq[s->nq].first; s->ev1 = s->dv->evq[s->nq].second; s->nq++;
   HIPCHK(hipEventRecord(s->ev0, st));
+  // a regex past the DFA limits (PRegex flags bit 1) selects the kernels with the NFA simulation
+  bool nfa = false;
+  for (auto& p : s->progs)
+    for (auto& r : p->prog.regex) nfa |= r.nfa;
+  // its inlined simulation deepens the evaluator's recursive frames: give the lanes a larger stack
+  if (nfa && !g_devs.dev[s->device].big_stack) {
+    HIPCHK(hipDeviceSetLimit(hipLimitStackSize, 32768));
+    g_devs.dev[s->device].big_stack = true;
+  }
   if (s->mode != 1) {
-    hipLaunchKernelGGL(guard_eval_lanes_kernel, dim3(s->lane_slots), dim3(64), A.lds_prog_words * 4, st, A);
+    hipLaunchKernelGGL(nfa ? guard_eval_lanes_kernel_nfa : guard_eval_lanes_kernel, dim3(s->lane_slots), dim3(64),
+                       A.lds_prog_words * 4, st, A);
     HIPCHK(hipGetLastError());
   }
-  auto wave_kernel = s->verbose ? guard_eval_verbose_kernel : guard_eval_kernel;
+  auto wave_kernel = s->verbose ? (nfa ? guard_eval_verbose_kernel_nfa : guard_eval_verbose_kernel)
+                                : (nfa ? guard_eval_kernel_nfa : guard_eval_kernel);
   hipLaunchKernelGGL(wave_kernel, dim3(s->nslots), dim3(64), A.lds_prog_words * 4, st, A);
   HIPCHK(hipGetLastError());
   if (s->dv->d_big_heaps.p) {
@@ -1026,6 +1042,10 @@ bool device_report_json(gg_session* s, size_t first, size_t count, size_t report
   const size_t kBlock = getenv("GG_DREPORT_BLOCK") ? (size_t)std::max(1, atoi(getenv("GG_DREPORT_BLOCK"))) : 65536;
   DevReportStats local;
   DevReportStats& S = stats ? *stats : local;
+  // GG_DREPORT_TRACE=1: per-block wall-clock spans of the render and the copy-out on stderr (overlap check)
+  const bool trace = getenv("GG_DREPORT_TRACE") != nullptr;
+  const auto t0 = std::chrono::steady_clock::now();
+  auto since = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
 
   struct Block {
     size_t d0 = 0, nb = 0;
@@ -1054,9 +1074,12 @@ bool device_report_json(gg_session* s, size_t first, size_t count, size_t report
           set = queued;
           queued = -1;
         }
+        cv.notify_all();   // the render loop waits for the hand-off slot to empty
         Block& b = blk[set];
         DeviceBufs::RenderSet& R = s->dv->rset[set];
+        const double cw = since();
         HIPCHK(hipEventSynchronize(b.done));
+        const double cb = since();
         size_t k = 0;
         while (k < b.nb && !failed) {
           if (b.sizes[k] & kHostDoc) {
@@ -1100,6 +1123,7 @@ bool device_report_json(gg_session* s, size_t first, size_t count, size_t report
           busy[set] = false;
         }
         cv.notify_all();
+        if (trace) fprintf(stderr, "[dreport] copy  set %d docs %zu: queued %.1f start %.1f end %.1f ms\n", set, b.d0, cw, cb, since());
         if (getenv("GG_PROGRESS"))
           fprintf(stderr, "[device report] %zu / %zu documents, %llu bytes\n", b.d0 + b.nb - first, count, (unsigned long long)S.bytes);
       }
@@ -1136,6 +1160,7 @@ bool device_report_json(gg_session* s, size_t first, size_t count, size_t report
     Block& b = blk[set];
     DeviceBufs::RenderSet& R = s->dv->rset[set];
     const size_t nb = std::min(kBlock, first + count - d0);
+    const double rb = since();
     b.d0 = d0; b.nb = nb;
     names.clear(); name_off.assign(1, 0);
     for (size_t k = 0; k < nb; k++) {
@@ -1181,6 +1206,7 @@ bool device_report_json(gg_session* s, size_t first, size_t count, size_t report
     HIPCHK(hipEventSynchronize(e1));
     float ms = 0;
     HIPCHK(hipEventElapsedTime(&ms, e0, e1)); S.write_ms += ms;
+    if (trace) fprintf(stderr, "[dreport] render set %d docs %zu: start %.1f end %.1f ms (kernels %.1f ms)\n", set, d0, rb, since(), ms);
     {
       std::lock_guard<std::mutex> lk(mu);
       busy[set] = true;
@@ -2427,7 +2453,7 @@ int32_t gg_parse_f64(const char* s, size_t n, double* out) {
 
 int32_t gg_regex_match(const char* pattern, const char* text, size_t len, uint32_t* stats) {
   CompiledRegex rx = compile_regex(pattern ? pattern : "");
-  if (stats) { stats[0] = rx.nstates; stats[1] = rx.ncls; }
+  if (stats) { stats[0] = rx.nstates | (rx.nfa ? 0x80000000u : 0u); stats[1] = rx.ncls; }
   if (!rx.valid) return -2;
   return dfa_match(rx, text ? text : "", text ? len : 0);
 }

@@ -90,7 +90,18 @@ struct Compiler {
     pr.nstates = cr.nstates;
     pr.start = cr.start;
     pr.ncls = cr.ncls;
-    pr.flags = (cr.unsupported ? 1u : 0u) | ((uint32_t)cr.bounds.size() << 8);
+    pr.flags = (cr.unsupported ? 1u : 0u) | (cr.nfa ? 2u : 0u) | ((uint32_t)cr.bounds.size() << 8);
+    if (cr.nfa) {   // the NFA simulation's u32 tables (regex_dfa.h kNfa*), 4-B aligned in the u16 section
+      while (dfa.size() & 1) dfa.push_back(0);
+      pr.table = (uint32_t)dfa.size();
+      for (uint32_t w : cr.nfa_tab) { dfa.push_back((uint16_t)(w & 0xFFFFu)); dfa.push_back((uint16_t)(w >> 16)); }
+      regexes.push_back(pr);
+      P.regex.push_back(cr);
+      P.regex_src.push_back(src);
+      const uint32_t id = (uint32_t)regexes.size() - 1;
+      regex_ids[src] = id;
+      return id;
+    }
     pr.table = (uint32_t)dfa.size();
     for (uint16_t t : cr.table) dfa.push_back(t);
     pr.accept = (uint32_t)dfa.size();

@@ -22,6 +22,16 @@
 
 #define DEV __device__ __attribute__((always_inline)) inline
 #define DEVN __device__ __attribute__((noinline))
+// GG_NFA 1 (eval_kernel_nfa.hip): the evaluator kernels again, with the regex NFA simulation compiled in
+// and the names suffixed _nfa; the shared helper kernels are built once, by the GG_NFA 0 unit.
+#ifndef GG_NFA
+#define GG_NFA 0
+#endif
+#if GG_NFA
+#define GG_KN(x) x##_nfa
+#else
+#define GG_KN(x) x
+#endif
 #ifndef GG_STEAL
 #define GG_STEAL 1   // cross-XCD batch stealing at the end of a launch (profiles/r02_ab_inline.log)
 #endif
@@ -135,7 +145,7 @@ __device__ __attribute__((always_inline)) inline void tile_stats(CtxT& c, const 
 // program over different documents.  Records are published with one atomic per wave (wave
 // prefix sum).  Tiles that outgrow the 64 KB lane heap (heap, record staging or frame limits)
 // are queued for the wave-mode kernel below instead of failing.
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE_WAVES_PER_EU))) guard_eval_lanes_kernel(LaunchArgs A) {
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE_WAVES_PER_EU))) GG_KN(guard_eval_lanes_kernel)(LaunchArgs A) {
   using namespace ln;
   const uint32_t lane = __lane_id();
   // 64 lanes share one interleaved region (see haddr in eval_core.inc)
@@ -268,7 +278,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
 // Wave mode: one wavefront per tile, all 64 lanes in lock-step (map lookups are wave-parallel),
 // 512 KB heap per wave.  Runs the tiles the lane kernel queued (A.retry_list), or every tile
 // when A.retry_list is null.
-__global__ void __launch_bounds__(64) guard_eval_kernel(LaunchArgs A) {
+__global__ void __launch_bounds__(64) GG_KN(guard_eval_kernel)(LaunchArgs A) {
   using namespace wv;
 #include "wave_tile_loop.inc"
 }
@@ -276,13 +286,14 @@ __global__ void __launch_bounds__(64) guard_eval_kernel(LaunchArgs A) {
 // guard-ffi run_checks(verbose = true): the same wave-mode evaluation recording every event of the
 // reference's EventRecord tree (eval_core.inc, GG_VERBOSE); the host renders it (reporter.cpp
 // verbose_tree).  Launched only for verbose requests, so the two kernels above keep no trace of it.
-__global__ void __launch_bounds__(64) guard_eval_verbose_kernel(LaunchArgs A) {
+__global__ void __launch_bounds__(64) GG_KN(guard_eval_verbose_kernel)(LaunchArgs A) {
   using namespace vb;
 #include "wave_tile_loop.inc"
 }
 
 }  // namespace gg
 
+#if !GG_NFA
 namespace gg {
 
 // Resource-type column (DevBatch::tix): one wavefront per document, lanes over the entries of the
@@ -454,3 +465,4 @@ __global__ void __launch_bounds__(256) pack_nodes_kernel(const DNode* in, DNodeP
 }
 
 }  // namespace gg
+#endif  // !GG_NFA

@@ -115,7 +115,19 @@ struct PParamRule { uint32_t rule, first_param, nparams, pad; }; // params: var 
 // 1 = match decided, 2 = match at the end of the haystack), the ASCII class map at `ascii` (128
 // bytes) and, at `bounds`, flags >> 8 u32 words (first code point << 8 | class) sorted by code point
 // for the classes above U+007F.  flags bit 0: unsupported on the MI355X path.
+// flags: bit 0 unsupported, bit 1 NFA simulation (table = its u32 tables, kNfa* layout), bits 8.. class runs
 struct PRegex { uint32_t table, nstates, start, flags, ncls, accept, ascii, bounds; };
+
+// nfa_tab layout (u32 words): header [kNfaM] states m, [kNfaW] words per bitset W = ceil(m / 32),
+// [kNfaCls] classes, [kNfaNb] class runs above U+007F, [kNfaStartFlags] / [kNfaAgainFlags] flags of S0 / Z;
+// then S0[W] (closure of the start state at offset 0), Z[W] (its closure elsewhere: the unanchored
+// restart), FL[m] (flags of each state's follow set), F[m][W] (follow set of each state: the closure of
+// its successor), M[ncls][W] (states whose class set holds the class), ascii[128] (class per ASCII code
+// point), runs[nb][2] (first code point, class).  Flags: 1 = the match state is in the set, 2 = an
+// end-of-text assertion is (a match if the haystack ends here).
+enum : uint32_t { kNfaM = 0, kNfaW = 1, kNfaCls = 2, kNfaNb = 3, kNfaStartFlags = 4, kNfaAgainFlags = 5, kNfaHdr = 8,
+                  kNfaMaxStates = 1024, kNfaMaxWords = kNfaMaxStates / 32 };
+
 
 enum FuncName : uint32_t { F_COUNT = 0, F_OTHER = 1 };
 

@@ -506,6 +506,67 @@ struct VecHash {
   }
 };
 
+
+// The NFA simulation for a regex whose DFA exceeds the limits (CompiledRegex::nfa; layout in regex_dfa.h).
+// Only class-set states (type 0) carry bits: the live set after a character is the union of the follow
+// sets F[s] of the live states whose class set holds it, plus Z (a match may start at every offset) --
+// the same sets the subset construction interns, unioned per step instead of tabulated.  Word assertions
+// would need the previous character's kind in every closure; such a regex stays refused.
+CompiledRegex& nfa_fallback(CompiledRegex& out, const Nfa& nfa, int nstart, uint32_t ncls0,
+                            const std::vector<std::pair<uint32_t, uint32_t>>& ivals, bool has_word, const char* why) {
+  auto refuse = [&](std::string w) -> CompiledRegex& { out.unsupported = true; out.why = std::move(w); return out; };
+  if (has_word) return refuse(std::string(why) + " (with word assertions)");
+  std::vector<int> bit(nfa.s.size(), -1), setst;
+  for (size_t k = 0; k < nfa.s.size(); k++) if (nfa.s[k].type == 0) { bit[k] = (int)setst.size(); setst.push_back((int)k); }
+  const uint32_t m = (uint32_t)setst.size();
+  if (m > kNfaMaxStates) return refuse(std::string(why) + "; NFA too large");
+  const uint32_t W = m ? (m + 31) / 32 : 1;
+  uint32_t nb = 0;
+  for (size_t k = 0; k < ivals.size(); k++)
+    if (ivals[k].first >= 128 && (k == 0 || ivals[k - 1].first < 128 || ivals[k - 1].second != ivals[k].second)) nb++;
+  const size_t words = kNfaHdr + 2 * (size_t)W + m + (size_t)m * W + (size_t)ncls0 * W + 128 + 2 * (size_t)nb;
+  if (words > (1u << 20)) return refuse(std::string(why) + "; NFA tables too large");
+  std::vector<uint32_t>& T = out.nfa_tab;
+  T.assign(words, 0);
+  T[kNfaM] = m; T[kNfaW] = W; T[kNfaCls] = ncls0; T[kNfaNb] = nb;
+  const size_t oS0 = kNfaHdr, oZ = oS0 + W, oFL = oZ + W, oF = oFL + m, oM = oF + (size_t)m * W, oA = oM + (size_t)ncls0 * W,
+               oB = oA + 128;
+  std::vector<uint8_t> mark(nfa.s.size(), 0);
+  // a closure as (bitset at `at`, flags)
+  auto put = [&](std::vector<int> st, bool at_start, size_t at) -> uint32_t {
+    closure(nfa, st, mark, at_start);
+    uint32_t fl = 0;
+    for (int x : st) {
+      const int t = nfa.s[x].type;
+      if (t == 0) T[at + bit[x] / 32] |= 1u << (bit[x] % 32);
+      else if (t == 2) fl |= 1;
+      else if (t == 5) fl |= 2;
+    }
+    return fl;
+  };
+  T[kNfaStartFlags] = put({nstart}, true, oS0);
+  T[kNfaAgainFlags] = put({nstart}, false, oZ);
+  for (uint32_t j = 0; j < m; j++) {
+    const NState& s = nfa.s[setst[j]];
+    T[oFL + j] = s.out >= 0 ? put({s.out}, false, oF + (size_t)j * W) : 0;
+  }
+  for (uint32_t c = 0; c < ncls0; c++)
+    for (uint32_t j = 0; j < m; j++)
+      if (nfa.csets[nfa.s[setst[j]].cset][c]) T[oM + (size_t)c * W + j / 32] |= 1u << (j % 32);
+  size_t r = 0;
+  for (size_t k = 0; k < ivals.size(); k++) {
+    if (ivals[k].first < 128) { T[oA + ivals[k].first] = ivals[k].second; continue; }
+    if (k == 0 || ivals[k - 1].first < 128 || ivals[k - 1].second != ivals[k].second) {
+      T[oB + 2 * r] = ivals[k].first; T[oB + 2 * r + 1] = ivals[k].second; r++;
+    }
+  }
+  out.nfa = true;
+  out.nstates = m;
+  out.ncls = ncls0;
+  out.why = why;
+  return out;
+}
+
 }  // namespace
 
 uint32_t regex_class_of(const CompiledRegex& rx, uint32_t cp) {
@@ -564,7 +625,6 @@ CompiledRegex compile_regex(const std::string& pattern) {
     ivals.push_back({lo, it->second});
   }
   const uint32_t ncls0 = (uint32_t)cls_sig.size();
-  if (ncls0 > 250) { out.unsupported = true; out.why = "too many character classes"; return out; }
   Nfa nfa;
   std::map<const RNode*, int> cset_of;
   for (size_t j = 0; j < sets_n.size(); j++) {
@@ -578,6 +638,7 @@ CompiledRegex compile_regex(const std::string& pattern) {
   int m = nfa.add(2);
   b.patch(f, m);
   const int nstart = f.start;
+  if (ncls0 > 250) return nfa_fallback(out, nfa, nstart, ncls0, ivals, ps.has_word, "too many character classes");
 
   // ---- subset construction over the classes (state 0 = dead)
   // With word assertions (regex-automata's look-behind state) a DFA state is (NFA states closed up to the
@@ -622,7 +683,7 @@ CompiledRegex compile_regex(const std::string& pattern) {
   std::vector<std::vector<uint32_t>> table(1, std::vector<uint32_t>(ncls0, 0));
   std::vector<int> here, ex;
   for (size_t cur = 1; cur < sets.size(); cur++) {
-    if (sets.size() > 4000) { out.unsupported = true; out.why = "DFA too large"; return out; }
+    if (sets.size() > 4000) return nfa_fallback(out, nfa, nstart, ncls0, ivals, hw, "DFA too large");
     bool pw, at0, sk;
     parts(sets[cur], here, pw, at0, sk);
     std::vector<uint32_t> row(ncls0);
@@ -719,8 +780,51 @@ CompiledRegex compile_regex(const std::string& pattern) {
   return out;
 }
 
+// host restatement of the device nfa_run (eval_core.inc)
+int nfa_match(const CompiledRegex& rx, const char* s, size_t n) {
+  const uint32_t* T = rx.nfa_tab.data();
+  const uint32_t m = T[kNfaM], W = T[kNfaW], ncls = T[kNfaCls], nb = T[kNfaNb];
+  const uint32_t *S0 = T + kNfaHdr, *Z = S0 + W, *FL = Z + W, *F = FL + m, *M = F + (size_t)m * W, *A = M + (size_t)ncls * W,
+                 *B = A + 128;
+  uint32_t cur[kNfaMaxWords], nx[kNfaMaxWords];
+  for (uint32_t w = 0; w < W; w++) cur[w] = S0[w];
+  uint32_t cf = T[kNfaStartFlags];
+  if (cf & 1) return 1;
+  uint32_t cp = 0, need = 0;
+  for (size_t k = 0; k < n; k++) {
+    const uint8_t by = (uint8_t)s[k];
+    if (by < 0x80) { cp = by; need = 0; }
+    else if (by >= 0xC0) { need = by >= 0xF0 ? 3 : by >= 0xE0 ? 2 : 1; cp = by & (0x3Fu >> need); continue; }
+    else { cp = (cp << 6) | (by & 0x3Fu); if (--need) continue; }
+    uint32_t cls;
+    if (cp < 128) cls = A[cp];
+    else {
+      uint32_t lo = 0, hi = nb;
+      while (hi - lo > 1) { const uint32_t md = (lo + hi) / 2; if (B[2 * md] <= cp) lo = md; else hi = md; }
+      cls = B[2 * lo + 1];
+    }
+    uint32_t nf = T[kNfaAgainFlags];
+    for (uint32_t w = 0; w < W; w++) nx[w] = Z[w];
+    for (uint32_t w = 0; w < W; w++) {
+      uint32_t x = cur[w] & M[(size_t)cls * W + w];
+      while (x) {
+        const uint32_t j = w * 32 + (uint32_t)__builtin_ctz(x);
+        x &= x - 1;
+        nf |= FL[j];
+        const uint32_t* f = F + (size_t)j * W;
+        for (uint32_t v = 0; v < W; v++) nx[v] |= f[v];
+      }
+    }
+    if (nf & 1) return 1;
+    for (uint32_t w = 0; w < W; w++) cur[w] = nx[w];
+    cf = nf;
+  }
+  return (cf & 2) ? 1 : 0;
+}
+
 int dfa_match(const CompiledRegex& rx, const char* s, size_t n) {
   if (!rx.valid || rx.unsupported) return -1;
+  if (rx.nfa) return nfa_match(rx, s, n);
   uint32_t st = rx.start;
   if (rx.accept[st] & 1) return 1;
   uint32_t cp = 0, need = 0;

@@ -15,6 +15,8 @@
 #include <string>
 #include <vector>
 
+#include "guard_types.h"
+
 namespace gg {
 
 struct CompiledRegex {
@@ -27,6 +29,11 @@ struct CompiledRegex {
   std::vector<std::pair<uint32_t, uint32_t>> bounds;   // (first code point, class) runs above U+007F
   std::vector<uint16_t> table;   // nstates * ncls
   std::vector<uint8_t> accept;   // nstates: 1 = match (decided), 2 = match if the haystack ends here
+  // No DFA within the limits (more than 4000 states or 250 classes): the epsilon-free NFA is simulated
+  // instead, one bitset of live states stepped per character (nfa_match, device nfa_run).  nstates / ncls
+  // then count NFA states / classes; table, accept, ascii, bounds are unused.  Layout: guard_types.h kNfa*.
+  bool nfa = false;
+  std::vector<uint32_t> nfa_tab;
   std::string why;
 };
 

@@ -193,7 +193,14 @@ def regex_match(pattern, text):
     b = _b(text)
     st = (ctypes.c_uint32 * 2)()
     rc = lib().gg_regex_match(_b(pattern), b, len(b), st)
-    return rc, st[0], st[1]
+    return rc, st[0] & 0x7FFFFFFF, st[1]
+
+
+def regex_engine(pattern):
+    """'dfa', or 'nfa' when the regex's DFA exceeds the compile limits and it runs as the NFA simulation."""
+    st = (ctypes.c_uint32 * 2)()
+    lib().gg_regex_match(_b(pattern), b"", 0, st)
+    return "nfa" if st[0] & 0x80000000 else "dfa"
 
 
 def load_dump(text, mode=0):

@@ -226,7 +226,8 @@ int32_t gg_parse_rules(const char *text, const char *name, extern_err_t *err);
 int32_t gg_program_stats(const char *text, const char *name, uint32_t *out);
 /* The rule-regex DFA (compiled as for a rules file) run on the host over one haystack: 1 match,
  * 0 no match, -1 unsupported on the MI355X path (look-around, back-references, ...), -2 invalid.
- * stats (may be NULL, 2 values): DFA states, byte classes. */
+ * stats (may be NULL, 2 values): DFA states, code-point classes; bit 31 of stats[0] set when the regex
+ * has no DFA within the limits and runs as the NFA simulation (then NFA states). */
 int32_t gg_regex_match(const char *pattern, const char *text, size_t len, uint32_t *stats);
 
 /* Synthetic CloudFormation corpus (BASELINE configs[1]); byte-identical to synth.py cfn_doc. */

@@ -299,6 +299,48 @@ def test_word_boundary_regex_pack_vs_oracle():
     s.close()
 
 
+def _nfa_docs():
+    import random
+    r = random.Random(5150)
+    cjk = "".join(chr(0x4E00 + 3 * k) for k in range(260))
+    docs = []
+    for i in range(80):
+        res = {}
+        for k in range(3):
+            n = r.choice([5, 12, 13, 14, 16, 25])
+            code = r.choice(["", "c", "q"]) + "".join(r.choice("ab") for _ in range(n))
+            props = {"Code": code}
+            if r.random() < 0.7:
+                m = r.choice([1, 2, 3, 6])
+                lab = "".join(r.choice(cjk) for _ in range(m))
+                props["Label"] = r.choice([lab, "x" + lab + "y", lab + "!", "ab" + lab])
+            res["r%d" % k] = {"Type": "AWS::S3::Bucket", "Properties": props}
+        docs.append(json.dumps({"Resources": res}, ensure_ascii=False))
+    return docs
+
+
+def test_nfa_regex_pack_vs_oracle():
+    """regexes past the DFA limits run as the NFA simulation on the device (tests/golden/nfa_rulepack):
+    byte-identical with the oracle in every format, lane and wave kernels, memo on and off"""
+    p = os.path.join(G, "nfa_rulepack")
+    rules = [(f, open(os.path.join(p, f)).read()) for f in sorted(os.listdir(p)) if f.endswith(".guard")]
+    data = [("n%d.json" % i, d) for i, d in enumerate(_nfa_docs())]
+    for fmt in ("json", "sarif"):
+        exp, ecode, _ = oracle_validate(rules, data, output=fmt)
+        out, code = guard_amd.validate_structured(rules, data, output=fmt)
+        assert (code, out) == (ecode, exp), fmt
+    exp, ecode, _ = oracle_validate(rules, data)
+    for mode in (1, 0):
+        s = guard_amd.Session()
+        s.configure(mode, 0)
+        for name, text in rules:
+            s.add_rules(text, name)
+        s.add_docs([t for _, t in data], [n for n, _ in data])
+        s.eval(1)
+        assert s.report("json") == (exp, ecode), mode
+        s.close()
+
+
 def test_app_b13_unicode_digit_class_on_gpu():
     rules = [("d.guard", "a == /^\\d+$/")]
     out, code = guard_amd.validate_structured(rules, [("d.json", '{"a": "١٢٣"}')])

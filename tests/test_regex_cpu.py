@@ -63,3 +63,47 @@ def test_app_b13_unicode_digits():
     # regex classes are Unicode, `/^\d+$/` matches "١٢٣"
     assert guard_amd.regex_match(r"^\d+$", "١٢٣")[0] == 1
     assert rxcompat.is_match(r"^\d+$", "١٢٣")
+
+
+# Regexes whose DFA exceeds the compile limits (4000 states / 250 classes) run as the NFA simulation
+# (regex_dfa.cpp nfa_fallback, device eval_core.inc nfa_run); the host nfa_match restates the device loop.
+_CJK = "".join(chr(0x4E00 + 3 * k) for k in range(260))
+NFA_PATTERNS = [
+    r"(a|b)*a(a|b){12}", r"^(a|b)*a(a|b){12}$", r"(a|b)*a(a|b){12}$", r"^(a|b)*a(a|b){12}",
+    r"(a|b)*a(a|b){12}c", r"x(a|b)*a(a|b){13}|^q", r"(?i)(a|b)*a(a|b){12}",
+    "^(" + "|".join(_CJK) + ")+$", "x(" + "|".join(_CJK) + "){2}y", "(" + "|".join(_CJK[:255]) + ")$",
+    "[" + _CJK + "]" + "|zz(a|b)*a(a|b){12}",
+]
+
+
+def _nfa_haystacks():
+    import random
+    r = random.Random(77)
+    hs = ["", "a", "b", "c", "q", "x", "y", "zz"]
+    for n in (12, 13, 14, 15, 20, 40):
+        for _ in range(12):
+            hs.append("".join(r.choice("ab") for _ in range(n)))
+            hs.append(r.choice(["", "x", "q", "zz"]) + "".join(r.choice("ab") for _ in range(n)) + r.choice(["", "c", "y"]))
+    for n in (1, 2, 3, 5):
+        for _ in range(10):
+            hs.append("".join(r.choice(_CJK + "ab") for _ in range(n)))
+            hs.append("x" + "".join(r.choice(_CJK) for _ in range(n)) + "y")
+    hs += ["A" * 13, "a" + "B" * 12, "é" + "a" * 13, "日本語", _CJK, _CJK[:2], "\U0001F600" + "a" * 13]
+    return hs
+
+
+@pytest.mark.parametrize("pattern", NFA_PATTERNS)
+def test_nfa_fallback_matches_oracle(pattern):
+    assert rxcompat.is_valid(pattern) and not rxcompat.fancy_only(pattern)
+    assert guard_amd.regex_engine(pattern) == "nfa", pattern
+    bad = [(h, rc) for h in _nfa_haystacks()
+           for rc in [guard_amd.regex_match(pattern, h)[0]] if rc != int(rxcompat.is_match(pattern, h))]
+    assert not bad, (pattern, bad[:5])
+
+
+def test_nfa_fallback_limits():
+    # small regexes keep the DFA; a word assertion in a too-large regex stays refused (-1), never approximated
+    assert guard_amd.regex_engine(r"(a|b)*a(a|b){3}") == "dfa"
+    assert guard_amd.regex_match(r"\b(a|b)*a(a|b){12}\b", "ab")[0] == -1
+    # more than 1024 NFA states: refused
+    assert guard_amd.regex_match(r"(a|b)*a(a|b){1100}", "ab")[0] == -1
