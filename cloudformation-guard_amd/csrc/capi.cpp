@@ -45,6 +45,8 @@ __global__ void guard_eval_verbose_kernel_nfa(LaunchArgs A);
 __global__ void guard_eval_lanes_kernel_nfa(LaunchArgs A);
 __global__ void resource_type_kernel(DevBatch D);
 __global__ void shape_key_kernel(DevBatch D, const uint32_t* top8, unsigned long long* key);
+__global__ void root_resources_kernel(const DNode* nodes, const uint64_t* base, const uint32_t* roots, uint32_t nd, uint32_t rkey,
+                                      uint32_t* rmap, uint32_t* cnt);
 __global__ void pack_nodes_kernel(const DNode* in, DNodeP* out, uint32_t* klen, uint32_t* parent, uint64_t n, uint32_t* bad);
 __global__ void report_kernel(RenderArgs A, uint32_t write);
 __global__ void rec_block_sums_kernel(const TileOut* tiles, uint32_t n, uint32_t* bsum);
@@ -356,6 +358,11 @@ struct gg_session {
   // arena from it instead of sending the nodes over PCIe again, then frees it
   void* dev_nodes = nullptr;
   size_t dev_nodes_n = 0;
+  // device-resident arena (gpu_load_json ResidentArena): docs.nodes / line / col / kline / kcol are
+  // empty on the host and live in HBM (dev_nodes, resident.*) until a host consumer needs them
+  // (ensure_host_arena); dev_nodes then outlives the upload
+  ResidentArena resident;
+  std::mutex arena_mu;
   unsigned long long* ext_counts = nullptr;   // caller-owned device tally buffer (RCCL all-reduce)
   bool launched = false;
   std::vector<unsigned long long> counts;
@@ -401,6 +408,7 @@ struct gg_session {
     if (dv && stream) hipStreamSynchronize(stream);
     release_bufs(dv);
     if (dev_nodes) { if (device >= 0) hipSetDevice(device); hipFree(dev_nodes); }
+    for (uint32_t* p : {resident.line, resident.col, resident.kline, resident.kcol}) if (p) hipFree(p);
   }
 };
 
@@ -424,14 +432,46 @@ void bind_device(gg_session* s) {
   if (!ensure_device(why, s->device, &s->device)) throw std::runtime_error(why);
 }
 
+// arena nodes of the session's documents, on the host or resident in HBM
+size_t arena_nodes(const gg_session* s) { return s->resident.nodes ? (size_t)s->resident.nodes : s->docs.nodes.size(); }
+
+// Copies a device-resident arena's columns down to the host batch (the host writers, tile errors, host
+// loads appended to the session need them); a no-op once they are there.  Thread-safe per session.
+void ensure_host_arena(gg_session* s) {
+  std::lock_guard<std::mutex> lk(s->arena_mu);
+  if (!s->resident.nodes) return;
+  bind_device(s);
+  const size_t N = s->resident.nodes;
+  if (!s->dev_nodes || s->dev_nodes_n != N) throw std::runtime_error("resident arena: its node copy is gone");
+  DocBatch& D = s->docs;
+  std::thread a([&]() { D.nodes.resize(N); });
+  std::thread b([&]() { D.line.resize(N); D.col.resize(N); });
+  D.kline.resize(N); D.kcol.resize(N);
+  a.join(); b.join();
+  HIPCHK(hipMemcpy(D.nodes.data(), s->dev_nodes, N * sizeof(DNode), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(D.line.data(), s->resident.line, N * 4, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(D.col.data(), s->resident.col, N * 4, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(D.kline.data(), s->resident.kline, N * 4, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(D.kcol.data(), s->resident.kcol, N * 4, hipMemcpyDeviceToHost));
+  for (uint32_t* p : {s->resident.line, s->resident.col, s->resident.kline, s->resident.kcol}) hipFree(p);
+  s->resident = ResidentArena{};
+  // the upload packed its arena already: the unpacked copy is no longer needed
+  if (s->uploaded) { hipFree(s->dev_nodes); s->dev_nodes = nullptr; s->dev_nodes_n = 0; }
+}
+
 void session_upload(gg_session* s) {
   bind_device(s);
+  const bool trace = getenv("GG_LOAD_TRACE") != nullptr;
+  const auto tu = std::chrono::steady_clock::now();
+  auto mark = [&](const char* what) {
+    if (trace) fprintf(stderr, "[upload] %-22s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tu).count());
+  };
   if (s->dv && s->dv->device != s->device) { release_bufs(s->dv); s->dv = nullptr; HIPCHK(hipSetDevice(s->device)); }
   if (!s->dv) s->dv = acquire_bufs(s->device);
   hipStream_t st = s->dv->stream;
   {
     // host arena (32 B nodes) -> device arena (16 B packed nodes + key-length column)
-    const size_t n = s->docs.nodes.size();
+    const size_t n = arena_nodes(s);
     // lane-mode tiles address their document by a 32-bit global node index (eval_core.inc Ctx)
     if (n >= 0xFFFFFFFFull) throw std::runtime_error("batch too large for one session: split it (>= 2^32 arena nodes)");
     DBuf<DNode> tmp;
@@ -470,9 +510,10 @@ void session_upload(gg_session* s) {
     uint32_t b = 0;
     HIPCHK(hipMemcpyAsync(&b, bad.p, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
-    if (s->dev_nodes) { hipFree(s->dev_nodes); s->dev_nodes = nullptr; s->dev_nodes_n = 0; }
+    if (s->dev_nodes && !s->resident.nodes) { hipFree(s->dev_nodes); s->dev_nodes = nullptr; s->dev_nodes_n = 0; }
     if (b & 1u) throw std::runtime_error("a string or container is too large for the device arena (count >= 2^28)");
     if (b & 2u) throw std::runtime_error("arena invariant broken: a map entry's key offset is not its key id");
+    mark("packed");
   }
   s->dv->d_bytes.upload(s->docs.bytes.data(), s->docs.bytes.size() ? s->docs.bytes.size() : 1, st);
   s->dv->d_roots.upload(s->docs.roots.data(), s->docs.roots.size(), st);
@@ -485,7 +526,31 @@ void session_upload(gg_session* s) {
     size_t nd = D.ndocs();
     std::vector<uint32_t> rmap(nd, NONE), toff(nd, 0);
     size_t total = 0;
-    if (rkey != NONE && s->type_key != NONE) {
+    // a resident arena: the first documents' nodes (the type-frequency sample below) come down, and the
+    // root scan runs on the device (root_resources_kernel, json_gpu.hip)
+    std::vector<DNode> sample;
+    const DNode* HN = D.nodes.data();
+    const size_t nsample = std::min<size_t>(nd, 4096);
+    if (s->resident.nodes && nd) {
+      const size_t sn = nsample < nd ? (size_t)D.base[nsample] : (size_t)s->resident.nodes;
+      sample.resize(std::max<size_t>(sn, 1));
+      HIPCHK(hipMemcpyAsync(sample.data(), s->dev_nodes, sn * sizeof(DNode), hipMemcpyDeviceToHost, st));
+      HN = sample.data();
+      if (rkey != NONE && s->type_key != NONE) {
+        DBuf<uint32_t> d_rm, d_cnt;
+        d_rm.alloc(nd); d_cnt.alloc(nd);
+        hipLaunchKernelGGL(root_resources_kernel, dim3(std::min<uint32_t>((uint32_t)((nd + 255) / 256), dev_ncu(s->device) * 16)),
+                           dim3(256), 0, st, (const DNode*)s->dev_nodes, s->dv->d_base.p, s->dv->d_roots.p, (uint32_t)nd, rkey,
+                           d_rm.p, d_cnt.p);
+        HIPCHK(hipGetLastError());
+        std::vector<uint32_t> cnt(nd);
+        HIPCHK(hipMemcpyAsync(rmap.data(), d_rm.p, nd * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(cnt.data(), d_cnt.p, nd * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        for (size_t d = 0; d < nd; d++) { toff[d] = (uint32_t)total; total += cnt[d]; }
+      }
+      HIPCHK(hipStreamSynchronize(st));
+    } else if (rkey != NONE && s->type_key != NONE) {
       for (size_t d = 0; d < nd; d++) {
         const DNode* N = D.nodes.data() + D.base[d];
         const DNode& root = N[D.roots[d]];
@@ -499,6 +564,7 @@ void session_upload(gg_session* s) {
         }
       }
     }
+    mark("resource map");
     if (total > 0xFFFFFFF0u) { std::fill(rmap.begin(), rmap.end(), NONE); total = 0; }
     s->has_order = false;
 
@@ -524,9 +590,9 @@ void session_upload(gg_session* s) {
       const bool sort_on = !getenv("GG_SHAPE_SORT") || atoi(getenv("GG_SHAPE_SORT")) != 0;
       if (sort_on && nd > 64) {
         std::unordered_map<uint32_t, uint32_t> freq, tlen;
-        for (size_t d = 0; d < std::min<size_t>(nd, 4096); d++) {
+        for (size_t d = 0; d < nsample; d++) {
           if (rmap[d] == NONE) continue;
-          const DNode* N = D.nodes.data() + D.base[d];
+          const DNode* N = HN + D.base[d];
           const DNode& m = N[rmap[d]];
           for (uint32_t j = 0; j < m.count; j++) {
             const DNode& r = N[m.a + j];
@@ -578,6 +644,7 @@ void session_upload(gg_session* s) {
       }
     }
     HIPCHK(hipStreamSynchronize(st));   // the host vectors above die at the end of this scope
+    mark("type column + order");
   }
   std::vector<DevProg> dps;
   s->max_top = 1;
@@ -630,7 +697,7 @@ void session_upload(gg_session* s) {
   static constexpr size_t kLaneHeapBudget = (size_t)8 << 30;
   s->lane_heap_bytes = s->lane_heap_set ? s->lane_heap_set : 64u * 1024u;
   s->lane_recs_bytes = 24576;
-  const bool large_docs = s->docs.ndocs() && s->docs.nodes.size() / s->docs.ndocs() > 4096;
+  const bool large_docs = s->docs.ndocs() && arena_nodes(s) / s->docs.ndocs() > 4096;
   if (!s->lane_heap_set && large_docs && s->lane_slots && (size_t)s->lane_slots * 64 * (256u << 10) <= kLaneHeapBudget) {
     s->lane_heap_bytes = 256u << 10;
     s->lane_recs_bytes = 2048u * (uint32_t)sizeof(Rec);
@@ -670,6 +737,7 @@ void session_upload(gg_session* s) {
   s->dv->d_counts.alloc(std::max<size_t>(s->ncounts, 1));
   HIPCHK(hipStreamSynchronize(st));
   s->uploaded = true;
+  mark("programs + buffers");
 }
 
 hipStream_t session_stream(gg_session* s) { return s->stream ? s->stream : s->dv->stream; }
@@ -1011,9 +1079,17 @@ void render_tables(gg_session* s) {
   s->r_sname_first = (const uint32_t*)(b + o_sfirst); s->r_sname_n = (const uint32_t*)(b + o_sn);
   s->r_sname_fk = (const uint32_t*)(b + o_sfk); s->r_nsname = (uint32_t)sname.size();
   if (!s->marks_on_device) {
-    const size_t n = s->docs.nodes.size();
-    s->dv->d_line.upload(s->docs.line.data(), std::max<size_t>(n, 1), st);
-    s->dv->d_col.upload(s->docs.col.data(), std::max<size_t>(n, 1), st);
+    std::lock_guard<std::mutex> lk(s->arena_mu);
+    const size_t n = arena_nodes(s);
+    if (s->resident.nodes) {   // the loader's marks are in HBM already
+      s->dv->d_line.alloc(std::max<size_t>(n, 1));
+      s->dv->d_col.alloc(std::max<size_t>(n, 1));
+      HIPCHK(hipMemcpyAsync(s->dv->d_line.p, s->resident.line, n * 4, hipMemcpyDeviceToDevice, st));
+      HIPCHK(hipMemcpyAsync(s->dv->d_col.p, s->resident.col, n * 4, hipMemcpyDeviceToDevice, st));
+    } else {
+      s->dv->d_line.upload(s->docs.line.data(), std::max<size_t>(n, 1), st);
+      s->dv->d_col.upload(s->docs.col.data(), std::max<size_t>(n, 1), st);
+    }
     s->marks_on_device = true;
   }
   if (!s->dv->pinned) HIPCHK(hipHostMalloc((void**)&s->dv->pinned, DeviceBufs::kPinnedBytes, hipHostMallocDefault));
@@ -1084,6 +1160,7 @@ bool device_report_json(gg_session* s, size_t first, size_t count, size_t report
         while (k < b.nb && !failed) {
           if (b.sizes[k] & kHostDoc) {
             const auto h0 = std::chrono::steady_clock::now();
+            ensure_host_arena(s);   // the host writer reads the arena's columns
             const size_t d = b.d0 + k;
             TextBuf t;
             if (d != report_first) t.append(",\n", 2);
@@ -1175,7 +1252,7 @@ bool device_report_json(gg_session* s, size_t first, size_t count, size_t report
     R.sizes.alloc_grow(nb);
     RenderArgs A{};
     A.nodes = s->dv->d_nodes.p; A.klen = s->dv->d_klen.p; A.pool = s->dv->d_bytes.p; A.parent = s->dv->d_parent.p;
-    A.line = s->dv->d_line.p; A.col = s->dv->d_col.p; A.base = s->dv->d_base.p; A.n_nodes = s->docs.nodes.size();
+    A.line = s->dv->d_line.p; A.col = s->dv->d_col.p; A.base = s->dv->d_base.p; A.n_nodes = arena_nodes(s);
     A.progs = s->dv->d_rprogs.p; A.nfiles = (uint32_t)nf; A.max_top = s->max_top;
     A.tiles = s->dv->d_tiles.p; A.rule_status = s->dv->d_rule_status.p; A.recs = s->dv->d_recs_dense.p; A.rec_off = s->dv->d_dense_off.p;
     A.sname_text = s->r_sname_text; A.sname = s->r_sname; A.sname_first = s->r_sname_first; A.sname_n = s->r_sname_n;
@@ -1244,6 +1321,7 @@ bool shards_report(const std::vector<ShardView>& sh, std::string& out, int32_t& 
     const size_t nf = v.s->progs.size();
     for (size_t t = v.first * nf; t < (v.first + v.count) * nf; t++) {
       if (v.s->tiles[t].err) {
+        ensure_host_arena(v.s);
         std::vector<const Program*> progs;
         for (auto& p : v.s->progs) progs.push_back(&p->prog);
         tile_error(v.s->docs, (uint32_t)(t / nf), *progs[t % nf], v.s->tiles[t], err);
@@ -1281,6 +1359,7 @@ bool shards_report(const std::vector<ShardView>& sh, std::string& out, int32_t& 
   std::vector<std::string> yaml_parts;
   for (const ShardView& v : sh) {
     gg_session* s = v.s;
+    ensure_host_arena(s);   // host writers
     std::vector<const Program*> progs;
     for (auto& p : s->progs) progs.push_back(&p->prog);
     const size_t nf = progs.size();
@@ -2217,6 +2296,7 @@ int64_t gg_session_report_bytes(gg_session* s, int32_t output_format, size_t max
   if (!s->evaluated) { set_err(err, -1, "session not evaluated"); return -1; }
   if (output_format != OUT_JSON && output_format != OUT_YAML) { set_err(err, 18, "IllegalArguments: json or yaml"); return -1; }
   try {
+    ensure_host_arena(s);
     std::vector<const Program*> progs;
     for (auto& p : s->progs) progs.push_back(&p->prog);
     const size_t nf = progs.size(), nd = max_docs ? std::min(max_docs, s->docs.ndocs()) : s->docs.ndocs();
@@ -2274,6 +2354,7 @@ int64_t gg_session_report_json_device(gg_session* s, size_t max_docs, int32_t* e
     const size_t nf = progs.size(), nd = max_docs ? std::min(max_docs, s->docs.ndocs()) : s->docs.ndocs();
     for (size_t t = 0; t < nd * nf; t++)
       if (s->tiles[t].err) {
+        ensure_host_arena(s);
         ReportError re;
         tile_error(s->docs, (uint32_t)(t / nf), *progs[t % nf], s->tiles[t], re);
         set_err(err, ffi_code(re.kind), error_display(re.kind, re.msg));
@@ -2352,6 +2433,7 @@ int32_t gg_session_add_docs(gg_session* s, const char* const* texts, const size_
     if (failed[t] >= 0) { set_err(err, ffi_code(errs[t].kind), error_display(errs[t].kind, errs[t].msg)); return 5; }
   }
   try {
+    ensure_host_arena(s);   // host documents join a device-loaded batch
     merge_batches(s->docs, parts);
   } catch (std::exception& e) { set_err(err, -1, e.what()); return -1; }
   s->uploaded = false;
@@ -2537,6 +2619,7 @@ int32_t gg_session_add_synthetic(gg_session* s, uint64_t first, size_t n, int32_
     parallel_run((size_t)nthreads, work);
     for (int t = 0; t < nthreads; t++)
       if (failed[t]) { set_err(err, ffi_code(errs[t].kind), error_display(errs[t].kind, errs[t].msg)); return 5; }
+    ensure_host_arena(s);
     merge_batches(s->docs, parts);
     s->uploaded = false;
     return 0;
@@ -2579,7 +2662,14 @@ int32_t gg_session_add_docs_device(gg_session* s, const char* const* texts, cons
     DocBatch b;
     std::vector<uint32_t> refused;
     void* dev_nodes = nullptr;
-    if (!gpu_load_json(b, texts, lens, nm, n, st, why, &refused, &dev_nodes)) { set_note(err, why); return 1; }
+    // the arena's columns stay in HBM unless GG_RESIDENT_ARENA=0 (ensure_host_arena brings them down)
+    ResidentArena res;
+    const bool keep = !getenv("GG_RESIDENT_ARENA") || atoi(getenv("GG_RESIDENT_ARENA")) != 0;
+    const auto tl = std::chrono::steady_clock::now();
+    if (!gpu_load_json(b, texts, lens, nm, n, st, why, &refused, &dev_nodes, keep ? &res : nullptr)) { set_note(err, why); return 1; }
+    struct ResHolder { ResidentArena& r; ~ResHolder() { for (uint32_t* p : {r.line, r.col, r.kline, r.kcol}) if (p) hipFree(p); } } rhold{res};
+    if (getenv("GG_LOAD_TRACE"))
+      fprintf(stderr, "[load] gpu_load_json returned %8.1f ms\n", std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tl).count());
     struct Holder { void*& p; ~Holder() { if (p) hipFree(p); } } hold{dev_nodes};
     const size_t dev_n = b.nodes.size();
     if (!refused.empty()) {
@@ -2608,9 +2698,13 @@ int32_t gg_session_add_docs_device(gg_session* s, const char* const* texts, cons
     s->docs = std::move(b);
     s->uploaded = false;
     if (s->dev_nodes) hipFree(s->dev_nodes);
-    s->dev_nodes = dev_nodes; s->dev_nodes_n = dev_n;
+    s->dev_nodes = dev_nodes; s->dev_nodes_n = res.nodes ? (size_t)res.nodes : dev_n;
     dev_nodes = nullptr;
+    s->resident = res;
+    res = ResidentArena{};
     load_stats(st, stats);
+    if (getenv("GG_LOAD_TRACE"))
+      fprintf(stderr, "[load] session holds the batch %8.1f ms\n", std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tl).count());
     return 0;
   } catch (std::exception& e) { set_err(err, -1, e.what()); return -1; }
 }
@@ -2635,6 +2729,14 @@ int32_t gg_session_add_synthetic_device(gg_session* s, uint64_t first, size_t n,
     const double gen_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - g0).count();
     const int32_t rc = gg_session_add_docs_device(s, p.data(), l.data(), nm.data(), n, stats, err);
     if (stats) stats[9] = gen_ms;
+    // the generated text is freed by the threads that allocated it (their own malloc arenas; freeing
+    // a million buffers from one thread serialises on the arenas' locks)
+    const auto f0 = std::chrono::steady_clock::now();
+    parallel_run((size_t)nthreads, [&](size_t t) {
+      for (size_t i = n * t / nthreads; i < n * (t + 1) / nthreads; i++) { std::string().swap(texts[i]); std::string().swap(names[i]); }
+    });
+    if (getenv("GG_LOAD_TRACE"))
+      fprintf(stderr, "[load] generated text freed %8.1f ms\n", std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - f0).count());
     return rc;
   } catch (std::exception& e) { set_err(err, -1, e.what()); return -1; }
 }
@@ -2797,7 +2899,7 @@ int64_t gg_session_stat(gg_session* s, int32_t what) {
   switch (what) {
     case 0: return (int64_t)s->docs.ndocs();
     case 1: return (int64_t)s->progs.size();
-    case 2: return (int64_t)s->docs.nodes.size();
+    case 2: return (int64_t)arena_nodes(s);
     case 3: return (int64_t)s->docs.bytes.size();
     case 4: case 5: case 6: {
       uint32_t want = what == 4 ? ST_FAIL : what == 5 ? ST_PASS : ST_SKIP;
@@ -2807,7 +2909,7 @@ int64_t gg_session_stat(gg_session* s, int32_t what) {
     }
     case 7: { int64_t c = 0; for (auto& t : s->tiles) if (t.err) c++; return c; }
     case 8: return (int64_t)s->recs.size();
-    case 9: return (int64_t)(s->docs.nodes.size() * sizeof(DNodeP) + s->docs.bytes.size() + s->docs.roots.size() * 12);
+    case 9: return (int64_t)(arena_nodes(s) * sizeof(DNodeP) + s->docs.bytes.size() + s->docs.roots.size() * 12);
     case 10: for (auto& t : s->tiles) if (t.err) return t.err; return 0;
     case 11: return (int64_t)s->recs.size() * (int64_t)sizeof(Rec);
     case 12: return (int64_t)s->rec_cap;

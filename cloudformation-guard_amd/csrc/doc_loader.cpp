@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <unordered_map>
 
 #include "host_format.h"
@@ -713,6 +714,44 @@ void DocBatch::adopt(uint32_t off, uint32_t n) {
   size_t h = fnv1a(bytes.data() + off, n) & mask;
   while (islots[h]) h = (h + 1) & mask;
   islots[h] = off + 1; ilen[h] = n; iused++;
+}
+
+void DocBatch::adopt_bulk(const uint32_t* off, const uint32_t* len, size_t n, unsigned threads) {
+  if (!n) return;
+  size_t cap = islots.empty() ? 4096 : islots.size();
+  while ((iused + n) * 2 > cap) cap *= 2;
+  if (cap != islots.size()) {
+    // rehash what is there (normally nothing: the device loader fills an empty batch)
+    const size_t keep = iused;
+    std::vector<uint32_t> old_s, old_l;
+    old_s.swap(islots); old_l.swap(ilen);
+    islots.assign(cap, 0); ilen.assign(cap, 0);
+    iused = 0;
+    for (size_t i = 0; i < old_s.size(); i++) if (old_s[i]) adopt(old_s[i] - 1, old_l[i]);
+    (void)keep;
+  }
+  const size_t mask = islots.size() - 1;
+  uint32_t* S = islots.data();
+  uint32_t* L = ilen.data();
+  const char* B = bytes.data();
+  threads = std::max(1u, std::min<unsigned>(threads, (unsigned)((n + 65535) / 65536)));
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < threads; t++)
+    th.emplace_back([=]() {
+      for (size_t i = n * t / threads; i < n * (t + 1) / threads; i++) {
+        size_t h = fnv1a(B + off[i], len[i]) & mask;
+        for (;;) {
+          uint32_t expect = 0;
+          if (__atomic_compare_exchange_n(&S[h], &expect, off[i] + 1, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {
+            L[h] = len[i];
+            break;
+          }
+          h = (h + 1) & mask;
+        }
+      }
+    });
+  for (auto& x : th) x.join();
+  iused += n;
 }
 
 std::string DocBatch::path(uint64_t base, uint32_t node) const {

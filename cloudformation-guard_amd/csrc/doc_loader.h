@@ -82,6 +82,10 @@ struct DocBatch {
   uint32_t find(const char* p, uint32_t n) const;   // pool offset of an interned string, or NONE
   // indexes a string already in the pool at `off` (a pool built on the device, json_gpu.hip)
   void adopt(uint32_t off, uint32_t n);
+  // adopt() for n strings at once on `threads` host threads: the index is sized once and filled by
+  // concurrent linear-probing inserts (compare-and-swap on the slot; no deletions, so every string sits
+  // at the first free slot from its hash at its insertion and find() reaches it)
+  void adopt_bulk(const uint32_t* off, const uint32_t* len, size_t n, unsigned threads);
 
   // resizes every per-node column to s nodes, zero-filling new nodes (the columns default-initialise;
   // loaders that do not write every field of a new node use this)

@@ -31,8 +31,21 @@ struct GpuLoadStats {
 // (batch-wide limits, or strict mode); `out` is then unchanged.  With `keep_nodes` non-null the
 // device copy of out.nodes (hipMalloc'ed, out.nodes.size() DNodes) is handed to the caller, who
 // frees it with hipFree: the session packs its arena from it instead of uploading the nodes again.
+//
+// With `resident` non-null as well (and no document refused) the per-node columns stay in HBM: out.nodes,
+// line, col, kline, kcol are left EMPTY, the device copies are handed over in *resident (node count
+// st.nodes; the caller owns every pointer, hipFree), and only the pool, the intern index, bases and names
+// reach the host.  The session copies the columns down when a host consumer first needs them
+// (capi.cpp ensure_host_arena); a job whose reports are all rendered on the device never does.
+struct ResidentArena {
+  uint32_t* line = nullptr;    // per node mark
+  uint32_t* col = nullptr;
+  uint32_t* kline = nullptr;   // per map-entry node: its key's mark
+  uint32_t* kcol = nullptr;
+  uint64_t nodes = 0;          // 0: the columns came down to the host (out is complete)
+};
 bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, const std::vector<std::string>& names,
                    size_t n, GpuLoadStats& st, std::string& why, std::vector<uint32_t>* refused = nullptr,
-                   void** keep_nodes = nullptr);
+                   void** keep_nodes = nullptr, ResidentArena* resident = nullptr);
 
 }  // namespace gg

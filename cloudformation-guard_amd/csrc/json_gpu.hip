@@ -759,9 +759,33 @@ struct Staging {
 
 }  // namespace
 
+// root.Resources of every document of a device-resident arena (the scan session_upload runs over host
+// nodes otherwise): rmap[d] = document-relative node of the entry (NONE: none, or not a map), cnt[d] =
+// its entry count.  The first entry keyed `rkey` decides, as on the host.
+__global__ void __launch_bounds__(256) root_resources_kernel(const DNode* nodes, const uint64_t* base, const uint32_t* roots,
+                                                             uint32_t nd, uint32_t rkey, uint32_t* rmap, uint32_t* cnt) {
+  for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < nd; d += gridDim.x * blockDim.x) {
+    const DNode* N = nodes + base[d];
+    const DNode root = N[roots[d]];
+    uint32_t r = NONE, c = 0;
+    if (root.kind == K_MAP) {
+      for (uint32_t k = 0; k < root.count; k++) {
+        const DNode e = N[root.a + k];
+        if (e.key_hash != rkey) continue;
+        if (e.kind == K_MAP) { r = root.a + k; c = e.count; }
+        break;
+      }
+    }
+    rmap[d] = r;
+    cnt[d] = c;
+  }
+}
+
 bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, const std::vector<std::string>& names,
                    size_t n, GpuLoadStats& st, std::string& why, std::vector<uint32_t>* refused,
-                   void** keep_nodes) {
+                   void** keep_nodes, ResidentArena* resident) {
+  if (resident) *resident = ResidentArena{};
+  if (!keep_nodes) resident = nullptr;   // the columns stay only beside the nodes
   static const char* kWhy[] = {"", "outside the strict-JSON subset", "nesting deeper than 64", "duplicate map keys",
                                "a number the host types (beyond 64 bits, or an infinite / undecided float)", "string table full", "string pool full",
                                "string fingerprint collision", "batch too large", "a container with more than 65535 elements"};
@@ -777,6 +801,12 @@ bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, 
   const uint64_t total = off[n];
   st.text_bytes = total;
   Staging stg;
+  // GG_LOAD_TRACE=1: wall-clock phase marks on stderr
+  const bool trace = getenv("GG_LOAD_TRACE") != nullptr;
+  const auto tw = std::chrono::steady_clock::now();
+  auto mark = [&](const char* what) {
+    if (trace) fprintf(stderr, "[load] %-22s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw).count());
+  };
 
   hipEvent_t e0, e1;
   JCHK(hipEventCreate(&e0));
@@ -787,6 +817,7 @@ bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, 
   stg.h2d_docs(d_text.p, texts, lens, off.data(), n);
   JCHK(hipMemcpy(d_off.p, off.data(), (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice));
   st.h2d_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  mark("h2d");
 
   DevArr<uint32_t> d_nn, d_nc, d_ns, d_bad, d_doc_bad, d_doc_bad0;
   d_nn.alloc(n); d_nc.alloc(n); d_ns.alloc(n); d_bad.alloc(1); d_doc_bad.alloc(n); d_doc_bad0.alloc(n);
@@ -815,6 +846,7 @@ bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, 
   JCHK(hipEventRecord(e1));
   JCHK(hipEventSynchronize(e1));
   JCHK(hipEventElapsedTime(&ms, e0, e1)); ms_total += ms;
+  mark("count pass");
   if (bad_now()) return false;
   // the count pass's per-document refusals; a table / pool retry starts again from them
   JCHK(hipMemcpy(d_doc_bad0.p, d_doc_bad.p, n * 4, hipMemcpyDeviceToDevice));
@@ -829,15 +861,19 @@ bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, 
     nbase[k] = N;
     N += nn[k]; S += ns[k];
   }
-  // the host columns are sized (zero-filled: page faults, seconds at 1M documents) while the
-  // device passes run; one thread per column
-  std::thread resizer([&out, N]() {
+  // the host columns are sized (page faults, seconds at 1M documents) while the device passes run; one
+  // thread per column.  A device-resident arena sizes them only if a document is refused (the host
+  // loader's documents are merged into host columns).
+  auto size_columns = [&out, N]() {
     std::thread a([&]() { out.nodes.resize(N); });
     std::thread b([&]() { out.line.resize(N); out.col.resize(N); });
     out.kline.resize(N); out.kcol.resize(N);
     a.join(); b.join();
-  });
+  };
+  std::thread resizer;
+  if (!resident) resizer = std::thread(size_columns);
   struct Joiner { std::thread& t; ~Joiner() { if (t.joinable()) t.join(); } } join_resizer{resizer};
+  mark("count D2H + scan");
   DevArr<uint64_t> d_nbase;
   d_nbase.alloc(n);
   JCHK(hipMemcpy(d_nbase.p, nbase.data(), n * 8, hipMemcpyHostToDevice));
@@ -865,6 +901,7 @@ bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, 
   d_recs.alloc(N);
   A.recs = d_recs.p;
   A.line = d_line.p; A.col = d_col.p; A.kline = d_kline.p; A.kcol = d_kcol.p;
+  mark("device allocs");
   for (;;) {
     if (d_pool.n != pool_cap + 16) d_pool.alloc(pool_cap + 16);
     A.pool = d_pool.p; A.pool_cursor = d_pool_cursor.p; A.pool_cap = pool_cap;
@@ -905,10 +942,11 @@ bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, 
     break;
   }
   st.kernel_ms = ms_total;
+  mark("emit/own/fix passes");
   JCHK(hipEventDestroy(e0));
   JCHK(hipEventDestroy(e1));
   if (bad_now()) {
-    resizer.join();
+    if (resizer.joinable()) resizer.join();
     out.clear();   // refused: the batch stays empty
     return false;
   }
@@ -918,38 +956,59 @@ bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, 
     if (!doc_bad[k]) continue;
     if (!refused) {   // strict: one refused document refuses the batch
       why = doc_bad[k] < 10 ? kWhy[doc_bad[k]] : "refused";
-      resizer.join();
+      if (resizer.joinable()) resizer.join();
       out.clear();
       return false;
     }
     refused->push_back((uint32_t)k);
   }
   st.refused_docs = refused ? refused->size() : 0;
+  mark("doc_bad");
 
   // results to the host batch (the host keeps the reporter's columns and the intern index)
   t0 = std::chrono::steady_clock::now();
   unsigned long long pool_used = 0;
   JCHK(hipMemcpy(&pool_used, d_pool_cursor.p, 8, hipMemcpyDeviceToHost));
-  resizer.join();
-  stg.d2h(out.nodes.data(), d_nodes.p, N * sizeof(DNode));
-  stg.d2h(out.line.data(), d_line.p, N * 4);
-  stg.d2h(out.col.data(), d_col.p, N * 4);
-  stg.d2h(out.kline.data(), d_kline.p, N * 4);
-  stg.d2h(out.kcol.data(), d_kcol.p, N * 4);
+  mark("pre-join");
+  if (resident && refused && !refused->empty()) resident = nullptr;   // host documents join: host columns
+  if (resident) {
+    resident->line = d_line.p; resident->col = d_col.p; resident->kline = d_kline.p; resident->kcol = d_kcol.p;
+    resident->nodes = N;
+    d_line.p = d_col.p = d_kline.p = d_kcol.p = nullptr;
+  } else {
+    if (resizer.joinable()) resizer.join(); else size_columns();
+    mark("columns sized");
+    stg.d2h(out.nodes.data(), d_nodes.p, N * sizeof(DNode));
+    stg.d2h(out.line.data(), d_line.p, N * 4);
+    stg.d2h(out.col.data(), d_col.p, N * 4);
+    stg.d2h(out.kline.data(), d_kline.p, N * 4);
+    stg.d2h(out.kcol.data(), d_kcol.p, N * 4);
+  }
   out.bytes.resize(pool_used);
   if (pool_used) stg.d2h(&out.bytes[0], d_pool.p, pool_used);
+  mark("arena D2H");
   std::vector<unsigned long long> tkey(tslots);
   std::vector<uint32_t> tlen(tslots), tid(tslots);
   JCHK(hipMemcpy(tkey.data(), d_tkey.p, tslots * 8, hipMemcpyDeviceToHost));
   JCHK(hipMemcpy(tlen.data(), d_tlen.p, tslots * 4, hipMemcpyDeviceToHost));
   JCHK(hipMemcpy(tid.data(), d_tid.p, tslots * 4, hipMemcpyDeviceToHost));
   st.d2h_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  mark("table D2H");
   uint64_t distinct = 0;
-  for (uint64_t s = 0; s < tslots; s++) if (tkey[s]) { out.adopt(tid[s], tlen[s]); distinct++; }
+  {
+    std::vector<uint32_t> aoff, alen;
+    aoff.reserve(tslots / 2); alen.reserve(tslots / 2);
+    for (uint64_t s = 0; s < tslots; s++) if (tkey[s]) { aoff.push_back(tid[s]); alen.push_back(tlen[s]); }
+    distinct = aoff.size();
+    mark("table scan");
+    out.adopt_bulk(aoff.data(), alen.data(), aoff.size(), std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
+    mark("index built");
+  }
   out.roots.assign(n, 0);
   out.base.assign(nbase.begin(), nbase.end());
   out.names.assign(names.begin(), names.begin() + n);
   st.nodes = N; st.distinct_strings = distinct; st.pool_bytes = pool_used;
+  mark("adopt + names");
   if (keep_nodes) { *keep_nodes = d_nodes.p; d_nodes.p = nullptr; }
   return true;
 }

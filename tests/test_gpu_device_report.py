@@ -88,3 +88,54 @@ def test_floats_and_debug_reasons_fall_back_to_host_in_place():
     assert st["host_docs"] > 0 and st["device_docs"] > 0
     exp, ecode, _ = oracle_validate(rules, [("f-%d.json" % i, d) for i, d in enumerate(docs)])
     assert (out, code) == (exp, ecode)
+
+
+def _device_loaded(rules, docs, prefix):
+    s = guard_amd.Session()
+    for name, text in rules:
+        s.add_rules(text, name)
+    st = s.add_docs_device(docs, ["%s-%d.json" % (prefix, i) for i in range(len(docs))])
+    assert st is not None, "device loader refused the corpus"
+    s.eval(1)
+    return s
+
+
+@pytest.mark.parametrize("resident", ["1", "0"])
+def test_resident_arena_reports_equal_oracle(resident, monkeypatch):
+    """the device loader leaves the arena's columns in HBM (capi.cpp ensure_host_arena): the device JSON
+    report never brings them down; a host writer (YAML, SARIF, a host-fallback document) does, at first
+    use -- every format equals the oracle either way"""
+    monkeypatch.setenv("GG_RESIDENT_ARENA", resident)
+    rules = rule_pack("cfg2")
+    docs = synth.cfn_corpus(300, start=4321, n_resources=25)
+    data = [("r-%d.json" % i, d) for i, d in enumerate(docs)]
+    s = _device_loaded(rules, docs, "r")
+    nodes = s.stat(s.STAT["nodes"]) if "nodes" in s.STAT else None
+    s.set_device_report(True)
+    exp, ecode, _ = oracle_validate(rules, data)
+    assert s.report("json") == (exp, ecode)
+    for fmt in ("yaml", "sarif"):
+        e, c, _ = oracle_validate(rules, data, output=fmt)
+        assert s.report(fmt) == (e, c), fmt
+    assert s.report("json") == (exp, ecode)
+    if nodes is not None:
+        assert s.stat(s.STAT["nodes"]) == nodes
+    s.close()
+
+
+def test_resident_arena_host_fallback_documents(monkeypatch):
+    monkeypatch.setenv("GG_RESIDENT_ARENA", "1")
+    rules = [("f.guard", "rule r { Resources.*.Properties.Size == 10 }\nrule i { Resources.*.Properties.Items[5] exists }")]
+    docs = []
+    for i in range(80):
+        size = 2.5 if i % 7 == 0 else i
+        items = [1, 2] if i % 3 == 0 else [1, 2, 3, 4, 5, 6]
+        docs.append(json.dumps({"Resources": {"a": {"Properties": {"Size": size, "Items": items}}}}))
+    s = _device_loaded(rules, docs, "f")
+    s.set_device_report(True)
+    n, code, st = s.report_json_device()
+    assert st["host_docs"] > 0 and st["device_docs"] > 0
+    exp, ecode, _ = oracle_validate(rules, [("f-%d.json" % i, d) for i, d in enumerate(docs)])
+    assert s.report("json") == (exp, ecode)
+    assert n == len(exp.encode()) and code == ecode
+    s.close()
