@@ -25,7 +25,7 @@ YAML_LIB = "/opt/conda/lib"
 
 HOST_SRCS = ["doc_loader.cpp", "rules_parser.cpp", "regex_dfa.cpp", "cruet.cpp", "compiler.cpp", "reporter.cpp",
              "synth_corpus.cpp"]
-HIP_SRCS = ["eval_kernel.hip", "eval_kernel_nfa.hip", "json_gpu.hip", "report_gpu.hip", "capi.cpp"]
+HIP_SRCS = ["eval_kernel.hip", "eval_kernel_nfa.hip", "json_gpu.hip", "report_gpu.hip", "order_sort.hip", "capi.cpp"]
 # occupancy target of the lane-mode kernel (waves per SIMD); it caps VGPRs at 512 / N.  4 (126 VGPRs,
 # 8 spilled) beats 2 (178) and 3 (168): the kernel waits on dependent loads, so resident waves are
 # worth more than registers (profiles/r02_ab_occupancy.log; capi.cpp sizes the grid to 16 waves/CU)

@@ -45,6 +45,8 @@ __global__ void guard_eval_verbose_kernel_nfa(LaunchArgs A);
 __global__ void guard_eval_lanes_kernel_nfa(LaunchArgs A);
 __global__ void resource_type_kernel(DevBatch D);
 __global__ void shape_key_kernel(DevBatch D, const uint32_t* top8, unsigned long long* key);
+void device_segmented_order(const unsigned long long* key, uint32_t* order, uint32_t n, const uint32_t* seg_host,
+                            uint32_t nseg, hipStream_t st);
 __global__ void root_resources_kernel(const DNode* nodes, const uint64_t* base, const uint32_t* roots, uint32_t nd, uint32_t rkey,
                                       uint32_t* rmap, uint32_t* cnt);
 __global__ void pack_nodes_kernel(const DNode* in, DNodeP* out, uint32_t* klen, uint32_t* parent, uint64_t n, uint32_t* bad);
@@ -581,6 +583,7 @@ void session_upload(gg_session* s) {
       const uint32_t blocks = std::min<uint32_t>((B.ndocs + 3) / 4, dev_ncu(s->device) * 16);
       hipLaunchKernelGGL(resource_type_kernel, dim3(blocks), dim3(256), 0, st, B);
       HIPCHK(hipGetLastError());
+      if (trace) { HIPCHK(hipStreamSynchronize(st)); mark("type column kernel"); }
       // Shape-sorted batches: the lane kernel's 64 lanes run in lock-step, so a batch costs the union
       // of its documents' paths.  Documents are ordered by their counts of the 8 most frequent Type
       // strings (taken from the first documents; most frequent first) inside each XCD's eighth of the
@@ -605,6 +608,7 @@ void session_upload(gg_session* s) {
         }
         // rank: types the rules files name (as a literal) first -- by how many files name them --
         // then by frequency, so the primary sort key aligns the most-checked resource type
+        mark("type sample");
         std::vector<std::pair<uint32_t, uint32_t>> top(freq.begin(), freq.end());
         std::unordered_map<uint32_t, uint32_t> named;
         for (auto& tp : top) {
@@ -626,20 +630,16 @@ void session_upload(gg_session* s) {
         hipLaunchKernelGGL(shape_key_kernel, dim3(std::min<uint32_t>((uint32_t)((nd + 255) / 256), dev_ncu(s->device) * 16)), dim3(256), 0, st,
                            B, (const uint32_t*)d_top.p, d_key.p);
         HIPCHK(hipGetLastError());
-        std::vector<unsigned long long> key(nd);
-        HIPCHK(hipMemcpyAsync(key.data(), d_key.p, nd * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
-        std::vector<uint32_t> order(nd);
-        for (size_t d = 0; d < nd; d++) order[d] = (uint32_t)d;
+        mark("shape keys");
+        // each XCD's eighth of the 64-document chunks sorted by key on the device, ties in load order
+        // (host threads with a comparator reading key[] at random took 0.4-0.6 s at 1M documents)
         const size_t nchunks = (nd + 63) / 64;
-        std::vector<std::thread> th;
-        for (size_t x = 0; x < 8; x++)
-          th.emplace_back([&, x]() {
-            const size_t p0 = std::min(nd, (size_t)(nchunks * x / 8) * 64), p1 = std::min(nd, (size_t)(nchunks * (x + 1) / 8) * 64);
-            std::stable_sort(order.begin() + p0, order.begin() + p1, [&](uint32_t a, uint32_t b) { return key[a] < key[b]; });
-          });
-        for (auto& t : th) t.join();
-        s->dv->d_order.upload(order.data(), nd, st);
+        uint32_t seg[9];
+        for (size_t x = 0; x <= 8; x++) seg[x] = (uint32_t)std::min(nd, (size_t)(nchunks * x / 8) * 64);
+        seg[8] = (uint32_t)nd;
+        s->dv->d_order.alloc(nd);
+        device_segmented_order(d_key.p, s->dv->d_order.p, (uint32_t)nd, seg, 8, st);
+        mark("order sorted");
         s->has_order = true;
       }
     }
