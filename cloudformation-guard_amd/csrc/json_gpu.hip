@@ -51,6 +51,8 @@ enum : uint32_t { M_COUNT = 0, M_EMIT = 2 };
 enum : uint32_t {
   BAD_NONE = 0, BAD_SYNTAX = 1, BAD_DEPTH = 2, BAD_DUPKEY = 3, BAD_NUMBER = 4, BAD_TABLE = 5, BAD_POOL = 6,
   BAD_VERIFY = 7, BAD_SIZE = 8, BAD_WIDE = 9,
+  BAD_NOTJSON = 10,   // count pass: not a JSON document (the YAML passes take it, yaml_gpu.inc)
+  BAD_YAML = 11,      // outside the block-style YAML subset the YAML passes parse
 };
 static const uint32_t kMaxDepth = 64;
 static const uint32_t kMaxPairwiseKeys = 256;
@@ -95,6 +97,8 @@ struct JArgs {
   uint64_t fp_mask;             // fingerprint bits kept (~0; tests narrow it to force collisions)
   uint32_t* bad;                // batch-wide refusal (BAD_TABLE / BAD_POOL: grow and retry), 0 = none
   uint32_t* doc_bad;            // per document: its refusal reason (BAD_*), 0 = loaded on the device
+  uint8_t* is_yaml;             // per document: parsed by the YAML passes
+  uint32_t* bad_at;             // diagnostics (GG_LOAD_DIAG): the YAML passes' byte offset of a refusal
 };
 
 __device__ inline void refuse(const JArgs& A, uint32_t why) { atomicCAS(A.bad, 0u, why); }
@@ -372,7 +376,7 @@ __device__ void parse_doc(const JArgs& A, uint32_t d) {
   // this document is outside the subset: the passes skip it and the host loads it
   auto bad = [&](uint32_t why) { if (!A.doc_bad[d]) A.doc_bad[d] = why; };   // the first reason
   if (MODE == M_COUNT) { A.n_nodes[d] = 0; A.n_cont[d] = 0; A.n_str[d] = 0; }
-  else if (A.doc_bad[d]) return;
+  else if (A.doc_bad[d] || A.is_yaml[d]) return;
   const uint64_t nb = (MODE >= M_EMIT) ? A.node_base[d] : 0;
   const uint64_t cb = b0 >> 1;
   uint32_t nn = 1, nc = 0, ns = 0, ci = 0, next = 1;
@@ -481,7 +485,7 @@ __device__ void parse_doc(const JArgs& A, uint32_t d) {
 
   ws();
   const uint32_t c0 = T.at(i);
-  if (c0 != '{' && c0 != '[') { bad(BAD_SYNTAX); return; }
+  if (c0 != '{' && c0 != '[') { bad(BAD_NOTJSON); return; }
   if (MODE == M_EMIT) {
     const bool list = c0 == '[';
     eline = list ? 0 : line; ecol = list ? 0 : column();   // emit_root: lists keep (0,0)
@@ -546,6 +550,8 @@ __device__ void parse_doc(const JArgs& A, uint32_t d) {
   if (MODE == M_COUNT) { A.n_nodes[d] = nn; A.n_cont[d] = nc; A.n_str[d] = ns; }
 }
 
+#include "yaml_gpu.inc"
+
 // resident waves per SIMD the passes are compiled for (their VGPR budget: 512 / waves)
 #ifndef GG_JSON_WPE_COUNT
 #define GG_JSON_WPE_COUNT 8
@@ -586,7 +592,7 @@ __global__ void __launch_bounds__(256) json_own_kernel(JArgs A) {
         for (uint32_t u = 0; u < r; u++) pool[p++] = (uint8_t)(T.bytes4(k + u) & 0xFFu);
       }
     } cs{A.pool, p};
-    decode_string(T, q, cs, cont);
+    decode_at(T, q, len, cs, cont);
   }
 }
 
@@ -603,7 +609,7 @@ __device__ bool same_string(const JArgs& A, Text& T, uint64_t q, uint32_t id, ui
     __device__ void run(const Text& T, uint32_t k, uint32_t r) { ws.run(T, k, r, [&](uint32_t w, uint32_t len) { check(w, len); }); }
   } cs{WordStream(), (const uint32_t*)(A.pool + id), want, true};
   uint32_t cont = 0;
-  const uint64_t end = decode_string(T, q, cs, cont);
+  const uint64_t end = decode_at(T, q, want, cs, cont);
   const uint32_t pos = cs.ws.len;
   if ((pos & 3u) && (pos > want || cs.pw[pos >> 2] != cs.ws.word)) cs.same = false;
   return end && cs.same && pos == want;
@@ -788,7 +794,8 @@ bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, 
   if (!keep_nodes) resident = nullptr;   // the columns stay only beside the nodes
   static const char* kWhy[] = {"", "outside the strict-JSON subset", "nesting deeper than 64", "duplicate map keys",
                                "a number the host types (beyond 64 bits, or an infinite / undecided float)", "string table full", "string pool full",
-                               "string fingerprint collision", "batch too large", "a container with more than 65535 elements"};
+                               "string fingerprint collision", "batch too large", "a container with more than 65535 elements",
+                               "not a JSON document (YAML device parser off)", "outside the block-style YAML subset"};
   if (!out.nodes.empty() || !out.roots.empty()) { why = "the device loader fills an empty batch"; return false; }
   if (n == 0) return true;
   if (n > 0xFFFFFFF0ull) { why = kWhy[BAD_SIZE]; return false; }
@@ -820,14 +827,21 @@ bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, 
   mark("h2d");
 
   DevArr<uint32_t> d_nn, d_nc, d_ns, d_bad, d_doc_bad, d_doc_bad0;
-  d_nn.alloc(n); d_nc.alloc(n); d_ns.alloc(n); d_bad.alloc(1); d_doc_bad.alloc(n); d_doc_bad0.alloc(n);
+  DevArr<uint8_t> d_yaml;
+  d_nn.alloc(n); d_nc.alloc(n); d_ns.alloc(n); d_bad.alloc(1); d_doc_bad.alloc(n); d_doc_bad0.alloc(n); d_yaml.alloc(n);
   JCHK(hipMemset(d_bad.p, 0, 4));
   JCHK(hipMemset(d_doc_bad.p, 0, n * 4));
+  JCHK(hipMemset(d_yaml.p, 0, n));
+  DevArr<uint32_t> d_bad_at;
+  const bool diag = getenv("GG_LOAD_DIAG") != nullptr;
+  if (diag) { d_bad_at.alloc(n); JCHK(hipMemset(d_bad_at.p, 0xFF, n * 4)); }
+  // block-style YAML documents parse on the device too (yaml_gpu.inc) unless GG_YAML_DEVICE=0
+  const bool yaml_on = !getenv("GG_YAML_DEVICE") || atoi(getenv("GG_YAML_DEVICE")) != 0;
   JArgs A{};
   A.text = d_text.p; A.off = d_off.p; A.ndocs = (uint32_t)n;
   A.fp_mask = ~0ull;
   if (const char* e = getenv("GG_JSON_FP_MASK")) A.fp_mask = strtoull(e, nullptr, 0);   // tests: forced collisions
-  A.n_nodes = d_nn.p; A.n_cont = d_nc.p; A.n_str = d_ns.p; A.bad = d_bad.p; A.doc_bad = d_doc_bad.p;
+  A.n_nodes = d_nn.p; A.n_cont = d_nc.p; A.n_str = d_ns.p; A.bad = d_bad.p; A.doc_bad = d_doc_bad.p; A.is_yaml = d_yaml.p; A.bad_at = diag ? d_bad_at.p : nullptr;
   DevArr<uint16_t> d_counts; d_counts.alloc(total / 2 + 1);
   A.counts = d_counts.p;
   const uint32_t dgrid = grid_for(n, 256);
@@ -835,7 +849,7 @@ bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, 
   auto bad_now = [&]() {
     uint32_t b = 0;
     JCHK(hipMemcpy(&b, d_bad.p, 4, hipMemcpyDeviceToHost));
-    if (b) why = b < 10 ? kWhy[b] : "refused";
+    if (b) why = b < 12 ? kWhy[b] : "refused";
     return b != 0;
   };
 
@@ -843,6 +857,10 @@ bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, 
   JCHK(hipEventRecord(e0));
   hipLaunchKernelGGL(json_pass_kernel<M_COUNT>, dim3(dgrid), dim3(256), 0, 0, A);
   JCHK(hipGetLastError());
+  if (yaml_on) {
+    hipLaunchKernelGGL(yaml_pass_kernel<M_COUNT>, dim3(dgrid), dim3(256), 0, 0, A);
+    JCHK(hipGetLastError());
+  }
   JCHK(hipEventRecord(e1));
   JCHK(hipEventSynchronize(e1));
   JCHK(hipEventElapsedTime(&ms, e0, e1)); ms_total += ms;
@@ -915,6 +933,7 @@ bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, 
     // 2. emit, 3. own, 4. fix + verify
     JCHK(hipEventRecord(e0));
     hipLaunchKernelGGL(json_pass_kernel<M_EMIT>, dim3(dgrid), dim3(256), 0, 0, A);
+    if (yaml_on) hipLaunchKernelGGL(yaml_pass_kernel<M_EMIT>, dim3(dgrid), dim3(256), 0, 0, A);
 #if !GG_JDIAG_NOINTERN
     hipLaunchKernelGGL(json_own_kernel, dim3(grid_for(tslots, 256)), dim3(256), 0, 0, A);
     hipLaunchKernelGGL(json_fix_verify_kernel, dim3(grid_for(n * 64ull, 256)), dim3(256), 0, 0, A);
@@ -955,7 +974,17 @@ bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, 
   for (size_t k = 0; k < n; k++) {
     if (!doc_bad[k]) continue;
     if (!refused) {   // strict: one refused document refuses the batch
-      why = doc_bad[k] < 10 ? kWhy[doc_bad[k]] : "refused";
+      why = doc_bad[k] < 12 ? kWhy[doc_bad[k]] : "refused";
+      if (diag) {
+        uint32_t at = 0;
+        JCHK(hipMemcpy(&at, d_bad_at.p + k, 4, hipMemcpyDeviceToHost));
+        why += " (document " + std::to_string(k);
+        if (at != 0xFFFFFFFFu && at <= lens[k]) {
+          const size_t a = at > 40 ? at - 40 : 0;
+          why += ", byte " + std::to_string(at) + ": ..." + std::string(texts[k] + a, std::min<size_t>(lens[k] - a, 80)) + "...";
+        }
+        why += ")";
+      }
       if (resizer.joinable()) resizer.join();
       out.clear();
       return false;

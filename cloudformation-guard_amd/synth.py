@@ -257,3 +257,135 @@ def config_snapshot_doc(i, n_groups=4):
 
 def config_corpus(n, start=0, n_groups=4):
     return [json.dumps(config_snapshot_doc(start + i, n_groups), separators=(",", ":")) for i in range(n)]
+
+
+# ---- CloudFormation YAML (block style) -------------------------------------------------------------
+# The cfn_doc templates written as YAML the way CloudFormation authors write them: block mappings,
+# indented and indentless sequences, compact `- Key: v` entries, flow sequences of scalars, short-form
+# intrinsic tags (!Ref, !GetAtt, !Sub, !Join ...), plain / single- / double-quoted scalars and comments,
+# with the choices drawn from a XorShift32 per document (deterministic).  The device YAML loader and the
+# host libyaml loader must build the same arena from it (tests/test_gpu_yaml.py).
+
+_YAML_INDICATORS = set("-?:,[]{}#&*!|>'\"%@`")
+_YAML_WORDS = {"true", "false", "yes", "no", "on", "off", "y", "n", "~", "null", "Null", "NULL", "True", "False",
+               "TRUE", "FALSE", "Yes", "No", "YES", "NO", "On", "Off", "ON", "OFF", "Y", "N"}
+_FN_SHORT = {"Ref": ("Ref", True, False), "Fn::GetAtt": ("GetAtt", True, True), "Fn::Sub": ("Sub", True, True),
+             "Fn::Base64": ("Base64", True, False), "Fn::Join": ("Join", False, True),
+             "Fn::Select": ("Select", False, True), "Fn::If": ("If", False, True), "Fn::Equals": ("Equals", False, True),
+             "Fn::FindInMap": ("FindInMap", False, True), "Fn::ImportValue": ("ImportValue", True, False)}
+
+
+def _numeric_like(s):
+    t = s[1:] if s[:1] in "+-" else s
+    if t.lower() in ("inf", "infinity", "nan"):
+        return True
+    digits = any(c.isdigit() for c in t)
+    return digits and all(c.isdigit() or c in ".eE+-" for c in t)
+
+
+def _plain_ok(s, flow=False):
+    if not s or s != s.strip() or s in _YAML_WORDS or _numeric_like(s):
+        return False
+    if s[0] in _YAML_INDICATORS or ": " in s or " #" in s or s.endswith(":") or "\n" in s:
+        return False
+    if any(ord(c) < 0x20 or ord(c) == 0x7F or ord(c) > 0x7E for c in s):
+        return False
+    if flow and any(c in s for c in ",[]{}:"):
+        return False
+    return True
+
+
+def _yaml_scalar(v, rng, flow=False):
+    if v is None:
+        return "null" if rng.next() % 2 else "~"
+    if v is True or v is False:
+        return "true" if v else "false"
+    if isinstance(v, int):
+        return str(v)
+    if isinstance(v, float):
+        return json.dumps(v)
+    s = str(v)
+    pick = rng.next() % 5
+    if _plain_ok(s, flow) and pick < 3:
+        return s
+    if pick == 3 and "\\" not in s and all(0x20 <= ord(c) < 0x7F for c in s):
+        return "'" + s.replace("'", "''") + "'"
+    return json.dumps(s, ensure_ascii=False)
+
+
+def _yaml_key(k, rng):
+    return k if _plain_ok(k) and rng.next() % 6 else json.dumps(k, ensure_ascii=False)
+
+
+def _yaml_fn(v, rng):
+    """a short-form tag for a one-key intrinsic function map, or None"""
+    if not isinstance(v, dict) or len(v) != 1:
+        return None
+    (k, x), = v.items()
+    if k not in _FN_SHORT or rng.next() % 4 == 0:
+        return None
+    short, single, seq = _FN_SHORT[k]
+    if single and isinstance(x, str) and _plain_ok(x):
+        return "!%s %s" % (short, x)
+    if seq and isinstance(x, list) and x and all(isinstance(e, (str, int)) and (not isinstance(e, str) or _plain_ok(e, True))
+                                                 for e in x):
+        return "!%s [%s]" % (short, ", ".join(str(e) for e in x))
+    return None
+
+
+def _yaml_lines(v, indent, rng, out):
+    pad = " " * indent
+    if isinstance(v, dict):
+        for k, x in v.items():
+            if rng.next() % 13 == 0:
+                out.append(pad + "# " + str(k).lower())
+            key = _yaml_key(k, rng)
+            fn = _yaml_fn(x, rng)
+            if fn is not None:
+                out.append("%s%s: %s" % (pad, key, fn))
+            elif isinstance(x, dict) and x:
+                out.append("%s%s:" % (pad, key))
+                _yaml_lines(x, indent + 2, rng, out)
+            elif isinstance(x, list) and x:
+                if all(not isinstance(e, (dict, list)) for e in x) and rng.next() % 3 == 0 and \
+                        all(not isinstance(e, str) or _plain_ok(e, True) for e in x):
+                    out.append("%s%s: [%s]" % (pad, key, ", ".join(_yaml_scalar(e, rng, True) for e in x)))
+                else:
+                    out.append("%s%s:" % (pad, key))
+                    _yaml_lines(x, indent + (2 if rng.next() % 2 else 0), rng, out)
+            elif isinstance(x, dict):
+                out.append("%s%s: {}" % (pad, key))
+            elif isinstance(x, list):
+                out.append("%s%s: []" % (pad, key))
+            else:
+                tail = "  # note" if rng.next() % 17 == 0 else ""
+                out.append("%s%s: %s%s" % (pad, key, _yaml_scalar(x, rng), tail))
+    else:
+        for x in v:
+            if isinstance(x, dict) and x and _yaml_fn(x, rng) is None:
+                sub = []
+                _yaml_lines(x, indent + 2, rng, sub)
+                out.append(pad + "- " + sub[0][indent + 2:])
+                out.extend(sub[1:])
+            elif isinstance(x, list) and x:
+                out.append(pad + "-")
+                _yaml_lines(x, indent + 2, rng, out)
+            elif isinstance(x, (dict, list)):
+                fn = _yaml_fn(x, rng)
+                out.append(pad + "- " + (fn if fn else ("{}" if isinstance(x, dict) else "[]")))
+            else:
+                out.append(pad + "- " + _yaml_scalar(x, rng))
+
+
+def cfn_yaml_doc(i, n_resources=50):
+    """synthetic template i (cfn_doc's content) as block-style CloudFormation YAML"""
+    rng = XorShift32(0x9E3779B9 ^ (i * 2654435761 & 0xFFFFFFFF) or 1)
+    out = ["---"] if rng.next() % 3 == 0 else []
+    if rng.next() % 2:
+        out.append("# synthetic template %d" % i)
+    _yaml_lines(cfn_doc(i, n_resources), 0, rng, out)
+    return "\n".join(out) + "\n"
+
+
+def cfn_yaml_corpus(n, start=0, n_resources=50):
+    return [cfn_yaml_doc(start + i, n_resources) for i in range(n)]
