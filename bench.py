@@ -204,6 +204,9 @@ def main():
                     help="documents whose structured report is rendered for e2e (0: all, the default); a sample's "
                          "report time is scaled to the whole job")
     ap.add_argument("--resources", type=int, default=50)
+    ap.add_argument("--format", choices=("json", "yaml"), default="json",
+                    help="cfg2/cfg3 synthetic templates as JSON, or as block-style CloudFormation YAML "
+                         "(synth.cfn_yaml_doc; the device YAML loader, csrc/yaml_gpu.inc)")
     ap.add_argument("--threads", type=int, default=0, help="host loader threads (default: CPU share)")
     ap.add_argument("--loader", choices=("device", "host"), default="device",
                     help="document loader: the MI355X JSON loader (csrc/json_gpu.hip; documents outside its "
@@ -282,7 +285,7 @@ def main():
             sess.add_docs(texts, names, threads=threads)
         texts = None
     elif args.loader == "device":
-        load_stats = sess.add_synthetic_device(first, count, n_resources=args.resources, threads=threads)
+        load_stats = sess.add_synthetic_device(first, count, n_resources=args.resources, threads=threads, fmt=args.format)
         if load_stats is None:
             raise RuntimeError("device loader refused the synthetic corpus")
         t_gen = load_stats["gen_ms"] / 1e3
@@ -410,7 +413,7 @@ def main():
                        "(rendered for report_docs_rendered documents; report_s scaled to all when that is fewer; "
                        "reporter=device: rendered on the MI355X and copied to host memory in blocks); "
                        "synthetic text generation (gen_s) is not part of the job%s"
-                       % ("device JSON loader: text H2D, parse, arena D2H for the reporter" if args.loader == "device"
+                       % (("device %s loader: text H2D, parse, intern index to the host (the arena stays in HBM)" % args.format.upper()) if args.loader == "device"
                           else "host loader threads", " (inside load_s with --loader host)" if gen_in_load else "")}
 
     total_units = ntiles * world * args.steps
@@ -424,6 +427,8 @@ def main():
     else:
         workload = "%s: %d synthetic CFN templates/GPU (%d resources) x %d-file rule pack" % (
             args.workload, args.docs, args.resources, nfiles)
+        if args.format == "yaml":
+            workload += " (block-style YAML text)"
     if rank == 0:
         traffic = load_pmc(workload)
         line = {

@@ -2588,6 +2588,17 @@ size_t gg_synth_cfn_doc(uint64_t index, int32_t n_resources, char* buf, size_t c
   return t.size();
 }
 
+size_t gg_synth_cfn_yaml_doc(uint64_t index, int32_t n_resources, char* buf, size_t cap) {
+  std::string t;
+  cfn_synth_yaml_doc(index, n_resources, t);
+  if (buf && cap) {
+    size_t n = std::min(cap - 1, t.size());
+    memcpy(buf, t.data(), n);
+    buf[n] = 0;
+  }
+  return t.size();
+}
+
 int32_t gg_session_add_synthetic(gg_session* s, uint64_t first, size_t n, int32_t n_resources, int32_t nthreads,
                                  extern_err_t* err) {
   set_err(err, 0, "");
@@ -2709,8 +2720,8 @@ int32_t gg_session_add_docs_device(gg_session* s, const char* const* texts, cons
   } catch (std::exception& e) { set_err(err, -1, e.what()); return -1; }
 }
 
-int32_t gg_session_add_synthetic_device(gg_session* s, uint64_t first, size_t n, int32_t n_resources, int32_t nthreads,
-                                        double* stats, extern_err_t* err) {
+int32_t gg_session_add_synthetic_device_fmt(gg_session* s, uint64_t first, size_t n, int32_t n_resources, int32_t nthreads,
+                                            int32_t format, double* stats, extern_err_t* err) {
   set_err(err, 0, "");
   try {
     if (nthreads < 1) nthreads = 1;
@@ -2718,8 +2729,9 @@ int32_t gg_session_add_synthetic_device(gg_session* s, uint64_t first, size_t n,
     std::vector<std::string> texts(n), names(n);
     auto work = [&](int t) {
       for (size_t i = n * t / nthreads; i < n * (t + 1) / nthreads; i++) {
-        cfn_synth_doc(first + i, n_resources, texts[i]);
-        names[i] = "synthetic-" + std::to_string(first + i) + ".json";
+        if (format == 1) cfn_synth_yaml_doc(first + i, n_resources, texts[i]);
+        else cfn_synth_doc(first + i, n_resources, texts[i]);
+        names[i] = "synthetic-" + std::to_string(first + i) + (format == 1 ? ".yaml" : ".json");
       }
     };
     parallel_run((size_t)nthreads, work);
@@ -2739,6 +2751,11 @@ int32_t gg_session_add_synthetic_device(gg_session* s, uint64_t first, size_t n,
       fprintf(stderr, "[load] generated text freed %8.1f ms\n", std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - f0).count());
     return rc;
   } catch (std::exception& e) { set_err(err, -1, e.what()); return -1; }
+}
+
+int32_t gg_session_add_synthetic_device(gg_session* s, uint64_t first, size_t n, int32_t n_resources, int32_t nthreads,
+                                        double* stats, extern_err_t* err) {
+  return gg_session_add_synthetic_device_fmt(s, first, n, n_resources, nthreads, 0, stats, err);
 }
 
 // Parity of the device loader with the host loader on the same documents: 1 = the same arena up

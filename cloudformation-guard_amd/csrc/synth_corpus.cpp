@@ -8,6 +8,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <vector>
 
 namespace gg {
 
@@ -191,6 +192,175 @@ void cfn_synth_doc(uint64_t index, int n_resources, std::string& s) {
     resource(r, t, k, o);
   }
   o.raw("}}");
+}
+
+// ---- block-style YAML (synth.py cfn_yaml_doc, byte-identical; tests/test_synth_cpu.py) ------------------
+namespace {
+
+// the generator's JSON as a tree (its own compact output: strings without escapes, ints, bools)
+struct YV {
+  int kind = 0;   // 0 string, 1 int, 2 bool, 3 map, 4 list
+  std::string s;
+  long long i = 0;
+  bool b = false;
+  std::vector<std::pair<std::string, YV>> m;
+  std::vector<YV> a;
+};
+
+struct JP {
+  const std::string& t;
+  size_t p = 0;
+  std::string str() {
+    std::string r;
+    p++;
+    while (t[p] != '"') r += t[p++];
+    p++;
+    return r;
+  }
+  YV val() {
+    YV v;
+    const char c = t[p];
+    if (c == '"') { v.kind = 0; v.s = str(); }
+    else if (c == '{') {
+      v.kind = 3; p++;
+      while (t[p] != '}') { std::string k = str(); p++; YV x = val(); v.m.emplace_back(std::move(k), std::move(x)); if (t[p] == ',') p++; }
+      p++;
+    } else if (c == '[') {
+      v.kind = 4; p++;
+      while (t[p] != ']') { v.a.push_back(val()); if (t[p] == ',') p++; }
+      p++;
+    } else if (c == 't' || c == 'f') { v.kind = 2; v.b = c == 't'; p += v.b ? 4 : 5; }
+    else { v.kind = 1; size_t e = p; while (t[e] == '-' || (t[e] >= '0' && t[e] <= '9')) e++; v.i = std::stoll(t.substr(p, e - p)); p = e; }
+    return v;
+  }
+};
+
+bool numeric_like(const std::string& s) {
+  std::string t = (!s.empty() && (s[0] == '+' || s[0] == '-')) ? s.substr(1) : s;
+  std::string low;
+  for (char c : t) low += (char)tolower((unsigned char)c);
+  if (low == "inf" || low == "infinity" || low == "nan") return true;
+  bool digits = false, all = true;
+  for (char c : t) {
+    if (c >= '0' && c <= '9') digits = true;
+    else if (!(c == '.' || c == 'e' || c == 'E' || c == '+' || c == '-')) all = false;
+  }
+  return digits && all;
+}
+
+bool plain_ok(const std::string& s, bool flow = false) {
+  static const char* const words[] = {"true", "false", "yes", "no", "on", "off", "y", "n", "~", "null", "Null", "NULL", "True",
+                                      "False", "TRUE", "FALSE", "Yes", "No", "YES", "NO", "On", "Off", "ON", "OFF", "Y", "N"};
+  if (s.empty() || s.front() == ' ' || s.back() == ' ' || s.front() == '\n' || s.back() == '\n') return false;
+  for (const char* w : words) if (s == w) return false;
+  if (numeric_like(s)) return false;
+  if (std::string("-?:,[]{}#&*!|>'\"%@`").find(s[0]) != std::string::npos) return false;
+  if (s.find(": ") != std::string::npos || s.find(" #") != std::string::npos || s.back() == ':' || s.find('\n') != std::string::npos) return false;
+  for (unsigned char c : s) if (c < 0x20 || c >= 0x7F) return false;
+  if (flow) for (char c : s) if (std::string(",[]{}:").find(c) != std::string::npos) return false;
+  return true;
+}
+
+std::string jdump(const std::string& s) {
+  std::string r = "\"";
+  for (char c : s) { if (c == '"' || c == '\\') r += '\\'; r += c; }
+  return r + "\"";
+}
+
+std::string yscalar(const YV& v, XorShift32& r, bool flow = false) {
+  if (v.kind == 2) return v.b ? "true" : "false";
+  if (v.kind == 1) return std::to_string(v.i);
+  const uint32_t pick = r.next() % 5u;
+  if (plain_ok(v.s, flow) && pick < 3) return v.s;
+  bool simple = v.s.find('\\') == std::string::npos;
+  for (unsigned char c : v.s) if (c < 0x20 || c >= 0x7F) simple = false;
+  if (pick == 3 && simple) {
+    std::string q = "'";
+    for (char c : v.s) { q += c; if (c == '\'') q += '\''; }
+    return q + "'";
+  }
+  return jdump(v.s);
+}
+
+std::string ykey(const std::string& k, XorShift32& r) { return (plain_ok(k) && r.next() % 6u) ? k : jdump(k); }
+
+std::string lower(const std::string& s) {
+  std::string r;
+  for (char c : s) r += (char)tolower((unsigned char)c);
+  return r;
+}
+
+void ylines(const YV& v, int indent, XorShift32& r, std::vector<std::string>& out) {
+  const std::string pad(indent, ' ');
+  if (v.kind == 3) {
+    for (auto& kv : v.m) {
+      const YV& x = kv.second;
+      if (r.next() % 13u == 0) out.push_back(pad + "# " + lower(kv.first));
+      const std::string key = ykey(kv.first, r);
+      if (x.kind == 3 && !x.m.empty()) {
+        out.push_back(pad + key + ":");
+        ylines(x, indent + 2, r, out);
+      } else if (x.kind == 4 && !x.a.empty()) {
+        bool scalars = true;
+        for (auto& e : x.a) if (e.kind >= 3) scalars = false;
+        bool flow = false;
+        if (scalars && r.next() % 3u == 0) {
+          flow = true;
+          for (auto& e : x.a) if (e.kind == 0 && !plain_ok(e.s, true)) flow = false;
+        }
+        if (flow) {
+          std::string f;
+          for (size_t j = 0; j < x.a.size(); j++) { if (j) f += ", "; f += yscalar(x.a[j], r, true); }
+          out.push_back(pad + key + ": [" + f + "]");
+        } else {
+          out.push_back(pad + key + ":");
+          ylines(x, indent + (r.next() % 2u ? 2 : 0), r, out);
+        }
+      } else if (x.kind == 3) {
+        out.push_back(pad + key + ": {}");
+      } else if (x.kind == 4) {
+        out.push_back(pad + key + ": []");
+      } else {
+        const std::string tail = r.next() % 17u == 0 ? "  # note" : "";
+        out.push_back(pad + key + ": " + yscalar(x, r) + tail);
+      }
+    }
+  } else {
+    for (auto& x : v.a) {
+      if (x.kind == 3 && !x.m.empty()) {
+        std::vector<std::string> sub;
+        ylines(x, indent + 2, r, sub);
+        out.push_back(pad + "- " + sub[0].substr(indent + 2));
+        for (size_t j = 1; j < sub.size(); j++) out.push_back(sub[j]);
+      } else if (x.kind == 4 && !x.a.empty()) {
+        out.push_back(pad + "-");
+        ylines(x, indent + 2, r, out);
+      } else if (x.kind >= 3) {
+        out.push_back(pad + "- " + (x.kind == 3 ? "{}" : "[]"));
+      } else {
+        out.push_back(pad + "- " + yscalar(x, r));
+      }
+    }
+  }
+}
+
+}  // namespace
+
+void cfn_synth_yaml_doc(uint64_t index, int n_resources, std::string& out) {
+  std::string json;
+  cfn_synth_doc(index, n_resources, json);
+  JP jp{json};
+  const YV root = jp.val();
+  uint32_t seed = 0x9E3779B9u ^ (uint32_t)((index * 2654435761ull) & 0xFFFFFFFFull);
+  if (!seed) seed = 1;
+  XorShift32 r(seed);
+  std::vector<std::string> lines;
+  if (r.next() % 3u == 0) lines.push_back("---");
+  if (r.next() % 2u) lines.push_back("# synthetic template " + std::to_string(index));
+  ylines(root, 0, r, lines);
+  out.clear();
+  for (size_t j = 0; j < lines.size(); j++) { if (j) out += '\n'; out += lines[j]; }
+  out += '\n';
 }
 
 }  // namespace gg

@@ -146,6 +146,8 @@ def lib():
     L.gg_session_kernel_stats.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
     L.gg_synth_cfn_doc.argtypes = [ctypes.c_uint64, ctypes.c_int32, ctypes.c_char_p, ctypes.c_size_t]
     L.gg_synth_cfn_doc.restype = ctypes.c_size_t
+    L.gg_synth_cfn_yaml_doc.argtypes = [ctypes.c_uint64, ctypes.c_int32, ctypes.c_char_p, ctypes.c_size_t]
+    L.gg_synth_cfn_yaml_doc.restype = ctypes.c_size_t
     L.gg_session_add_synthetic.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_int32,
                                            ctypes.c_int32, ctypes.POINTER(ExternError)]
     L.gg_session_add_docs_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_size_t),
@@ -157,6 +159,9 @@ def lib():
                                          ctypes.POINTER(ExternError)]
     L.gg_load_dump.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int32, ctypes.POINTER(ExternError)]
     L.gg_load_dump.restype = ctypes.c_void_p
+    L.gg_session_add_synthetic_device_fmt.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_int32,
+                                                      ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_double),
+                                                      ctypes.POINTER(ExternError)]
     L.gg_parse_rules.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(ExternError)]
     L.gg_parse_rules.restype = ctypes.c_int32
     L.gg_regex_match.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint32)]
@@ -478,10 +483,11 @@ class Session:
         rc = lib().gg_session_add_docs_device(self.s, T, Ls, N, n, st, ctypes.byref(err))
         return _load_result(rc, err, st)
 
-    def add_synthetic_device(self, first, n, n_resources=50, threads=8):
+    def add_synthetic_device(self, first, n, n_resources=50, threads=8, fmt="json"):
         st = (ctypes.c_double * len(LOAD_STATS))()
         err = ExternError()
-        rc = lib().gg_session_add_synthetic_device(self.s, first, n, n_resources, threads, st, ctypes.byref(err))
+        rc = lib().gg_session_add_synthetic_device_fmt(self.s, first, n, n_resources, threads, {"json": 0, "yaml": 1}[fmt], st,
+                                                        ctypes.byref(err))
         return _load_result(rc, err, st)
 
     def upload(self):
@@ -674,6 +680,14 @@ class Session:
         if self.stat(self.STAT["fail"]) > 0 and not (output == "junit" and parse):
             return 19
         return 5 if parse else 0
+
+
+def synth_cfn_yaml_doc(index, n_resources=50):
+    """Native synthetic template as block-style YAML (byte-identical to synth.cfn_yaml_doc; no GPU needed)."""
+    n = lib().gg_synth_cfn_yaml_doc(index, n_resources, None, 0)
+    buf = ctypes.create_string_buffer(n + 1)
+    lib().gg_synth_cfn_yaml_doc(index, n_resources, buf, n + 1)
+    return buf.value.decode("utf-8")
 
 
 def synth_cfn_doc(index, n_resources=50):

@@ -232,6 +232,8 @@ int32_t gg_regex_match(const char *pattern, const char *text, size_t len, uint32
 
 /* Synthetic CloudFormation corpus (BASELINE configs[1]); byte-identical to synth.py cfn_doc. */
 size_t gg_synth_cfn_doc(uint64_t index, int32_t n_resources, char *buf, size_t cap);
+/* the same template as block-style CloudFormation YAML (byte-identical to synth.py cfn_yaml_doc) */
+size_t gg_synth_cfn_yaml_doc(uint64_t index, int32_t n_resources, char *buf, size_t cap);
 int32_t gg_session_add_synthetic(gg_session *s, uint64_t first, size_t n, int32_t n_resources, int32_t nthreads,
                                  extern_err_t *err);
 
@@ -251,6 +253,9 @@ int32_t gg_session_add_docs_device(gg_session *s, const char *const *texts, cons
                                    size_t n, double *stats, extern_err_t *err);
 int32_t gg_session_add_synthetic_device(gg_session *s, uint64_t first, size_t n, int32_t n_resources, int32_t nthreads,
                                         double *stats, extern_err_t *err);
+/* gg_session_add_synthetic_device with the corpus written as format 0 JSON or 1 block-style YAML */
+int32_t gg_session_add_synthetic_device_fmt(gg_session *s, uint64_t first, size_t n, int32_t n_resources, int32_t nthreads,
+                                            int32_t format, double *stats, extern_err_t *err);
 /* Host diagnostic: the device loader's float parser (Eisel-Lemire, csrc/eisel_lemire.h) on the JSON
  * number s[0..n): 1 = *out is the correctly rounded double, 0 = refused (its document loads on the host). */
 int32_t gg_parse_f64(const char *s, size_t n, double *out);

@@ -125,3 +125,20 @@ def test_device_loaded_yaml_with_refused_documents():
     s.eval(1)
     assert s.report("json") == (exp, ecode)
     s.close()
+
+
+def test_reference_yaml_fixtures():
+    """the reference's own YAML data files (tests/golden, from guard/resources): each one the device takes
+    builds the host's arena; the rest are refused, never built differently"""
+    import glob
+    import os
+    root = os.path.join(os.path.dirname(__file__), "golden")
+    files = sorted(glob.glob(os.path.join(root, "**", "*.yaml"), recursive=True))
+    files = [f for f in files if "rulepack" not in f]
+    taken = 0
+    for f in files:
+        text = open(f, encoding="utf-8").read()
+        rc, msg = guard_amd.loader_device_check([text])
+        assert rc != 0, (f, msg)
+        taken += rc == 1
+    assert taken >= 6, taken

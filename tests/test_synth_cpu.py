@@ -11,3 +11,13 @@ def test_native_generator_matches_python():
 def test_native_generator_resource_counts():
     for nres in (0, 1, 7):
         assert guard_amd.synth_cfn_doc(5, nres) == synth.cfn_corpus(1, start=5, n_resources=nres)[0]
+
+
+def test_native_yaml_generator_matches_python():
+    """gg_synth_cfn_yaml_doc (synth_corpus.cpp) writes synth.cfn_yaml_doc's bytes, and the YAML reads back
+    as the template cfn_doc builds"""
+    import yaml
+    for i in list(range(40)) + [12345, 999999]:
+        assert guard_amd.synth_cfn_yaml_doc(i, 12) == synth.cfn_yaml_doc(i, 12), i
+    for i in range(20):
+        assert yaml.safe_load(synth.cfn_yaml_doc(i, 30)) == synth.cfn_doc(i, 30)
