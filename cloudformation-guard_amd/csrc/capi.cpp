@@ -515,6 +515,7 @@ void session_upload(gg_session* s) {
     if (s->dev_nodes && !s->resident.nodes) { hipFree(s->dev_nodes); s->dev_nodes = nullptr; s->dev_nodes_n = 0; }
     if (b & 1u) throw std::runtime_error("a string or container is too large for the device arena (count >= 2^28)");
     if (b & 2u) throw std::runtime_error("arena invariant broken: a map entry's key offset is not its key id");
+    if (b & 4u) throw std::runtime_error("arena invariant broken: a string id is not a 16-byte pool slot");
     mark("packed");
   }
   s->dv->d_bytes.upload(s->docs.bytes.data(), s->docs.bytes.size() ? s->docs.bytes.size() : 1, st);

@@ -56,6 +56,11 @@ struct default_init_allocator : std::allocator<T> {
 template <class T>
 using column = std::vector<T, default_init_allocator<T>>;
 
+// Append-only once a device copy exists: the device loader keeps its HBM copy of nodes[0, n) (and a
+// resident arena keeps every column there, capi.cpp ensure_host_arena), and the session's next upload
+// packs the evaluator's arena from that copy while the reporter reads the host columns.  Mutators may
+// append documents (merge_batches, merge_into_last, grow_zeroed past the end) but must not rewrite an
+// existing node; a path that did would have to drop the device copy (gg_session dev_nodes) first.
 struct DocBatch {
   column<DNode> nodes;
   std::string bytes;

@@ -456,6 +456,8 @@ __global__ void __launch_bounds__(256) pack_nodes_kernel(const DNode* in, DNodeP
     const DNode d = in[i];
     if (d.count > kMaxPackedCount) atomicOr(bad, 1u);
     if (d.key_off != NONE && d.key_off != d.key_hash) atomicOr(bad, 2u);
+    // the regex memo (eval_core.inc regex_match_ref) is keyed by a string's 16-byte pool slot
+    if (d.kind == K_STRING && (d.a & 15u)) atomicOr(bad, 4u);
     DNodeP p;
     p.kc = d.kind | (d.count << 4); p.a = d.a; p.b = d.b; p.key_hash = d.key_off != NONE ? d.key_hash : 0u;
     out[i] = p;

@@ -53,6 +53,7 @@ enum : uint32_t {
   BAD_VERIFY = 7, BAD_SIZE = 8, BAD_WIDE = 9,
   BAD_NOTJSON = 10,   // count pass: not a JSON document (the YAML passes take it, yaml_gpu.inc)
   BAD_YAML = 11,      // outside the block-style YAML subset the YAML passes parse
+  BAD_WIDEMAP = 12,   // a map with more keys than the verify pass's duplicate-key scan takes
 };
 static const uint32_t kMaxDepth = 64;
 static const uint32_t kMaxPairwiseKeys = 256;
@@ -509,7 +510,7 @@ __device__ void parse_doc(const JArgs& A, uint32_t d) {
         ekey = slot; elen = len;
         ekpos = (uint32_t)kstart; ekl = kl; ekc = kc;
         // duplicate keys are found by the fix / verify pass; maps past its scan bound are refused
-        if (F.j >= kMaxPairwiseKeys) { bad(BAD_DUPKEY); return; }
+        if (F.j >= kMaxPairwiseKeys) { bad(BAD_WIDEMAP); return; }
       }
       while (T.at(i) == ' ') i++;
       if (T.at(i) != ':' || line != kl || i - kstart > 1000) { bad(BAD_SYNTAX); return; }
@@ -659,10 +660,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_JSO
       A.nodes[nb + r] = x;
       A.line[nb + r] = rec.line; A.col[nb + r] = rec.col; A.kline[nb + r] = rec.kline; A.kcol[nb + r] = rec.kcol;
     }
-    const bool any_dup = __ballot(dup) != 0;
-    if (any_dup || __ballot(!ok)) {
+    // a bytes mismatch explains an apparent duplicate (two keys of one map sharing a fingerprint): the
+    // collision is the reason then; a duplicate whose occurrences all match their pool bytes is real
+    const bool any_dup = __ballot(dup) != 0, any_bad = __ballot(!ok) != 0;
+    if (any_dup || any_bad) {
       kill();
-      if (lane == 0) A.doc_bad[d] = any_dup ? BAD_DUPKEY : BAD_VERIFY;
+      if (lane == 0) A.doc_bad[d] = any_bad ? BAD_VERIFY : BAD_DUPKEY;
     }
   }
 }
@@ -795,7 +798,8 @@ bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, 
   static const char* kWhy[] = {"", "outside the strict-JSON subset", "nesting deeper than 64", "duplicate map keys",
                                "a number the host types (beyond 64 bits, or an infinite / undecided float)", "string table full", "string pool full",
                                "string fingerprint collision", "batch too large", "a container with more than 65535 elements",
-                               "not a JSON document (YAML device parser off)", "outside the block-style YAML subset"};
+                               "not a JSON document (YAML device parser off)", "outside the block-style YAML subset",
+                               "a map with more than 256 keys"};
   if (!out.nodes.empty() || !out.roots.empty()) { why = "the device loader fills an empty batch"; return false; }
   if (n == 0) return true;
   if (n > 0xFFFFFFF0ull) { why = kWhy[BAD_SIZE]; return false; }
@@ -840,7 +844,12 @@ bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, 
   JArgs A{};
   A.text = d_text.p; A.off = d_off.p; A.ndocs = (uint32_t)n;
   A.fp_mask = ~0ull;
-  if (const char* e = getenv("GG_JSON_FP_MASK")) A.fp_mask = strtoull(e, nullptr, 0);   // tests: forced collisions
+  if (const char* e = getenv("GG_JSON_FP_MASK")) {
+    // tests only: narrowed fingerprints collide, and every colliding document falls back to the host
+    A.fp_mask = strtoull(e, nullptr, 0);
+    static bool warned = false;
+    if (!warned) { warned = true; fprintf(stderr, "cfn-guard-mi355x: GG_JSON_FP_MASK=%s narrows the device loader's string fingerprints (test setting)\n", e); }
+  }
   A.n_nodes = d_nn.p; A.n_cont = d_nc.p; A.n_str = d_ns.p; A.bad = d_bad.p; A.doc_bad = d_doc_bad.p; A.is_yaml = d_yaml.p; A.bad_at = diag ? d_bad_at.p : nullptr;
   DevArr<uint16_t> d_counts; d_counts.alloc(total / 2 + 1);
   A.counts = d_counts.p;
@@ -849,7 +858,7 @@ bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, 
   auto bad_now = [&]() {
     uint32_t b = 0;
     JCHK(hipMemcpy(&b, d_bad.p, 4, hipMemcpyDeviceToHost));
-    if (b) why = b < 12 ? kWhy[b] : "refused";
+    if (b) why = b < 13 ? kWhy[b] : "refused";
     return b != 0;
   };
 
@@ -974,7 +983,7 @@ bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, 
   for (size_t k = 0; k < n; k++) {
     if (!doc_bad[k]) continue;
     if (!refused) {   // strict: one refused document refuses the batch
-      why = doc_bad[k] < 12 ? kWhy[doc_bad[k]] : "refused";
+      why = doc_bad[k] < 13 ? kWhy[doc_bad[k]] : "refused";
       if (diag) {
         uint32_t at = 0;
         JCHK(hipMemcpy(&at, d_bad_at.p + k, 4, hipMemcpyDeviceToHost));

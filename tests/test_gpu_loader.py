@@ -265,3 +265,21 @@ def test_intern_table_doubles_when_full(monkeypatch):
     st = s.add_docs_device(docs, ["d%d.json" % i for i in range(len(docs))])
     s.close()
     assert st is not None and st["table_retries"] >= 1 and st["distinct_strings"] == 1500 * 61
+
+
+def test_key_fingerprint_collision_is_a_collision(monkeypatch):
+    """two different keys of one map sharing a narrowed fingerprint: the verify pass names the collision
+    (BAD_VERIFY), not a duplicate key; a true duplicate stays a duplicate"""
+    monkeypatch.setenv("GG_JSON_FP_MASK", "0x1")
+    doc = "{" + ", ".join('"key-%d": %d' % (i, i) for i in range(12)) + "}"
+    rc, msg = guard_amd.loader_device_check([doc])
+    assert rc == -1 and "collision" in msg, msg
+    monkeypatch.delenv("GG_JSON_FP_MASK")
+    rc, msg = guard_amd.loader_device_check(['{"a": 1, "b": 2, "a": 3}'])
+    assert rc == -1 and "duplicate" in msg, msg
+
+
+def test_wide_map_reason():
+    doc = "{" + ", ".join('"k%d": %d' % (i, i) for i in range(300)) + "}"
+    rc, msg = guard_amd.loader_device_check([doc])
+    assert rc == -1 and "more than 256 keys" in msg, msg
