@@ -111,7 +111,7 @@ struct Text {
   uint64_t wb;
   __device__ Text(const uint8_t* t, uint64_t b, uint64_t len) : s(t), base(b), n(len), wb(~0ull) {}
   // byte i of the document, 256 past its end
-  __device__ uint32_t at(uint64_t i) {
+  __device__ __attribute__((always_inline)) uint32_t at(uint64_t i) {
     if (i >= n) return 256u;
     const uint64_t g = base + i, a = g & ~15ull;
     if (a != wb) { w = *(const uint4*)(s + a); wb = a; }
