@@ -124,7 +124,10 @@ struct Devices {
     if (hipSetDevice(d) != hipSuccess) { why = "hipSetDevice failed"; return false; }
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, d) == hipSuccess) D.ncu = prop.multiProcessorCount;
-    hipDeviceSetLimit(hipLimitStackSize, 16384);
+    // the evaluator recurses (eval_conj <-> clauses, filters, rule references): 16 KB of lane stack.  32 KB
+    // cannot be had with several queues live (HSA_STATUS_ERROR_OUT_OF_RESOURCES in the concurrent-caller
+    // test); GG_STACK_BYTES overrides
+    hipDeviceSetLimit(hipLimitStackSize, getenv("GG_STACK_BYTES") ? (size_t)atol(getenv("GG_STACK_BYTES")) : (size_t)16384);
     D.ready = true;
     return true;
   }
