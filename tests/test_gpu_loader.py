@@ -90,7 +90,7 @@ def test_arena_parity_fixture_json():
 
 
 @pytest.mark.parametrize("doc,why", [
-    ("Resources: |\n  a\n", "YAML subset"),   # block scalar: outside the YAML subset too
+    ("Resources: &x\n  a: 1\n", "YAML subset"),   # an anchor: outside the YAML subset too
     ('{"a": 1, "a": 2}', "duplicate"),
     ("[" * 70 + "]" * 70, "deeper"),
     ('{"x": 1e400}', "float"),
@@ -130,7 +130,7 @@ def test_session_refused_documents_load_on_the_host():
     report equals a host-loaded session's and the oracle's"""
     rules = rule_pack()
     base = synth.cfn_corpus(12, start=700, n_resources=15)
-    odd = ['Resources:\n  b:\n    Type: AWS::S3::Bucket\n    Properties: {BucketName: x}\n    Metadata: |\n      block\n',
+    odd = ['Resources:\n  b:\n    Type: AWS::S3::Bucket\n    Properties: {BucketName: x}\n    Metadata: &a x\n',
            '{"Resources": {"a": {"Type": "AWS::S3::Bucket"}, "a": {"Type": "AWS::IAM::Role"}}}',
            '{"Resources": {"v": {"Type": "AWS::EC2::Volume", "Properties": {"Size": 99999999999999999999}}}}',
            UTF8_DOCS[1]]
@@ -140,7 +140,7 @@ def test_session_refused_documents_load_on_the_host():
     for name, text in rules:
         s.add_rules(text, name)
     st = s.add_docs_device(texts, names)
-    assert st is not None and st["refused_docs"] == 3   # the block-scalar YAML, duplicate-key and beyond-u64 documents
+    assert st is not None and st["refused_docs"] == 3   # the anchored YAML, duplicate-key and beyond-u64 documents
     s.eval(1)
     dev = s.report()
     s.close()

@@ -38,6 +38,12 @@ EDGE = [
     "s: 'it''s'\nt: \"tab\\tand\\u00e9 \\\"q\\\"\"\nu: plain, with commas [and] brackets # c\nv: a:b\n",
     "Resources:\n  X:\n    Type: T\n    DependsOn:\n    - A\n    - B\n    Properties: {}\n    Y: []\n  Z:\n    Type: U\n",
     "- a\n- b: 1\n  c: [x]\n- - 1\n  - 2\n",
+    # block scalars: literal / folded, clip / strip / keep, more-indented literal lines, tags, in lists and maps
+    "d: |\n  line one\n  line two\n\n  after blank\ne: >\n  folded one\n  folded two\n\n  para\nf: |-\n  strip\n"
+    "g: |+\n  keep\n\nh: x\n",
+    "u: !Sub |\n  #!/bin/bash\n  echo ${AWS::Region}\n     indented more\n\nv: 1\n",
+    "- |\n  in a list\n- >-\n  folded\n  list\n- last\n",
+    "k:\n  nested: | # a comment\n    deep\n      deeper\n  next: z\nlast: |\n  at the end",
 ]
 
 
@@ -60,7 +66,9 @@ def test_mixed_json_and_yaml_batch():
 
 
 @pytest.mark.parametrize("doc,why", [
-    ("a: |\n  text\n", "YAML subset"),               # block scalar
+    ("a: |2\n  text\n", "YAML subset"),              # an indentation indicator
+    ("a: >\n  x\n    more\n", "YAML subset"),          # a more-indented line in a folded scalar
+    ("a: |\nb: 1\n", "YAML subset"),                 # an empty block scalar
     ("a: b\n  c\n", "YAML subset"),                   # multi-line plain scalar
     ("a: &x 1\nb: *x\n", "YAML subset"),             # anchors / aliases
     ("a: !!str 1\n", "YAML subset"),                  # a !! tag
@@ -113,7 +121,7 @@ def test_device_loaded_yaml_reports_equal_oracle():
 def test_device_loaded_yaml_with_refused_documents():
     rules = rule_pack("cfg2")
     docs = synth.cfn_yaml_corpus(40, start=900, n_resources=10)
-    docs[5] = docs[5].replace("Resources:", "Description: |\n  block\nResources:", 1)   # host-loaded
+    docs[5] = docs[5].replace("Resources:", "Description: &d anchored\nResources:", 1)   # host-loaded
     docs[17] = docs[17] + "Extra: !Ref Thing\n"
     data = [("r-%d.yaml" % i, d) for i, d in enumerate(docs)]
     exp, ecode, _ = oracle_validate(rules, data)
@@ -142,3 +150,7 @@ def test_reference_yaml_fixtures():
         assert rc != 0, (f, msg)
         taken += rc == 1
     assert taken >= 6, taken
+    # every template of the reference's validate data-dir loads on the device
+    for f in files:
+        if os.sep + "data-dir" + os.sep in f:
+            assert guard_amd.loader_device_check([open(f, encoding="utf-8").read()])[0] == 1, f
