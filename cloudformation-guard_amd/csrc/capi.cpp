@@ -718,7 +718,9 @@ void session_upload(gg_session* s) {
   size_t reserve = 0;
   if (s->mode != 1) {
     const size_t lane_batches = nbatches;
-    size_t ch = 32;
+    // 64 slots: cfg-2 42.3 -> 41.4 ms against 32 on one box (16: 42.8, 48: 41.6, 96: 41.5, 128: 41.4,
+    // profiles/r04_sweep_rec_chunk.log); the 24 GB reservation cap below halves it for larger launches
+    size_t ch = 64;
     // few batches (large documents, hundreds of records per tile): chunks as large as 2 GB of
     // reservations allows, up to 1024 records per lane
     static constexpr size_t kSmallChunkBytes = (size_t)2 << 30;
