@@ -1605,6 +1605,30 @@ char* cfn_guard_validate_batch_format(const validate_input_t* docs, size_t n_doc
   return cfn_guard_validate_batch_params(docs, n_docs, rules, n_rules, nullptr, 0, output_format, exit_code, err);
 }
 
+// The batch entries load a batch of at least GG_BATCH_DEVICE_LOAD_MIN documents (64; 0 = never) without input
+// parameters with the device loader (JSON and block-style YAML on the MI355X, the rest on host threads at
+// their positions); when that path does not take the whole batch -- too few large documents, a document
+// the host loader then rejects -- the documents load one by one on the host as before, so a load error is
+// still the first failing document's, with the reference's message.
+static bool batch_device_load(gg_session* s, const validate_input_t* docs, size_t n_docs, size_t first, size_t count) {
+  const char* e = getenv("GG_BATCH_DEVICE_LOAD_MIN");
+  const size_t min_docs = e ? (size_t)std::max(0, atoi(e)) : 64;
+  if (!min_docs || count < min_docs || s->params || s->docs.ndocs()) return false;
+  (void)n_docs;
+  std::vector<const char*> t(count), nm(count);
+  std::vector<size_t> l(count);
+  for (size_t i = 0; i < count; i++) {
+    const validate_input_t& d = docs[first + i];
+    t[i] = d.content ? d.content : "";
+    l[i] = strlen(t[i]);
+    nm[i] = d.file_name ? d.file_name : "";
+  }
+  extern_err_t le{0, nullptr};
+  const int32_t rc = gg_session_add_docs_device(s, t.data(), l.data(), nm.data(), count, nullptr, &le);
+  if (le.message) free(le.message);
+  return rc == 0;
+}
+
 char* cfn_guard_validate_batch_params(const validate_input_t* docs, size_t n_docs, const validate_input_t* rules,
                                       size_t n_rules, const validate_input_t* params, size_t n_params,
                                       int32_t output_format, int32_t* exit_code, extern_err_t* err) {
@@ -1631,7 +1655,8 @@ char* cfn_guard_validate_batch_params(const validate_input_t* docs, size_t n_doc
     const bool params_ok = load_params(params, n_params, s.params, pe);
     LoadError panic;
     bool panicked = false;
-    for (size_t i = 0; i < n_docs; i++) {
+    const bool on_device = !n_params && batch_device_load(&s, docs, n_docs, 0, n_docs);
+    for (size_t i = 0; i < n_docs && !on_device; i++) {
       LoadError le;
       const char* t = docs[i].content ? docs[i].content : "";
       if (!load_document(s.docs, t, strlen(t), docs[i].file_name ? docs[i].file_name : "", LOAD_LIBYAML, le)) {
@@ -1703,7 +1728,8 @@ char* validate_batch_devices(const validate_input_t* docs, size_t n_docs, const 
       if (!add_rules(&S.s, rules[i].content ? rules[i].content : "", name, perr))
         S.s.parse_errors.push_back("Parsing error handling rule file = " + name + ", Error = " + error_display("ParseError", perr) + "\n---");
     }
-    for (size_t i = starts[k]; i < starts[k + 1]; i++) {
+    const bool on_device = !n_params && batch_device_load(&S.s, docs, n_docs, starts[k], starts[k + 1] - starts[k]);
+    for (size_t i = starts[k]; i < starts[k + 1] && !on_device; i++) {
       const char* t = docs[i].content ? docs[i].content : "";
       if (!load_document(S.s.docs, t, lens[i], docs[i].file_name ? docs[i].file_name : "", LOAD_LIBYAML, S.le)) {
         S.load_fail = i;
