@@ -200,6 +200,9 @@ def main():
     ap.add_argument("--rx-memo", choices=("per-launch", "warm"), default="per-launch",
                     help="regex is_match memo: zeroed before every launch, or kept warm across launches")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--e2e-stream", type=int, default=262144,
+                    help="also time the streamed batch entry (cfn_guard_validate_batch_stream) over the same synthetic "
+                         "texts with this many documents per chunk (0: off; cfg2/cfg3 at N=1 only)")
     ap.add_argument("--e2e-report-docs", type=int, default=0,
                     help="documents whose structured report is rendered for e2e (0: all, the default); a sample's "
                          "report time is scaled to the whole job")
@@ -416,6 +419,37 @@ def main():
                        % (("device %s loader: text H2D, parse, intern index to the host (the arena stays in HBM)" % args.format.upper()) if args.loader == "device"
                           else "host loader threads", " (inside load_s with --loader host)" if gen_in_load else "")}
 
+    e2e_stream = None
+    if (rank == 0 and world == 1 and not args.no_e2e and args.e2e_stream and args.workload in ("cfg2", "cfg3")
+            and args.loader == "device"):
+        # the drop-in batch entry end to end: cfn_guard_validate_batch_stream over the same templates as
+        # validate inputs, chunks of --e2e-stream documents on two alternating sessions (the next chunk's text
+        # H2D, parse and evaluation overlap this chunk's device render and report D2H); the bytes reach host
+        # memory (the library's pinned staging) and are counted
+        log("e2e stream: %d documents in chunks of %d" % (count, args.e2e_stream))
+        t0 = time.time()
+        st_texts = guard_amd.SynthTexts(first, count, n_resources=args.resources, fmt=args.format, threads=threads)
+        t_gen_s = time.time() - t0
+        nbytes = [0]
+
+        def _count(n):
+            nbytes[0] += n
+        try:
+            t0 = time.time()
+            _, st_code = guard_amd.validate_structured_stream(rules, None, write=_count, chunk_docs=args.e2e_stream,
+                                                              inputs=st_texts.inputs, n_docs=st_texts.n,
+                                                              count_only=True)
+            t_stream = time.time() - t0
+        finally:
+            st_texts.close()
+        e2e_stream = {"value": round(ntiles / t_stream, 1), "unit": "evals/s", "seconds": round(t_stream, 3),
+                      "chunk_docs": args.e2e_stream, "report_bytes": nbytes[0],
+                      "report_GBps": round(nbytes[0] / t_stream / 1e9, 3), "exit_code": st_code,
+                      "gen_s": round(t_gen_s, 3),
+                      "note": "cfn_guard_validate_batch_stream (the C ABI batch entry, JSON) over the same synthetic "
+                              "texts resident in host memory: load + upload + evaluation + fetch + device-rendered "
+                              "report to host memory, chunked and overlapped; text generation (gen_s) not included"}
+
     total_units = ntiles * world * args.steps
     value = total_units / elapsed
     if args.workload == "cfg5":
@@ -461,6 +495,8 @@ def main():
         }
         line["cpu_baseline"] = cpu
         line["e2e"] = e2e
+        if e2e_stream is not None:
+            line["e2e_stream"] = e2e_stream
         if gather is not None:
             line["report_gather"] = gather
         print(json.dumps(line), flush=True)

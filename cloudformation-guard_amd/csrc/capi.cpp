@@ -1768,6 +1768,194 @@ char* validate_batch_devices(const validate_input_t* docs, size_t n_docs, const 
 }
 }  // namespace
 
+// ---------------------------------------------------------------- streamed structured JSON ---
+// cfn_guard_validate_batch_format(JSON) for a batch whose report does not fit one string (1 M templates:
+// 149 GB): the documents run in chunks of `chunk_docs` on two alternating sessions -- a producer thread
+// loads (device JSON / YAML loader), uploads, evaluates and fetches chunk k + 1 while this thread renders
+// chunk k on the device and hands its text to `write` in document order (text H2D of the next chunk and
+// report D2H of this one share the link in opposite directions).  The bytes written are the one-string
+// call's; an abort (a load error, an evaluation error, a failing write) ends the stream with code -1 and
+// the error, after the chunks before the failing one were written: the caller drops that prefix.
+namespace {
+struct CallbackSink : ReportSink {
+  cfn_guard_write_fn fn;
+  void* ctx;
+  char* stage;
+  size_t stage_bytes;
+  bool failed = false;
+  uint64_t n = 0;
+  CallbackSink(cfn_guard_write_fn f, void* c, char* st, size_t sb) : fn(f), ctx(c), stage(st), stage_bytes(sb) {}
+  char* reserve(size_t) override { return stage; }
+  void commit(size_t k) override {
+    if (!failed && k && fn(ctx, stage, k) != 0) failed = true;
+    n += k;
+  }
+  size_t max_piece() const override { return stage_bytes; }
+};
+}  // namespace
+
+int32_t cfn_guard_validate_batch_stream(const validate_input_t* docs, size_t n_docs, const validate_input_t* rules,
+                                        size_t n_rules, size_t chunk_docs, cfn_guard_write_fn write, void* ctx,
+                                        int32_t* exit_code, extern_err_t* err) {
+  set_err(err, 0, "");
+  if (exit_code) *exit_code = 0;
+  auto fail = [&](int32_t code, const std::string& msg) { set_err(err, code, msg); if (exit_code) *exit_code = -1; return -1; };
+  if (!write) return fail(18, "IllegalArguments: no write callback");
+  try {
+    std::string why;
+    if (!ensure_device(why)) return fail(-1, why);
+    int dev = 0;
+    HIPCHK(hipGetDevice(&dev));
+    const size_t chunk = chunk_docs ? chunk_docs : (size_t)262144;
+    const size_t nchunks = (n_docs + chunk - 1) / chunk;
+    char* stage = nullptr;
+    HIPCHK(hipHostMalloc((void**)&stage, DeviceBufs::kPinnedBytes, hipHostMallocDefault));
+    struct StageFree { char* p; ~StageFree() { if (p) hipHostFree(p); } } stage_free{stage};
+    CallbackSink sink(write, ctx, stage, DeviceBufs::kPinnedBytes);
+    // producer / consumer over two slots
+    struct Slot {
+      std::unique_ptr<gg_session> s;
+      size_t k = SIZE_MAX;     // chunk held
+      int state = 0;           // 0 free, 1 ready, 2 failed
+      std::string kind, msg;
+    } slot[2];
+    std::mutex mu;
+    std::condition_variable cv;
+    bool stop = false;
+    int32_t parse_code = 0;
+    std::thread producer([&]() {
+      for (size_t k = 0; k < nchunks; k++) {
+        Slot& sl = slot[k & 1];
+        {
+          std::unique_lock<std::mutex> lk(mu);
+          cv.wait(lk, [&] { return sl.state == 0 || stop; });
+          if (stop) return;
+        }
+        std::string kind, msg;
+        std::unique_ptr<gg_session> ses(new gg_session());
+        try {
+          ses->device = dev;
+          for (size_t i = 0; i < n_rules; i++) {
+            std::string perr;
+            const std::string name = rules[i].file_name ? rules[i].file_name : "";
+            if (!add_rules(ses.get(), rules[i].content ? rules[i].content : "", name, perr))
+              ses->parse_errors.push_back("Parsing error handling rule file = " + name + ", Error = " + error_display("ParseError", perr) + "\n---");
+          }
+          const size_t first = k * chunk, count = std::min(chunk, n_docs - first);
+          if (!batch_device_load(ses.get(), docs, n_docs, first, count)) {
+            for (size_t i = first; i < first + count; i++) {
+              LoadError le;
+              const char* t = docs[i].content ? docs[i].content : "";
+              if (!load_document(ses->docs, t, strlen(t), docs[i].file_name ? docs[i].file_name : "", LOAD_LIBYAML, le)) {
+                kind = le.kind; msg = le.msg;
+                break;
+              }
+            }
+          }
+          if (kind.empty()) {
+            if (ses->progs.empty()) {
+              ses->tiles.clear(); ses->rule_status.clear(); ses->recs.clear(); ses->evaluated = true;
+            } else {
+              session_upload(ses.get());
+              session_run(ses.get(), true);
+            }
+          }
+        } catch (std::exception& e) { kind = "Internal"; msg = e.what(); }
+        {
+          std::lock_guard<std::mutex> lk(mu);
+          sl.s = std::move(ses);
+          sl.k = k;
+          sl.state = kind.empty() ? 1 : 2;
+          sl.kind = kind; sl.msg = msg;
+        }
+        cv.notify_all();
+        if (!kind.empty()) return;
+      }
+    });
+    struct Join {
+      std::thread& t; std::mutex& mu; std::condition_variable& cv; bool& stop;
+      ~Join() { { std::lock_guard<std::mutex> lk(mu); stop = true; } cv.notify_all(); if (t.joinable()) t.join(); }
+    } join{producer, mu, cv, stop};
+    bool anyfail = false;
+    if (!n_docs) sink.write("[]", 2);
+    for (size_t k = 0; k < nchunks; k++) {
+      Slot& sl = slot[k & 1];
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return sl.state != 0 && sl.k == k; });
+      }
+      if (sl.state == 2) return fail(ffi_code(sl.kind), error_display(sl.kind, sl.msg));
+      gg_session* s = sl.s.get();
+      if (k == 0) parse_code = s->parse_errors.empty() ? 0 : 5;
+      const size_t nf = s->progs.size(), nd = s->docs.ndocs();
+      for (size_t t = 0; t < nd * nf; t++) {
+        if (s->tiles[t].err) {
+          ensure_host_arena(s);
+          std::vector<const Program*> progs;
+          for (auto& p : s->progs) progs.push_back(&p->prog);
+          ReportError re;
+          tile_error(s->docs, (uint32_t)(t / nf), *progs[t % nf], s->tiles[t], re);
+          return fail(ffi_code(re.kind), error_display(re.kind, re.msg));
+        }
+        if (s->tiles[t].status == ST_FAIL) anyfail = true;
+      }
+      if (k == 0) sink.write("[\n", 2);
+      ReportError re;
+      if (nf && device_report_on(s) && s->fetched_on_device) {
+        if (!device_report_json(s, 0, nd, k == 0 ? 0 : SIZE_MAX, sink, re, nullptr)) return fail(ffi_code(re.kind), error_display(re.kind, re.msg));
+      } else {
+        // host writer for this chunk: its "[\n" ... "\n]" unwrapped, joined with ",\n"
+        std::string out;
+        char* cs = nullptr;
+        int32_t code = 0;
+        if (!session_report(s, out, code, re, OUT_JSON, &cs)) return fail(ffi_code(re.kind), error_display(re.kind, re.msg));
+        std::string text = cs ? std::string(cs) : out;
+        if (cs) free(cs);
+        if (text.size() >= 4 && text.compare(0, 2, "[\n") == 0) {
+          if (k) sink.write(",\n", 2);
+          sink.write(text.data() + 2, text.size() - 4);
+        }
+      }
+      if (sink.failed) return fail(-1, "the write callback failed");
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        sl.s.reset();
+        sl.state = 0;
+        sl.k = SIZE_MAX;
+      }
+      cv.notify_all();
+      if (k + 1 == nchunks) sink.write("\n]", 2);
+    }
+    if (sink.failed) return fail(-1, "the write callback failed");
+    if (exit_code) *exit_code = anyfail ? 19 : parse_code;
+    return 0;
+  } catch (std::exception& e) {
+    return fail(-1, e.what());
+  }
+}
+
+// synthetic corpora as validate inputs (bench.py's streamed end-to-end job): texts generated on host threads
+struct gg_texts {
+  std::vector<std::string> text, name;
+  std::vector<validate_input_t> in;
+};
+gg_texts* gg_synth_texts(uint64_t first, size_t n, int32_t n_resources, int32_t format, int32_t nthreads) {
+  gg_texts* t = new gg_texts();
+  t->text.resize(n); t->name.resize(n); t->in.resize(n);
+  if (nthreads < 1) nthreads = 1;
+  parallel_run((size_t)nthreads, [&](size_t th) {
+    for (size_t i = n * th / nthreads; i < n * (th + 1) / nthreads; i++) {
+      if (format == 1) cfn_synth_yaml_doc(first + i, n_resources, t->text[i]);
+      else cfn_synth_doc(first + i, n_resources, t->text[i]);
+      t->name[i] = "synthetic-" + std::to_string(first + i) + (format == 1 ? ".yaml" : ".json");
+    }
+  });
+  for (size_t i = 0; i < n; i++) { t->in[i].content = t->text[i].c_str(); t->in[i].file_name = t->name[i].c_str(); }
+  return t;
+}
+const validate_input_t* gg_texts_inputs(gg_texts* t) { return t ? t->in.data() : nullptr; }
+void gg_texts_free(gg_texts* t) { delete t; }
+
 char* cfn_guard_validate_batch_devices(const validate_input_t* docs, size_t n_docs, const validate_input_t* rules,
                                        size_t n_rules, const validate_input_t* params, size_t n_params,
                                        int32_t output_format, const int32_t* devices, size_t n_devices, int32_t* exit_code,

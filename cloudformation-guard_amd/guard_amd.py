@@ -55,6 +55,16 @@ def lib():
                                                   ctypes.POINTER(ValidateInput), ctypes.c_size_t, ctypes.c_int32,
                                                   ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ExternError)]
     L.cfn_guard_validate_batch_format.restype = ctypes.c_void_p
+    L.cfn_guard_validate_batch_stream.argtypes = [ctypes.POINTER(ValidateInput), ctypes.c_size_t,
+                                                  ctypes.POINTER(ValidateInput), ctypes.c_size_t, ctypes.c_size_t,
+                                                  WRITE_FN, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32),
+                                                  ctypes.POINTER(ExternError)]
+    L.cfn_guard_validate_batch_stream.restype = ctypes.c_int32
+    L.gg_synth_texts.argtypes = [ctypes.c_uint64, ctypes.c_size_t, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]
+    L.gg_synth_texts.restype = ctypes.c_void_p
+    L.gg_texts_inputs.argtypes = [ctypes.c_void_p]
+    L.gg_texts_inputs.restype = ctypes.POINTER(ValidateInput)
+    L.gg_texts_free.argtypes = [ctypes.c_void_p]
     L.cfn_guard_validate_batch_params.argtypes = [ctypes.POINTER(ValidateInput), ctypes.c_size_t,
                                                   ctypes.POINTER(ValidateInput), ctypes.c_size_t,
                                                   ctypes.POINTER(ValidateInput), ctypes.c_size_t, ctypes.c_int32,
@@ -320,6 +330,53 @@ def validate_structured(rules, data, output="json", params=None):
     if err.code != 0:
         _raise(err)
     return _take_string(p), code.value
+
+
+WRITE_FN = ctypes.CFUNCTYPE(ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
+
+
+def validate_structured_stream(rules, data, write=None, chunk_docs=0, inputs=None, n_docs=None, count_only=False):
+    """cfn_guard_validate_batch_stream: the JSON report of validate_structured streamed to write(bytes) in
+    document order, the documents evaluated in chunks of chunk_docs (0: 262144) on two alternating sessions.
+    Returns (text or None, exit_code): the text when write is None (collected), else None.  Raises GuardError on
+    an abort (the chunks written before it are a prefix to drop).  inputs / n_docs: a prepared
+    ValidateInput array (SynthTexts.inputs) instead of data.  count_only: the text reaches host memory (the
+    library's pinned staging) and only its length is taken -- write(n) gets byte counts (measurement)."""
+    R = (ValidateInput * max(1, len(rules)))(*[ValidateInput(_b(t), _b(n)) for n, t in rules])
+    if inputs is None:
+        inputs = (ValidateInput * max(1, len(data)))(*[ValidateInput(_b(t), _b(n)) for n, t in data])
+        n_docs = len(data)
+    parts = []
+    sink = write if write is not None else parts.append
+
+    def cb(_ctx, ptr, n):
+        try:
+            sink(n if count_only else ctypes.string_at(ptr, n))
+            return 0
+        except Exception:
+            return 1
+    cbf = WRITE_FN(cb)
+    code = ctypes.c_int32(0)
+    err = ExternError()
+    lib().cfn_guard_validate_batch_stream(inputs, n_docs, R, len(rules), chunk_docs, cbf, None, ctypes.byref(code),
+                                          ctypes.byref(err))
+    if err.code != 0:
+        _raise(err)
+    return (b"".join(parts).decode("utf-8") if write is None else None), code.value
+
+
+class SynthTexts:
+    """synthetic templates generated natively as validate inputs (gg_synth_texts): .inputs, .n"""
+
+    def __init__(self, first, n, n_resources=50, fmt="json", threads=8):
+        self.h = lib().gg_synth_texts(first, n, n_resources, {"json": 0, "yaml": 1}[fmt], threads)
+        self.inputs = lib().gg_texts_inputs(self.h)
+        self.n = n
+
+    def close(self):
+        if self.h:
+            lib().gg_texts_free(self.h)
+            self.h = None
 
 
 def validate_structured_devices(rules, data, devices=None, output="json", params=None):

@@ -77,6 +77,20 @@ char *cfn_guard_validate_batch_devices(const validate_input_t *docs, size_t n_do
                                        size_t n_rules, const validate_input_t *params, size_t n_params,
                                        int32_t output_format, const int32_t *devices, size_t n_devices,
                                        int32_t *exit_code, extern_err_t *err);
+/* cfn_guard_validate_batch_format(JSON) streamed for batches whose report does not fit one string: the
+ * documents run in chunks of chunk_docs (0: 262144) on two alternating sessions (the next chunk loads and
+ * evaluates while this one's report renders on the device), and the report's bytes go to write(ctx, data,
+ * len) in order (a nonzero return aborts).  Returns 0 with *exit_code as the one-string call's, or -1 with
+ * err on an abort -- after the chunks before the failing one were written (the caller drops that prefix). */
+typedef int32_t (*cfn_guard_write_fn)(void *ctx, const char *data, size_t len);
+int32_t cfn_guard_validate_batch_stream(const validate_input_t *docs, size_t n_docs, const validate_input_t *rules,
+                                        size_t n_rules, size_t chunk_docs, cfn_guard_write_fn write, void *ctx,
+                                        int32_t *exit_code, extern_err_t *err);
+/* synthetic corpora as validate inputs (bench.py): format 0 JSON (synth.cfn_doc), 1 block-style YAML */
+typedef struct gg_texts gg_texts;
+gg_texts *gg_synth_texts(uint64_t first, size_t n, int32_t n_resources, int32_t format, int32_t nthreads);
+const validate_input_t *gg_texts_inputs(gg_texts *t);
+void gg_texts_free(gg_texts *t);
 /* the n_gpus form of SURVEY.md 8(b): devices 0 .. n_gpus - 1 (n_gpus <= 0: every visible device), no -i. */
 char *cfn_guard_validate_batch_gpus(const validate_input_t *docs, size_t n_docs, const validate_input_t *rules,
                                     size_t n_rules, int32_t output_format, int32_t n_gpus, int32_t *exit_code,

@@ -1,0 +1,74 @@
+"""cfn_guard_validate_batch_stream (capi.cpp): the structured JSON report streamed through a write callback
+while the documents run in chunks on two alternating sessions -- the same bytes and exit code as the
+one-string cfn_guard_validate_batch_format call (structured.rs:99-133), whatever the chunk size."""
+import json
+
+import pytest
+
+import guard_amd
+import synth
+from rulepack import rule_pack
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("chunk", [1, 7, 64, 100, 0])
+def test_stream_equals_one_string(chunk):
+    rules = rule_pack("cfg2")
+    docs = synth.cfn_corpus(130, start=42, n_resources=12) + synth.cfn_yaml_corpus(40, start=7, n_resources=6)
+    data = [("d%d.%s" % (i, "json" if i < 130 else "yaml"), d) for i, d in enumerate(docs)]
+    exp = guard_amd.validate_structured(rules, data)
+    got = guard_amd.validate_structured_stream(rules, data, chunk_docs=chunk)
+    assert got == exp
+
+
+def test_stream_host_fallback_documents_and_parse_errors():
+    rules = rule_pack("cfg2") + [("broken.guard", "rule r { Resources.*.Properties.X == }")]
+    docs = synth.cfn_corpus(90, start=3, n_resources=8)
+    docs[10] = json.dumps({"Resources": {"a": {"Type": "AWS::S3::Bucket", "Properties": {"Size": 2.5}}}})   # host writer
+    docs[70] = "Resources:\n  a: &x\n    Type: AWS::S3::Bucket\n"   # host loader
+    data = [("h%d.json" % i, d) for i, d in enumerate(docs)]
+    exp = guard_amd.validate_structured(rules, data)
+    for chunk in (16, 65, 0):
+        assert guard_amd.validate_structured_stream(rules, data, chunk_docs=chunk) == exp
+
+
+def test_stream_empty_and_error():
+    rules = rule_pack("cfg2")
+    assert guard_amd.validate_structured_stream(rules, [], chunk_docs=4) == guard_amd.validate_structured(rules, [])
+    # an evaluation error (a key on a non-struct in a `keys` filter is fine; an unresolved type block aborts)
+    bad_rules = [("t.guard", "AWS::S3::Bucket { Properties.Missing.Deep == 1 }\nrule r when Resources.*.Type exists { Resources.*.Properties[ keys == /x/ ] !empty }")]
+    docs = synth.cfn_corpus(20, start=1, n_resources=4)
+    data = [("e%d.json" % i, d) for i, d in enumerate(docs)]
+    try:
+        exp = guard_amd.validate_structured(bad_rules, data)
+    except guard_amd.GuardError as e:
+        with pytest.raises(guard_amd.GuardError) as g:
+            guard_amd.validate_structured_stream(bad_rules, data, chunk_docs=5)
+        assert (g.value.code, g.value.message) == (e.code, e.message)
+        return
+    assert guard_amd.validate_structured_stream(bad_rules, data, chunk_docs=5) == exp
+
+
+def test_stream_callback_failure_aborts():
+    rules = rule_pack("cfg2")
+    data = [("c%d.json" % i, d) for i, d in enumerate(synth.cfn_corpus(30, start=9, n_resources=4))]
+    seen = []
+
+    def write(b):
+        seen.append(b)
+        if len(seen) > 1:
+            raise RuntimeError("disk full")
+    with pytest.raises(guard_amd.GuardError):
+        guard_amd.validate_structured_stream(rules, data, write=write, chunk_docs=10)
+
+
+def test_synth_texts_inputs_stream():
+    rules = rule_pack("cfg2")
+    t = guard_amd.SynthTexts(100, 80, n_resources=10, fmt="yaml")
+    try:
+        got = guard_amd.validate_structured_stream(rules, None, inputs=t.inputs, n_docs=t.n, chunk_docs=30)
+    finally:
+        t.close()
+    data = [("synthetic-%d.yaml" % (100 + i), synth.cfn_yaml_doc(100 + i, 10)) for i in range(80)]
+    assert got == guard_amd.validate_structured(rules, data)
