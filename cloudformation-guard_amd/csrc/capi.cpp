@@ -1877,7 +1877,16 @@ int32_t cfn_guard_validate_batch_stream(const validate_input_t* docs, size_t n_d
       ~Join() { { std::lock_guard<std::mutex> lk(mu); stop = true; } cv.notify_all(); if (t.joinable()) t.join(); }
     } join{producer, mu, cv, stop};
     bool anyfail = false;
-    if (!n_docs) sink.write("[]", 2);
+    if (!n_docs) {
+      // no documents: "[]", exit 5 when a rules file does not parse (as the one-string call)
+      gg_session rs;
+      for (size_t i = 0; i < n_rules; i++) {
+        std::string perr;
+        if (!add_rules(&rs, rules[i].content ? rules[i].content : "", rules[i].file_name ? rules[i].file_name : "", perr))
+          parse_code = 5;
+      }
+      sink.write("[]", 2);
+    }
     for (size_t k = 0; k < nchunks; k++) {
       Slot& sl = slot[k & 1];
       {
