@@ -21,3 +21,17 @@ def test_native_yaml_generator_matches_python():
         assert guard_amd.synth_cfn_yaml_doc(i, 12) == synth.cfn_yaml_doc(i, 12), i
     for i in range(20):
         assert yaml.safe_load(synth.cfn_yaml_doc(i, 30)) == synth.cfn_doc(i, 30)
+
+
+def test_synth_texts_inputs():
+    """gg_synth_texts: the validate inputs the bench's streamed leg passes to cfn_guard_validate_batch_stream"""
+    import ctypes
+    for fmt, gen, ext in (("json", lambda i: synth.cfn_corpus(1, start=i, n_resources=6)[0], "json"),
+                          ("yaml", lambda i: synth.cfn_yaml_doc(i, 6), "yaml")):
+        t = guard_amd.SynthTexts(50, 12, n_resources=6, fmt=fmt, threads=3)
+        try:
+            for k in range(12):
+                assert ctypes.string_at(t.inputs[k].content).decode() == gen(50 + k)
+                assert ctypes.string_at(t.inputs[k].file_name).decode() == "synthetic-%d.%s" % (50 + k, ext)
+        finally:
+            t.close()
