@@ -530,7 +530,7 @@ void session_upload(gg_session* s) {
     const uint32_t rkey = D.find("Resources", 9);
     s->type_key = D.find("Type", 4);
     size_t nd = D.ndocs();
-    std::vector<uint32_t> rmap(nd, NONE), toff(nd, 0);
+    std::vector<uint32_t> rmap(std::max<size_t>(nd, 1), NONE), toff(std::max<size_t>(nd, 1), 0);   // one entry at least: the uploads below
     size_t total = 0;
     // a resident arena: the first documents' nodes (the type-frequency sample below) come down, and the
     // root scan runs on the device (root_resources_kernel, json_gpu.hip)
