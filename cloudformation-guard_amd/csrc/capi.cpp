@@ -25,6 +25,7 @@
 #include <unordered_map>
 
 #include "../../include/cfn_guard_mi355x.h"
+#include "dev_cache.h"
 #include "doc_loader.h"
 #include "eval_device.h"
 #include "host_format.h"
@@ -154,10 +155,12 @@ struct DBuf {
   void alloc(size_t count) {
     n = count;
     if (count <= cap && p) return;
-    release();
+    // a growing buffer may still be read by work queued on its session's stream: hipFree waits for it
+    dev_free_sync(p);
+    p = nullptr;
     n = count;
     cap = count;
-    if (count) HIPCHK(hipMalloc((void**)&p, count * sizeof(T)));
+    if (count) HIPCHK(dev_alloc(&p, count * sizeof(T)));
   }
   // alloc with headroom: a growing buffer is reallocated rarely (hipFree synchronises the whole device,
   // which would serialise the device reporter's overlapped render and copy-out)
@@ -170,7 +173,8 @@ struct DBuf {
     alloc(count);
     if (count) HIPCHK(hipMemcpyAsync(p, src, count * sizeof(T), hipMemcpyHostToDevice, s));
   }
-  void release() { if (p) hipFree(p); p = nullptr; n = 0; cap = 0; }
+  // after every stream that used the buffer is drained (~DeviceBufs destroys its streams first)
+  void release() { dev_free(p); p = nullptr; n = 0; cap = 0; }
   size_t bytes() const { return cap * sizeof(T); }
   ~DBuf() { release(); }
 };
@@ -412,8 +416,8 @@ struct gg_session {
     // drain it before the set goes back to the pool, where the next session's uploads reuse it
     if (dv && stream) hipStreamSynchronize(stream);
     release_bufs(dv);
-    if (dev_nodes) { if (device >= 0) hipSetDevice(device); hipFree(dev_nodes); }
-    for (uint32_t* p : {resident.line, resident.col, resident.kline, resident.kcol}) if (p) hipFree(p);
+    dev_free(dev_nodes);
+    for (uint32_t* p : {resident.line, resident.col, resident.kline, resident.kcol}) dev_free(p);
   }
 };
 
@@ -458,10 +462,10 @@ void ensure_host_arena(gg_session* s) {
   HIPCHK(hipMemcpy(D.col.data(), s->resident.col, N * 4, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(D.kline.data(), s->resident.kline, N * 4, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(D.kcol.data(), s->resident.kcol, N * 4, hipMemcpyDeviceToHost));
-  for (uint32_t* p : {s->resident.line, s->resident.col, s->resident.kline, s->resident.kcol}) hipFree(p);
+  for (uint32_t* p : {s->resident.line, s->resident.col, s->resident.kline, s->resident.kcol}) dev_free(p);
   s->resident = ResidentArena{};
   // the upload packed its arena already: the unpacked copy is no longer needed
-  if (s->uploaded) { hipFree(s->dev_nodes); s->dev_nodes = nullptr; s->dev_nodes_n = 0; }
+  if (s->uploaded) { dev_free(s->dev_nodes); s->dev_nodes = nullptr; s->dev_nodes_n = 0; }
 }
 
 void session_upload(gg_session* s) {
@@ -515,7 +519,7 @@ void session_upload(gg_session* s) {
     uint32_t b = 0;
     HIPCHK(hipMemcpyAsync(&b, bad.p, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
-    if (s->dev_nodes && !s->resident.nodes) { hipFree(s->dev_nodes); s->dev_nodes = nullptr; s->dev_nodes_n = 0; }
+    if (s->dev_nodes && !s->resident.nodes) { dev_free(s->dev_nodes); s->dev_nodes = nullptr; s->dev_nodes_n = 0; }
     if (b & 1u) throw std::runtime_error("a string or container is too large for the device arena (count >= 2^28)");
     if (b & 2u) throw std::runtime_error("arena invariant broken: a map entry's key offset is not its key id");
     if (b & 4u) throw std::runtime_error("arena invariant broken: a string id is not a 16-byte pool slot");
@@ -1808,6 +1812,9 @@ int32_t cfn_guard_validate_batch_stream(const validate_input_t* docs, size_t n_d
     HIPCHK(hipGetDevice(&dev));
     const size_t chunk = chunk_docs ? chunk_docs : (size_t)262144;
     const size_t nchunks = (n_docs + chunk - 1) / chunk;
+    // blocks cached by earlier (larger) calls are of other sizes: freed now, while nothing of this call
+    // runs, so that the chunks' own blocks fit under the cache bound and are reused from chunk 3 on
+    dev_cache_flush(dev);
     char* stage = nullptr;
     HIPCHK(hipHostMalloc((void**)&stage, DeviceBufs::kPinnedBytes, hipHostMallocDefault));
     struct StageFree { char* p; ~StageFree() { if (p) hipHostFree(p); } } stage_free{stage};
@@ -2907,10 +2914,10 @@ int32_t gg_session_add_docs_device(gg_session* s, const char* const* texts, cons
     const bool keep = !getenv("GG_RESIDENT_ARENA") || atoi(getenv("GG_RESIDENT_ARENA")) != 0;
     const auto tl = std::chrono::steady_clock::now();
     if (!gpu_load_json(b, texts, lens, nm, n, st, why, &refused, &dev_nodes, keep ? &res : nullptr)) { set_note(err, why); return 1; }
-    struct ResHolder { ResidentArena& r; ~ResHolder() { for (uint32_t* p : {r.line, r.col, r.kline, r.kcol}) if (p) hipFree(p); } } rhold{res};
+    struct ResHolder { ResidentArena& r; ~ResHolder() { for (uint32_t* p : {r.line, r.col, r.kline, r.kcol}) dev_free(p); } } rhold{res};
     if (getenv("GG_LOAD_TRACE"))
       fprintf(stderr, "[load] gpu_load_json returned %8.1f ms\n", std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tl).count());
-    struct Holder { void*& p; ~Holder() { if (p) hipFree(p); } } hold{dev_nodes};
+    struct Holder { void*& p; ~Holder() { dev_free(p); } } hold{dev_nodes};
     const size_t dev_n = b.nodes.size();
     if (!refused.empty()) {
       // the documents the device refused, built by the host loader (libyaml) on host threads and
@@ -2937,7 +2944,7 @@ int32_t gg_session_add_docs_device(gg_session* s, const char* const* texts, cons
     }
     s->docs = std::move(b);
     s->uploaded = false;
-    if (s->dev_nodes) hipFree(s->dev_nodes);
+    dev_free(s->dev_nodes);
     s->dev_nodes = dev_nodes; s->dev_nodes_n = res.nodes ? (size_t)res.nodes : dev_n;
     dev_nodes = nullptr;
     s->resident = res;
@@ -3204,6 +3211,16 @@ int32_t gg_device_available(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
   return n;
+}
+
+int64_t gg_device_cache_release(int32_t device) {
+  int64_t released = 0;
+  for (int d = 0; d < DevCache::kDevs; d++) {
+    if (device >= 0 && d != device) continue;
+    released += (int64_t)dev_cache_held(d);
+    dev_cache_flush(d);
+  }
+  return released;
 }
 
 }  // extern "C"

@@ -1,0 +1,139 @@
+// Device allocations through a per-device cache of freed blocks.
+//
+// hipFree waits for the whole device to go idle.  The streamed batch (cfn_guard_validate_batch_stream)
+// loads chunk k+1 and tears down chunk k-1's session while chunk k's report kernels and copies run on
+// another thread: every hipFree of a loader temporary or a session buffer waited for that report.
+// dev_free puts a block on its device's free list instead (the caller has synchronised every stream
+// that used it, as before a hipFree); dev_alloc takes a cached block of the same size class before
+// calling hipMalloc.  A hipMalloc that fails empties the device's list and tries once more.
+// GG_DEV_CACHE_GB bounds the bytes a device's list holds (default 48; 0 turns the cache off).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+#include <map>
+#include <mutex>
+#include <unordered_map>
+#include <vector>
+
+namespace gg {
+
+struct DevCache {
+  static constexpr int kDevs = 64;
+  std::mutex mu;
+  std::multimap<size_t, void*> free_list[kDevs];
+  size_t held[kDevs] = {};
+  std::unordered_map<void*, std::pair<int, size_t>> live;   // block -> (device, class bytes)
+  size_t cap = 0;
+  DevCache() {
+    const char* e = getenv("GG_DEV_CACHE_GB");
+    cap = (size_t)(e ? atof(e) : 48.0) * (1ull << 30);
+  }
+};
+
+// never destroyed: blocks still cached at exit go with the process (a static destructor calling
+// hipFree after the runtime's own teardown is undefined)
+inline DevCache& dev_cache() {
+  static DevCache* c = new DevCache;
+  return *c;
+}
+
+// size classes: 8 per octave above 4 KB (at most 12.5% over the request), 256-byte steps below
+inline size_t dev_cache_class(size_t b) {
+  if (b <= 4096) return (b + 255) & ~(size_t)255;
+  size_t p = 1;
+  while (p < b) p <<= 1;
+  const size_t step = p / 16;
+  return (b + step - 1) / step * step;
+}
+
+inline size_t dev_cache_held(int dev) {
+  DevCache& C = dev_cache();
+  std::lock_guard<std::mutex> lk(C.mu);
+  return C.held[dev];
+}
+
+inline void dev_cache_flush(int dev) {
+  DevCache& C = dev_cache();
+  std::vector<void*> out;
+  {
+    std::lock_guard<std::mutex> lk(C.mu);
+    for (auto& kv : C.free_list[dev]) out.push_back(kv.second);
+    C.free_list[dev].clear();
+    C.held[dev] = 0;
+  }
+  for (void* p : out) (void)hipFree(p);
+}
+
+inline hipError_t dev_alloc(void** out, size_t bytes) {
+  DevCache& C = dev_cache();
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= DevCache::kDevs) dev = 0;
+  const size_t c = dev_cache_class(bytes ? bytes : 1);
+  {
+    std::lock_guard<std::mutex> lk(C.mu);
+    auto& fl = C.free_list[dev];
+    auto it = fl.lower_bound(c);
+    if (it != fl.end() && it->first == c) {
+      *out = it->second;
+      C.held[dev] -= c;
+      fl.erase(it);
+      C.live[*out] = {dev, c};
+      return hipSuccess;
+    }
+  }
+  void* p = nullptr;
+  hipError_t e = hipMalloc(&p, c);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    dev_cache_flush(dev);
+    e = hipMalloc(&p, c);
+    if (e != hipSuccess) return e;
+  }
+  std::lock_guard<std::mutex> lk(C.mu);
+  C.live[p] = {dev, c};
+  *out = p;
+  return hipSuccess;
+}
+
+template <class T>
+inline hipError_t dev_alloc(T** out, size_t bytes) {
+  void* p = nullptr;
+  const hipError_t e = dev_alloc(&p, bytes);
+  *out = (T*)p;
+  return e;
+}
+
+// p: from dev_alloc (or null); no stream may still use it
+inline void dev_free(void* p) {
+  if (!p) return;
+  DevCache& C = dev_cache();
+  {
+    std::lock_guard<std::mutex> lk(C.mu);
+    auto it = C.live.find(p);
+    if (it != C.live.end()) {
+      const int dev = it->second.first;
+      const size_t c = it->second.second;
+      C.live.erase(it);
+      if (C.held[dev] + c <= C.cap) {
+        C.free_list[dev].emplace(c, p);
+        C.held[dev] += c;
+        return;
+      }
+    }
+  }
+  (void)hipFree(p);
+}
+
+// p: from dev_alloc (or null), possibly still in use by queued work: hipFree's device-wide wait
+inline void dev_free_sync(void* p) {
+  if (!p) return;
+  {
+    DevCache& C = dev_cache();
+    std::lock_guard<std::mutex> lk(C.mu);
+    C.live.erase(p);
+  }
+  (void)hipFree(p);
+}
+
+}  // namespace gg

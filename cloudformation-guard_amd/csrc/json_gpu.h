@@ -29,12 +29,12 @@ struct GpuLoadStats {
 // `out` holds an empty placeholder for it (the caller builds it with the host loader); with
 // `refused` null the whole batch is refused.  Returns false with `why` set when the batch is refused
 // (batch-wide limits, or strict mode); `out` is then unchanged.  With `keep_nodes` non-null the
-// device copy of out.nodes (hipMalloc'ed, out.nodes.size() DNodes) is handed to the caller, who
-// frees it with hipFree: the session packs its arena from it instead of uploading the nodes again.
+// device copy of out.nodes (dev_alloc'ed, out.nodes.size() DNodes) is handed to the caller, who
+// frees it with dev_free (dev_cache.h): the session packs its arena from it instead of uploading the nodes again.
 //
 // With `resident` non-null as well (and no document refused) the per-node columns stay in HBM: out.nodes,
 // line, col, kline, kcol are left EMPTY, the device copies are handed over in *resident (node count
-// st.nodes; the caller owns every pointer, hipFree), and only the pool, the intern index, bases and names
+// st.nodes; the caller owns every pointer, dev_free), and only the pool, the intern index, bases and names
 // reach the host.  The session copies the columns down when a host consumer first needs them
 // (capi.cpp ensure_host_arena); a job whose reports are all rendered on the device never does.
 struct ResidentArena {

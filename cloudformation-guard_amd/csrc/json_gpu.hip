@@ -30,12 +30,15 @@
 #define GG_HD __host__ __device__
 #define GG_POW5_QUAL __constant__
 #include "eisel_lemire.h"
+#include "dev_cache.h"
 
 #include <algorithm>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <stdexcept>
+#include <memory>
+#include <mutex>
 #include <thread>
 
 #ifndef GG_JDIAG_NOINTERN
@@ -674,11 +677,12 @@ template <typename T>
 struct DevArr {
   T* p = nullptr;
   size_t n = 0;
-  ~DevArr() { if (p) hipFree(p); }
+  ~DevArr() { dev_free(p); }
   void alloc(size_t count) {
-    if (p) { hipFree(p); p = nullptr; }
+    dev_free(p);
+    p = nullptr;
     n = count;
-    JCHK(hipMalloc(&p, std::max<size_t>(count, 1) * sizeof(T)));
+    JCHK(dev_alloc(&p, std::max<size_t>(count, 1) * sizeof(T)));
   }
 };
 
@@ -811,7 +815,18 @@ bool gpu_load_json(DocBatch& out, const char* const* texts, const size_t* lens, 
   }
   const uint64_t total = off[n];
   st.text_bytes = total;
-  Staging stg;
+  // one Staging per device, kept between loads (hipHostFree waits for the device to go idle, as hipFree
+  // does); a concurrent load on the same device builds its own
+  static std::mutex stg_mu[64];
+  static Staging* stg_cache[64];
+  int cur_dev = 0;
+  if (hipGetDevice(&cur_dev) != hipSuccess) cur_dev = 0;
+  cur_dev &= 63;
+  std::unique_lock<std::mutex> stg_lk(stg_mu[cur_dev], std::try_to_lock);
+  std::unique_ptr<Staging> stg_own;
+  if (stg_lk.owns_lock() && !stg_cache[cur_dev]) stg_cache[cur_dev] = new Staging;
+  if (!stg_lk.owns_lock()) stg_own.reset(new Staging);
+  Staging& stg = stg_lk.owns_lock() ? *stg_cache[cur_dev] : *stg_own;
   // GG_LOAD_TRACE=1: wall-clock phase marks on stderr
   const bool trace = getenv("GG_LOAD_TRACE") != nullptr;
   const auto tw = std::chrono::steady_clock::now();

@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/device/device_segmented_radix_sort.hpp>
 
+#include "dev_cache.h"
+
 #include <stdexcept>
 #include <string>
 
@@ -31,18 +33,18 @@ void device_segmented_order(const unsigned long long* key, uint32_t* order, uint
   size_t tmp_bytes = 0;
   struct Free {
     void** p[4];
-    ~Free() { for (auto q : p) if (*q) hipFree(*q); }
+    ~Free() { for (auto q : p) gg::dev_free(*q); }
   } fr{{(void**)&vals_in, (void**)&d_seg, (void**)&keys_out, &tmp}};
-  chk(hipMalloc(&vals_in, (size_t)n * 4), "order values");
-  chk(hipMalloc(&keys_out, (size_t)n * 8), "order keys");
-  chk(hipMalloc(&d_seg, (size_t)(nseg + 1) * 4), "order segments");
+  chk(gg::dev_alloc(&vals_in, (size_t)n * 4), "order values");
+  chk(gg::dev_alloc(&keys_out, (size_t)n * 8), "order keys");
+  chk(gg::dev_alloc(&d_seg, (size_t)(nseg + 1) * 4), "order segments");
   chk(hipMemcpyAsync(d_seg, seg_host, (size_t)(nseg + 1) * 4, hipMemcpyHostToDevice, st), "order segments H2D");
   hipLaunchKernelGGL(iota_kernel, dim3((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096), dim3(256), 0, st, vals_in, n);
   chk(hipGetLastError(), "iota_kernel");
   chk(hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, tmp_bytes, key, keys_out, vals_in, order, (int)n, (int)nseg,
                                                   d_seg, d_seg + 1, 0, 64, st),
       "segmented sort (size)");
-  chk(hipMalloc(&tmp, tmp_bytes ? tmp_bytes : 1), "segmented sort scratch");
+  chk(gg::dev_alloc(&tmp, tmp_bytes ? tmp_bytes : 1), "segmented sort scratch");
   chk(hipcub::DeviceSegmentedRadixSort::SortPairs(tmp, tmp_bytes, key, keys_out, vals_in, order, (int)n, (int)nseg,
                                                   d_seg, d_seg + 1, 0, 64, st),
       "segmented sort");

@@ -135,6 +135,8 @@ def lib():
     L.gg_session_last_kernel_ms.argtypes = [ctypes.c_void_p]
     L.gg_session_last_kernel_ms.restype = ctypes.c_double
     L.gg_device_available.restype = ctypes.c_int32
+    L.gg_device_cache_release.argtypes = [ctypes.c_int32]
+    L.gg_device_cache_release.restype = ctypes.c_int64
     L.gg_session_set_stream.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     L.gg_session_set_stream.restype = None
     L.gg_session_launch.argtypes = [ctypes.c_void_p, ctypes.POINTER(ExternError)]
@@ -757,3 +759,9 @@ def synth_cfn_doc(index, n_resources=50):
 
 def device_available():
     return lib().gg_device_available() > 0
+
+
+def release_device_cache(device=-1):
+    """gg_device_cache_release: frees the device blocks the library keeps for reuse (every device with -1);
+    returns the bytes released."""
+    return int(lib().gg_device_cache_release(device))

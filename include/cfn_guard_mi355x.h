@@ -180,6 +180,11 @@ int32_t gg_session_load_results(gg_session *s, const char *path, extern_err_t *e
 int32_t gg_session_tile_status(gg_session *s, uint8_t *out, size_t n);
 double gg_session_last_kernel_ms(gg_session *s);
 int32_t gg_device_available(void);
+/* Frees the device blocks the library keeps for reuse on `device` (-1: every device).  Freed loader
+ * temporaries and session buffers are cached per device (bounded by GG_DEV_CACHE_GB, default 48)
+ * because hipFree waits for the whole device to go idle; this hands them back, as
+ * torch.cuda.empty_cache() does for torch's allocator.  Returns the bytes released. */
+int64_t gg_device_cache_release(int32_t device);
 
 /* Asynchronous evaluation on a caller stream (bench.py passes a non-default torch stream).  NULL
  * selects the library's own non-blocking stream -- the legacy default stream cannot be named. */

@@ -72,3 +72,21 @@ def test_synth_texts_inputs_stream():
         t.close()
     data = [("synthetic-%d.yaml" % (100 + i), synth.cfn_yaml_doc(100 + i, 10)) for i in range(80)]
     assert got == guard_amd.validate_structured(rules, data)
+
+
+def test_device_block_cache_reuse_and_release():
+    """dev_cache.h: loader temporaries and session buffers freed to the per-device cache are reused dirty by
+    later calls (a different batch in between) with the same bytes as fresh blocks; the release entry
+    empties the cache."""
+    rules = rule_pack("cfg2")
+    a = [("a%d.json" % i, d) for i, d in enumerate(synth.cfn_corpus(150, start=5, n_resources=9))]
+    b = [("b%d.yaml" % i, d) for i, d in enumerate(synth.cfn_yaml_corpus(120, start=77, n_resources=11))]
+    assert guard_amd.release_device_cache() >= 0
+    assert guard_amd.release_device_cache() == 0
+    exp_a = guard_amd.validate_structured(rules, a)    # fresh blocks
+    exp_b = guard_amd.validate_structured(rules, b)    # some of a's blocks, dirty
+    assert guard_amd.validate_structured(rules, a) == exp_a
+    assert guard_amd.validate_structured_stream(rules, a + b, chunk_docs=64) == guard_amd.validate_structured(rules, a + b)
+    assert guard_amd.validate_structured(rules, b) == exp_b
+    assert guard_amd.release_device_cache(0) > 0
+    assert guard_amd.release_device_cache(-1) == 0
