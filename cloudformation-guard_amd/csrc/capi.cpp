@@ -308,6 +308,15 @@ struct DeviceBufs {
     for (auto& pr : evq) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
     if (stream) hipStreamDestroy(stream);
   }
+  // every device buffer back to the device block cache (the stream, events and pinned staging stay)
+  void release_device() {
+    d_nodes.release(); d_klen.release(); d_parent.release(); d_line.release(); d_col.release(); d_rtab.release(); d_rprogs.release();
+    for (auto& r : rset) { r.names.release(); r.text.release(); r.name_off.release(); r.sizes.release(); r.offs.release(); }
+    d_bytes.release(); d_roots.release(); d_base.release(); d_res_map.release(); d_tix_off.release(); d_order.release(); d_tix.release();
+    d_progs.release(); d_rx_memo.release(); d_heaps.release(); d_lane_heaps.release(); d_retry.release(); d_big_heaps.release();
+    d_retry2.release(); d_tiles.release(); d_rule_status.release(); d_recs.release(); d_recs_dense.release(); d_dense_off.release();
+    d_bsum.release(); d_counters.release(); d_counts.release(); d_stats.release();
+  }
   size_t bytes() const {
     return d_nodes.bytes() + d_klen.bytes() + d_parent.bytes() + d_line.bytes() + d_col.bytes() + d_rtab.bytes() +
            rset[0].text.bytes() + rset[1].text.bytes() + d_bytes.bytes() + d_roots.bytes() + d_base.bytes() + d_res_map.bytes() +
@@ -322,7 +331,7 @@ struct BufPool {
   std::mutex mu;
   std::vector<DeviceBufs*> free;
   static constexpr size_t kMaxFree = 8;               // idle sets kept
-  static constexpr size_t kMaxKeepBytes = 1ull << 30; // larger sets (batch jobs) are freed, not kept
+  static constexpr size_t kMaxKeepBytes = 1ull << 30; // larger sets (batch jobs) keep no device buffers
 };
 BufPool g_pool[kMaxDevices];   // one per device: a set's buffers and stream belong to its device
 
@@ -337,11 +346,13 @@ DeviceBufs* acquire_bufs(int d) {
 void release_bufs(DeviceBufs* b) {
   if (!b) return;
   hipSetDevice(b->device);
-  if (b->bytes() <= BufPool::kMaxKeepBytes) {
-    if (hipStreamSynchronize(b->stream) == hipSuccess) {
-      std::lock_guard<std::mutex> lk(g_pool[b->device].mu);
-      if (g_pool[b->device].free.size() < BufPool::kMaxFree) { g_pool[b->device].free.push_back(b); return; }
-    }
+  if (hipStreamSynchronize(b->stream) == hipSuccess && (!b->copy_stream || hipStreamSynchronize(b->copy_stream) == hipSuccess)) {
+    // a larger set (a batch job) keeps only its stream, events and pinned staging: its device buffers go
+    // to the block cache, where the next batch's allocations find them (deleting the set would
+    // hipHostFree the staging, which waits for the device to go idle)
+    if (b->bytes() > BufPool::kMaxKeepBytes) b->release_device();
+    std::lock_guard<std::mutex> lk(g_pool[b->device].mu);
+    if (g_pool[b->device].free.size() < BufPool::kMaxFree) { g_pool[b->device].free.push_back(b); return; }
   }
   delete b;
 }
@@ -396,6 +407,11 @@ struct gg_session {
   bool rx_memo_per_launch = false;   // zero the memo before every launch (bench: no warm memo across steps)
   bool marks_on_device = false;   // d_line / d_col hold docs.line / docs.col (device reporter)
   bool fetched_on_device = false; // the fetched results are the device's (tiles, dense records): it can report them
+  // session_fetch leaves the dense records on the device (the streamed batch: its device report reads
+  // them there); ensure_host_arena copies them down for a host writer.  recs_pending: not copied yet.
+  bool defer_recs = false;
+  bool recs_pending = false;
+  uint32_t recs_total = 0;
   bool rtab_ready = false;        // d_rtab / d_rprogs built for the current programs
   int32_t device_report = -1;     // 1: JSON reports rendered on the device, 0: host, -1: GG_DEVICE_REPORT (default 1)
   // device reporter: the sorted rule-name tables inside d_rtab (render_tables)
@@ -448,6 +464,12 @@ size_t arena_nodes(const gg_session* s) { return s->resident.nodes ? (size_t)s->
 // loads appended to the session need them); a no-op once they are there.  Thread-safe per session.
 void ensure_host_arena(gg_session* s) {
   std::lock_guard<std::mutex> lk(s->arena_mu);
+  if (s->recs_pending) {   // host writers read the records as well
+    bind_device(s);
+    s->recs.resize(s->recs_total);
+    HIPCHK(hipMemcpy(s->recs.data(), s->dv->d_recs_dense.p, (size_t)s->recs_total * sizeof(Rec), hipMemcpyDeviceToHost));
+    s->recs_pending = false;
+  }
   if (!s->resident.nodes) return;
   bind_device(s);
   const size_t N = s->resident.nodes;
@@ -507,6 +529,7 @@ void session_upload(gg_session* s) {
     s->marks_on_device = false;
     s->rtab_ready = false;
     s->fetched_on_device = false;
+    s->recs_pending = false;
     DBuf<uint32_t> bad;
     bad.alloc(1);
     HIPCHK(hipMemsetAsync(bad.p, 0, 4, st));
@@ -894,8 +917,14 @@ void session_fetch(gg_session* s) {
     HIPCHK(hipMemcpy(doff.data(), s->dv->d_dense_off.p, ntiles * sizeof(uint32_t), hipMemcpyDeviceToHost));
     for (uint32_t t = 0; t < ntiles; t++) { s->tiles[t].rec_off = doff[t]; s->tiles[t].pad1 = 0; }
   }
-  s->recs.resize(total);
-  if (total) HIPCHK(hipMemcpy(s->recs.data(), s->dv->d_recs_dense.p, (size_t)total * sizeof(Rec), hipMemcpyDeviceToHost));
+  s->recs_total = total;
+  s->recs_pending = s->defer_recs && total;
+  if (s->recs_pending) {
+    s->recs.clear();
+  } else {
+    s->recs.resize(total);
+    if (total) HIPCHK(hipMemcpy(s->recs.data(), s->dv->d_recs_dense.p, (size_t)total * sizeof(Rec), hipMemcpyDeviceToHost));
+  }
   s->counts.resize(s->ncounts);
   HIPCHK(hipMemcpy(s->counts.data(), s->ext_counts ? s->ext_counts : s->dv->d_counts.p, s->ncounts * sizeof(unsigned long long),
                    hipMemcpyDeviceToHost));
@@ -1621,12 +1650,16 @@ static bool batch_device_load(gg_session* s, const validate_input_t* docs, size_
   (void)n_docs;
   std::vector<const char*> t(count), nm(count);
   std::vector<size_t> l(count);
-  for (size_t i = 0; i < count; i++) {
-    const validate_input_t& d = docs[first + i];
-    t[i] = d.content ? d.content : "";
-    l[i] = strlen(t[i]);
-    nm[i] = d.file_name ? d.file_name : "";
-  }
+  // the texts' lengths on the host threads (strlen over ~11 GB of templates is a second on one)
+  const size_t nt = std::max<size_t>(1, std::min<size_t>(report_threads(), count / 1024 + 1));
+  parallel_run(nt, [&](size_t w) {
+    for (size_t i = count * w / nt; i < count * (w + 1) / nt; i++) {
+      const validate_input_t& d = docs[first + i];
+      t[i] = d.content ? d.content : "";
+      l[i] = strlen(t[i]);
+      nm[i] = d.file_name ? d.file_name : "";
+    }
+  });
   extern_err_t le{0, nullptr};
   const int32_t rc = gg_session_add_docs_device(s, t.data(), l.data(), nm.data(), count, nullptr, &le);
   if (le.message) free(le.message);
@@ -1830,6 +1863,12 @@ int32_t cfn_guard_validate_batch_stream(const validate_input_t* docs, size_t n_d
     std::condition_variable cv;
     bool stop = false;
     int32_t parse_code = 0;
+    // GG_STREAM_TRACE=1: per-chunk wall-clock marks on stderr
+    const bool trace = getenv("GG_STREAM_TRACE") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    auto mark = [&](const char* what, size_t k) {
+      if (trace) fprintf(stderr, "[stream] %8.1f ms  chunk %zu %s\n", std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(), k, what);
+    };
     std::thread producer([&]() {
       for (size_t k = 0; k < nchunks; k++) {
         Slot& sl = slot[k & 1];
@@ -1838,10 +1877,12 @@ int32_t cfn_guard_validate_batch_stream(const validate_input_t* docs, size_t n_d
           cv.wait(lk, [&] { return sl.state == 0 || stop; });
           if (stop) return;
         }
+        mark("load start", k);
         std::string kind, msg;
         std::unique_ptr<gg_session> ses(new gg_session());
         try {
           ses->device = dev;
+          ses->defer_recs = true;   // the device report reads the records in HBM
           for (size_t i = 0; i < n_rules; i++) {
             std::string perr;
             const std::string name = rules[i].file_name ? rules[i].file_name : "";
@@ -1859,14 +1900,17 @@ int32_t cfn_guard_validate_batch_stream(const validate_input_t* docs, size_t n_d
               }
             }
           }
+          mark("loaded", k);
           if (kind.empty()) {
             if (ses->progs.empty()) {
               ses->tiles.clear(); ses->rule_status.clear(); ses->recs.clear(); ses->evaluated = true;
             } else {
               session_upload(ses.get());
+              mark("uploaded", k);
               session_run(ses.get(), true);
             }
           }
+          mark("evaluated", k);
         } catch (std::exception& e) { kind = "Internal"; msg = e.what(); }
         {
           std::lock_guard<std::mutex> lk(mu);
@@ -1883,6 +1927,10 @@ int32_t cfn_guard_validate_batch_stream(const validate_input_t* docs, size_t n_d
       std::thread& t; std::mutex& mu; std::condition_variable& cv; bool& stop;
       ~Join() { { std::lock_guard<std::mutex> lk(mu); stop = true; } cv.notify_all(); if (t.joinable()) t.join(); }
     } join{producer, mu, cv, stop};
+    // a reported chunk's session is torn down on a thread of its own (its host columns and index take
+    // tens of ms to free), so the next chunk's report starts at once
+    std::vector<std::thread> reapers;
+    struct JoinAll { std::vector<std::thread>& v; ~JoinAll() { for (auto& t : v) if (t.joinable()) t.join(); } } join_reapers{reapers};
     bool anyfail = false;
     if (!n_docs) {
       // no documents: "[]", exit 5 when a rules file does not parse (as the one-string call)
@@ -1900,6 +1948,7 @@ int32_t cfn_guard_validate_batch_stream(const validate_input_t* docs, size_t n_d
         std::unique_lock<std::mutex> lk(mu);
         cv.wait(lk, [&] { return sl.state != 0 && sl.k == k; });
       }
+      mark("report start", k);
       if (sl.state == 2) return fail(ffi_code(sl.kind), error_display(sl.kind, sl.msg));
       gg_session* s = sl.s.get();
       if (k == 0) parse_code = s->parse_errors.empty() ? 0 : 5;
@@ -1933,13 +1982,16 @@ int32_t cfn_guard_validate_batch_stream(const validate_input_t* docs, size_t n_d
         }
       }
       if (sink.failed) return fail(-1, "the write callback failed");
+      mark("reported", k);
+      std::unique_ptr<gg_session> done;
       {
         std::lock_guard<std::mutex> lk(mu);
-        sl.s.reset();
+        done = std::move(sl.s);
         sl.state = 0;
         sl.k = SIZE_MAX;
       }
       cv.notify_all();
+      reapers.emplace_back([](gg_session* p) { delete p; }, done.release());
       if (k + 1 == nchunks) sink.write("\n]", 2);
     }
     if (sink.failed) return fail(-1, "the write callback failed");
@@ -3119,6 +3171,7 @@ int32_t gg_session_save_results(gg_session* s, const char* path, extern_err_t* e
   if (!s->evaluated) { set_err(err, -1, "session not evaluated"); return -1; }
   FILE* f = fopen(path, "wb");
   if (!f) { set_err(err, -1, std::string("cannot write ") + path); return -1; }
+  try { ensure_host_arena(s); } catch (std::exception& e) { set_err(err, -1, e.what()); return -1; }
   const uint64_t h[4] = {0x47475245ull, s->tiles.size(), s->max_top, s->recs.size()};
   bool ok = fwrite(h, sizeof(h), 1, f) == 1;
   ok = ok && (s->tiles.empty() || fwrite(s->tiles.data(), sizeof(TileOut), s->tiles.size(), f) == s->tiles.size());
