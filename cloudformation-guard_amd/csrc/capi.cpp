@@ -1869,12 +1869,15 @@ int32_t cfn_guard_validate_batch_stream(const validate_input_t* docs, size_t n_d
     auto mark = [&](const char* what, size_t k) {
       if (trace) fprintf(stderr, "[stream] %8.1f ms  chunk %zu %s\n", std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(), k, what);
     };
+    // GG_STREAM_SERIAL=1 (diagnostic): a chunk loads only after the previous one is reported
+    const bool serial = getenv("GG_STREAM_SERIAL") != nullptr;
+    size_t reported = 0;
     std::thread producer([&]() {
       for (size_t k = 0; k < nchunks; k++) {
         Slot& sl = slot[k & 1];
         {
           std::unique_lock<std::mutex> lk(mu);
-          cv.wait(lk, [&] { return sl.state == 0 || stop; });
+          cv.wait(lk, [&] { return (sl.state == 0 && (!serial || reported == k)) || stop; });
           if (stop) return;
         }
         mark("load start", k);
@@ -1989,6 +1992,7 @@ int32_t cfn_guard_validate_batch_stream(const validate_input_t* docs, size_t n_d
         done = std::move(sl.s);
         sl.state = 0;
         sl.k = SIZE_MAX;
+        reported = k + 1;
       }
       cv.notify_all();
       reapers.emplace_back([](gg_session* p) { delete p; }, done.release());
