@@ -101,10 +101,17 @@ void set_note(extern_err_t* err, const std::string& msg) {
 // device: the device current on the first calling thread -- torch.cuda.set_device(LOCAL_RANK) in a
 // one-process-per-GPU job -- or GG_DEVICE.  cfn_guard_validate_batch_devices names its devices.
 static constexpr int kMaxDevices = 64;
+static size_t default_stack_bytes() {
+  return getenv("GG_STACK_BYTES") ? (size_t)atol(getenv("GG_STACK_BYTES")) : (size_t)16384;
+}
 struct DeviceState {
   bool ready = false;
   int ncu = 256;
-  bool big_stack = false;   // lane stack raised to 32 KB for the NFA kernel variant
+  // the lane stack is raised to 32 KB while an NFA kernel variant's launch is in flight (nfa_inflight
+  // launches, under stack_mu) and lowered again when the last one has completed: 32 KB of stack on
+  // several live queues exhausts the scratch (HSA_STATUS_ERROR_OUT_OF_RESOURCES)
+  std::mutex stack_mu;
+  int nfa_inflight = 0;
 };
 struct Devices {
   std::mutex mu;
@@ -128,7 +135,7 @@ struct Devices {
     // the evaluator recurses (eval_conj <-> clauses, filters, rule references): 16 KB of lane stack.  32 KB
     // cannot be had with several queues live (HSA_STATUS_ERROR_OUT_OF_RESOURCES in the concurrent-caller
     // test); GG_STACK_BYTES overrides
-    hipDeviceSetLimit(hipLimitStackSize, getenv("GG_STACK_BYTES") ? (size_t)atol(getenv("GG_STACK_BYTES")) : (size_t)16384);
+    hipDeviceSetLimit(hipLimitStackSize, default_stack_bytes());
     D.ready = true;
     return true;
   }
@@ -406,6 +413,7 @@ struct gg_session {
   size_t rx_memo_words = 0;       // words of the regex is_match memo (0: none)
   bool rx_memo_per_launch = false;   // zero the memo before every launch (bench: no warm memo across steps)
   bool marks_on_device = false;   // d_line / d_col hold docs.line / docs.col (device reporter)
+  bool nfa_launched = false;       // an NFA-variant launch of this session holds the raised lane stack
   bool fetched_on_device = false; // the fetched results are the device's (tiles, dense records): it can report them
   // session_fetch leaves the dense records on the device (the streamed batch: its device report reads
   // them there); ensure_host_arena copies them down for a host writer.  recs_pending: not copied yet.
@@ -431,6 +439,12 @@ struct gg_session {
     // work enqueued on a caller stream (gg_session_set_stream) may still read or write these buffers:
     // drain it before the set goes back to the pool, where the next session's uploads reuse it
     if (dv && stream) hipStreamSynchronize(stream);
+    if (nfa_launched) {   // launched, never waited for: drain it, then give the raised lane stack back
+      if (dv) hipStreamSynchronize(stream ? stream : dv->stream);
+      DeviceState& D = g_devs.dev[device >= 0 ? device : 0];
+      std::lock_guard<std::mutex> lk(D.stack_mu);
+      if (--D.nfa_inflight == 0) hipDeviceSetLimit(hipLimitStackSize, default_stack_bytes());
+    }
     release_bufs(dv);
     dev_free(dev_nodes);
     for (uint32_t* p : {resident.line, resident.col, resident.kline, resident.kcol}) dev_free(p);
@@ -820,9 +834,11 @@ void session_launch(gg_session* s) {
   for (auto& p : s->progs)
     for (auto& r : p->prog.regex) nfa |= r.nfa;
   // its inlined simulation deepens the evaluator's recursive frames: give the lanes a larger stack
-  if (nfa && !g_devs.dev[s->device].big_stack) {
-    HIPCHK(hipDeviceSetLimit(hipLimitStackSize, 32768));
-    g_devs.dev[s->device].big_stack = true;
+  if (nfa && !s->nfa_launched) {
+    DeviceState& D = g_devs.dev[s->device];
+    std::lock_guard<std::mutex> lk(D.stack_mu);
+    if (D.nfa_inflight++ == 0) HIPCHK(hipDeviceSetLimit(hipLimitStackSize, 32768));
+    s->nfa_launched = true;
   }
   if (s->mode != 1) {
     hipLaunchKernelGGL(nfa ? guard_eval_lanes_kernel_nfa : guard_eval_lanes_kernel, dim3(s->lane_slots), dim3(64),
@@ -853,11 +869,22 @@ void session_launch(gg_session* s) {
   s->launched = true;
 }
 
+// the session's NFA-variant launch has completed (or the session ends): the last one in flight on the
+// device lowers the lane stack again
+void nfa_done(gg_session* s) {
+  if (!s->nfa_launched) return;
+  s->nfa_launched = false;
+  DeviceState& D = g_devs.dev[s->device];
+  std::lock_guard<std::mutex> lk(D.stack_mu);
+  if (--D.nfa_inflight == 0) HIPCHK(hipDeviceSetLimit(hipLimitStackSize, default_stack_bytes()));
+}
+
 // waits for the last launch; returns the evaluation kernel's milliseconds (HIP events on its stream)
 double session_wait(gg_session* s) {
   if (!s->launched) return 0;
   bind_device(s);
   HIPCHK(hipEventSynchronize(s->ev1));
+  nfa_done(s);
   float ms = 0;
   HIPCHK(hipEventElapsedTime(&ms, s->ev0, s->ev1));
   s->last_kernel_ms = ms;
