@@ -2022,7 +2022,7 @@ int32_t cfn_guard_validate_batch_stream(const validate_input_t* docs, size_t n_d
         reported = k + 1;
       }
       cv.notify_all();
-      reapers.emplace_back([](gg_session* p) { delete p; }, done.release());
+      reapers.emplace_back([&mark, k](gg_session* p) { delete p; mark("torn down", k); }, done.release());
       if (k + 1 == nchunks) sink.write("\n]", 2);
     }
     if (sink.failed) return fail(-1, "the write callback failed");
