@@ -125,12 +125,17 @@ def _oracle_worker(args):
     t_e2e = time.time() - t
     parsed = [load_document(d, name) for name, d in zip(names, docs)]
     prs = [parse_rules(text, rn) for rn, text in rules]
+    code = {E.PASS: 0, E.FAIL: 1, E.SKIP: 2}   # guard_types.h ST_PASS / ST_FAIL / ST_SKIP
+    st = bytearray()
     t = time.time()
     for name, doc in zip(names, parsed):
         for rf in prs:
-            E.eval_rules_file(rf, E.RootScope(rf, doc), name)
+            try:
+                st.append(code[E.eval_rules_file(rf, E.RootScope(rf, doc), name)])
+            except E.GuardError:
+                st.append(3)   # an erroring tile (gg_session_tile_status)
     t_eval = time.time() - t
-    return t_e2e, t_eval, n * len(rules)
+    return t_e2e, t_eval, n * len(rules), first, bytes(st)
 
 
 def cpu_baseline(workload, n_resources, per_core):
@@ -145,7 +150,10 @@ def cpu_baseline(workload, n_resources, per_core):
     evals = sum(r[2] for r in res)
     busy = max(r[0] for r in res)
     busy_eval = max(r[1] for r in res)
+    # per-(document, rules file) statuses of the sample, tile order: the GPU's are checked against them
+    statuses = b"".join(r[4] for r in sorted(res, key=lambda r: r[3]))
     return {"value": round(evals / busy, 2), "unit": "evals/s", "cores": cores, "kind": "port",
+            "_statuses": statuses,
             "eval_only_value": round(evals / busy_eval, 2), "host": host_info(),
             "sample": "%d %s documents x %d rules files (%d evals) through the Python restatement of the reference "
                       "(oracle/guard_oracle, not the reference binary), one process per core; value = load + evaluate + "
@@ -267,6 +275,9 @@ def main():
     if args.mode != "auto":
         sess.configure(mode=1 if args.mode == "wave" else 0)
     sess.set_option("rx_memo_per_launch", args.rx_memo == "per-launch")
+    # the records stay in HBM where the evaluation wrote them: the device reporter reads them in place, so
+    # nothing is compacted after a launch (host writers would compact and copy them on demand)
+    sess.set_option("defer_records", args.reporter == "device")
     for name, text in rules:
         sess.add_rules(text, name)
     log("load %d documents" % count)
@@ -348,6 +359,19 @@ def main():
     k_mean_ms = sum(kms) / max(1, len(kms))
     achieved = b_alg / (k_mean_ms / 1e3) / 1e9
     tally = sess.counts()
+    if cpu is not None and first == 0:
+        # the CPU baseline's sample is the first documents of this corpus: their (document, rules file)
+        # statuses from the oracle must equal the GPU's, tile for tile
+        exp = cpu.pop("_statuses")
+        got = sess.tile_status(len(exp))
+        bad = [i for i in range(len(exp)) if exp[i] != got[i]]
+        cpu["statuses_checked"] = len(exp)
+        cpu["statuses_equal"] = not bad
+        if bad:
+            cpu["first_mismatch_tile"] = bad[0]
+            log("CPU/GPU status MISMATCH at %d of %d tiles (first: tile %d)" % (len(bad), len(exp), bad[0]))
+    elif cpu is not None:
+        cpu.pop("_statuses", None)
     tally_sum = int(counts.sum().item())   # the all-reduced tensor: every rank's last-step tallies
     n_fail, n_pass, n_skip, n_err = sess.stat(4), sess.stat(5), sess.stat(6), sess.stat(7)
 

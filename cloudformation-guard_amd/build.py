@@ -51,6 +51,25 @@ def _obj(obj_dir, s):
     return os.path.join(obj_dir, s.replace(".cpp", ".o").replace(".hip", ".o"))
 
 
+def _includes(path, seen=None):
+    """the local headers `path` includes, transitively (#include "x")"""
+    import re
+    seen = set() if seen is None else seen
+    try:
+        text = open(path).read()
+    except OSError:
+        return seen
+    for inc in re.findall(r'^\s*#\s*include\s+"([^"]+)"', text, re.M):
+        for base in (os.path.dirname(path), CSRC, os.path.join(HERE, "..", "include")):
+            cand = os.path.normpath(os.path.join(base, inc))
+            if os.path.exists(cand):
+                if cand not in seen:
+                    seen.add(cand)
+                    _includes(cand, seen)
+                break
+    return seen
+
+
 def _needs(src, obj, deps, cmd):
     stamp = obj + ".cmd"
     if not os.path.exists(obj) or not os.path.exists(stamp):
@@ -73,14 +92,12 @@ def build(verbose=False, variant=""):
     elif variant:
         raise ValueError("unknown build variant %r" % variant)
     os.makedirs(obj_dir, exist_ok=True)
-    headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".h", ".inc"))]
-    headers.append(os.path.join(HERE, "..", "include", "cfn_guard_mi355x.h"))
     jobs = []
     for s in HOST_SRCS + HIP_SRCS:
         src = os.path.join(CSRC, s)
         obj = _obj(obj_dir, s)
         cmd = [HIPCC, "--offload-arch=gfx950"] + flags + SRC_FLAGS.get(s, []) + ["-c", src, "-o", obj]
-        if _needs(src, obj, headers, cmd):
+        if _needs(src, obj, sorted(_includes(src)), cmd):
             jobs.append((s, obj, cmd))
 
     def run(job):

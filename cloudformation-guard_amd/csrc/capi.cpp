@@ -107,11 +107,6 @@ static size_t default_stack_bytes() {
 struct DeviceState {
   bool ready = false;
   int ncu = 256;
-  // the lane stack is raised to 32 KB while an NFA kernel variant's launch is in flight (nfa_inflight
-  // launches, under stack_mu) and lowered again when the last one has completed: 32 KB of stack on
-  // several live queues exhausts the scratch (HSA_STATUS_ERROR_OUT_OF_RESOURCES)
-  std::mutex stack_mu;
-  int nfa_inflight = 0;
 };
 struct Devices {
   std::mutex mu;
@@ -413,7 +408,6 @@ struct gg_session {
   size_t rx_memo_words = 0;       // words of the regex is_match memo (0: none)
   bool rx_memo_per_launch = false;   // zero the memo before every launch (bench: no warm memo across steps)
   bool marks_on_device = false;   // d_line / d_col hold docs.line / docs.col (device reporter)
-  bool nfa_launched = false;       // an NFA-variant launch of this session holds the raised lane stack
   bool fetched_on_device = false; // the fetched results are the device's (tiles, dense records): it can report them
   // session_fetch leaves the dense records on the device (the streamed batch: its device report reads
   // them there); ensure_host_arena copies them down for a host writer.  recs_pending: not copied yet.
@@ -439,12 +433,6 @@ struct gg_session {
     // work enqueued on a caller stream (gg_session_set_stream) may still read or write these buffers:
     // drain it before the set goes back to the pool, where the next session's uploads reuse it
     if (dv && stream) hipStreamSynchronize(stream);
-    if (nfa_launched) {   // launched, never waited for: drain it, then give the raised lane stack back
-      if (dv) hipStreamSynchronize(stream ? stream : dv->stream);
-      DeviceState& D = g_devs.dev[device >= 0 ? device : 0];
-      std::lock_guard<std::mutex> lk(D.stack_mu);
-      if (--D.nfa_inflight == 0) hipDeviceSetLimit(hipLimitStackSize, default_stack_bytes());
-    }
     release_bufs(dv);
     dev_free(dev_nodes);
     for (uint32_t* p : {resident.line, resident.col, resident.kline, resident.kcol}) dev_free(p);
@@ -476,13 +464,12 @@ size_t arena_nodes(const gg_session* s) { return s->resident.nodes ? (size_t)s->
 
 // Copies a device-resident arena's columns down to the host batch (the host writers, tile errors, host
 // loads appended to the session need them); a no-op once they are there.  Thread-safe per session.
+void compact_records_to_host(gg_session* s);
 void ensure_host_arena(gg_session* s) {
   std::lock_guard<std::mutex> lk(s->arena_mu);
-  if (s->recs_pending) {   // host writers read the records as well
+  if (s->recs_pending) {   // host writers read the records as well: compacted, in tile order
     bind_device(s);
-    s->recs.resize(s->recs_total);
-    HIPCHK(hipMemcpy(s->recs.data(), s->dv->d_recs_dense.p, (size_t)s->recs_total * sizeof(Rec), hipMemcpyDeviceToHost));
-    s->recs_pending = false;
+    compact_records_to_host(s);
   }
   if (!s->resident.nodes) return;
   bind_device(s);
@@ -833,13 +820,6 @@ void session_launch(gg_session* s) {
   bool nfa = false;
   for (auto& p : s->progs)
     for (auto& r : p->prog.regex) nfa |= r.nfa;
-  // its inlined simulation deepens the evaluator's recursive frames: give the lanes a larger stack
-  if (nfa && !s->nfa_launched) {
-    DeviceState& D = g_devs.dev[s->device];
-    std::lock_guard<std::mutex> lk(D.stack_mu);
-    if (D.nfa_inflight++ == 0) HIPCHK(hipDeviceSetLimit(hipLimitStackSize, 32768));
-    s->nfa_launched = true;
-  }
   if (s->mode != 1) {
     hipLaunchKernelGGL(nfa ? guard_eval_lanes_kernel_nfa : guard_eval_lanes_kernel, dim3(s->lane_slots), dim3(64),
                        A.lds_prog_words * 4, st, A);
@@ -869,22 +849,11 @@ void session_launch(gg_session* s) {
   s->launched = true;
 }
 
-// the session's NFA-variant launch has completed (or the session ends): the last one in flight on the
-// device lowers the lane stack again
-void nfa_done(gg_session* s) {
-  if (!s->nfa_launched) return;
-  s->nfa_launched = false;
-  DeviceState& D = g_devs.dev[s->device];
-  std::lock_guard<std::mutex> lk(D.stack_mu);
-  if (--D.nfa_inflight == 0) HIPCHK(hipDeviceSetLimit(hipLimitStackSize, default_stack_bytes()));
-}
-
 // waits for the last launch; returns the evaluation kernel's milliseconds (HIP events on its stream)
 double session_wait(gg_session* s) {
   if (!s->launched) return 0;
   bind_device(s);
   HIPCHK(hipEventSynchronize(s->ev1));
-  nfa_done(s);
   float ms = 0;
   HIPCHK(hipEventElapsedTime(&ms, s->ev0, s->ev1));
   s->last_kernel_ms = ms;
@@ -913,17 +882,16 @@ uint32_t session_records_wanted(gg_session* s) {
   return nrec;
 }
 
-void session_fetch(gg_session* s) {
-  bind_device(s);
-  // the tally kernel runs after ev1 on a non-blocking stream: wait for the whole launch
-  hipStream_t st = session_stream(s);
-  HIPCHK(hipStreamSynchronize(st));
-  uint32_t ntiles = (uint32_t)(s->docs.ndocs() * s->progs.size());
-  s->tiles.resize(ntiles);
-  s->rule_status.resize((size_t)ntiles * s->max_top);
+// Compacts every tile's records -- in place in their lane's direct chunk (TileOut.pad1 == 1) or contiguous
+// -- into one dense array in tile order and copies it to the host (s->recs), rewriting the host tiles'
+// rec_off to the dense offsets.  Only host writers read the dense array: the device reporter reads the
+// records where the evaluation left them (report_gpu.hip RecSeq), so a device-rendered report needs no
+// compaction at all.
+void compact_records_to_host(gg_session* s) {
+  const uint32_t ntiles = (uint32_t)s->tiles.size();
   uint32_t total = 0;
   if (ntiles) {
-    // compact every tile's records (direct chunks or contiguous) into one dense array in tile order
+    hipStream_t st = session_stream(s);
     const uint32_t nb = (ntiles + 1023u) / 1024u;
     s->dv->d_bsum.alloc((size_t)nb + 1);
     s->dv->d_dense_off.alloc(ntiles);
@@ -938,20 +906,37 @@ void session_fetch(gg_session* s) {
                        s->dv->d_recs.p, s->dv->d_recs_dense.p, s->dv->d_dense_off.p);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(st));
-    HIPCHK(hipMemcpy(s->tiles.data(), s->dv->d_tiles.p, ntiles * sizeof(TileOut), hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(s->rule_status.data(), s->dv->d_rule_status.p, s->rule_status.size(), hipMemcpyDeviceToHost));
     std::vector<uint32_t> doff(ntiles);
     HIPCHK(hipMemcpy(doff.data(), s->dv->d_dense_off.p, ntiles * sizeof(uint32_t), hipMemcpyDeviceToHost));
     for (uint32_t t = 0; t < ntiles; t++) { s->tiles[t].rec_off = doff[t]; s->tiles[t].pad1 = 0; }
   }
+  s->recs.resize(total);
+  if (total) HIPCHK(hipMemcpy(s->recs.data(), s->dv->d_recs_dense.p, (size_t)total * sizeof(Rec), hipMemcpyDeviceToHost));
   s->recs_total = total;
-  s->recs_pending = s->defer_recs && total;
-  if (s->recs_pending) {
-    s->recs.clear();
-  } else {
-    s->recs.resize(total);
-    if (total) HIPCHK(hipMemcpy(s->recs.data(), s->dv->d_recs_dense.p, (size_t)total * sizeof(Rec), hipMemcpyDeviceToHost));
+  s->recs_pending = false;
+}
+
+// Statuses, rule statuses and tallies to the host.  The records stay in HBM as the evaluation wrote them
+// when the session defers them (defer_recs: the device reporter reads them there; ensure_host_arena
+// compacts and copies them once a host writer needs them), else they are compacted and copied now.
+void session_fetch(gg_session* s) {
+  bind_device(s);
+  // the tally kernel runs after ev1 on a non-blocking stream: wait for the whole launch
+  hipStream_t st = session_stream(s);
+  HIPCHK(hipStreamSynchronize(st));
+  uint32_t ntiles = (uint32_t)(s->docs.ndocs() * s->progs.size());
+  s->tiles.resize(ntiles);
+  s->rule_status.resize((size_t)ntiles * s->max_top);
+  if (ntiles) {
+    HIPCHK(hipMemcpy(s->tiles.data(), s->dv->d_tiles.p, ntiles * sizeof(TileOut), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(s->rule_status.data(), s->dv->d_rule_status.p, s->rule_status.size(), hipMemcpyDeviceToHost));
   }
+  uint64_t total = 0;
+  for (const TileOut& t : s->tiles) total += (uint64_t)t.rec_n + t.pad0;
+  s->recs_total = (uint32_t)total;
+  s->recs.clear();
+  s->recs_pending = total != 0;
+  if (!s->defer_recs) compact_records_to_host(s);
   s->counts.resize(s->ncounts);
   HIPCHK(hipMemcpy(s->counts.data(), s->ext_counts ? s->ext_counts : s->dv->d_counts.p, s->ncounts * sizeof(unsigned long long),
                    hipMemcpyDeviceToHost));
@@ -1320,7 +1305,7 @@ bool device_report_json(gg_session* s, size_t first, size_t count, size_t report
     A.nodes = s->dv->d_nodes.p; A.klen = s->dv->d_klen.p; A.pool = s->dv->d_bytes.p; A.parent = s->dv->d_parent.p;
     A.line = s->dv->d_line.p; A.col = s->dv->d_col.p; A.base = s->dv->d_base.p; A.n_nodes = arena_nodes(s);
     A.progs = s->dv->d_rprogs.p; A.nfiles = (uint32_t)nf; A.max_top = s->max_top;
-    A.tiles = s->dv->d_tiles.p; A.rule_status = s->dv->d_rule_status.p; A.recs = s->dv->d_recs_dense.p; A.rec_off = s->dv->d_dense_off.p;
+    A.tiles = s->dv->d_tiles.p; A.rule_status = s->dv->d_rule_status.p; A.recs = s->dv->d_recs.p;
     A.sname_text = s->r_sname_text; A.sname = s->r_sname; A.sname_first = s->r_sname_first; A.sname_n = s->r_sname_n;
     A.sname_fk = s->r_sname_fk; A.n_sname = s->r_nsname;
     A.doc0 = (uint32_t)d0; A.ndocs = (uint32_t)nb; A.report_first = (uint32_t)std::min<size_t>(report_first, 0xFFFFFFFFu);
@@ -2570,6 +2555,7 @@ int32_t gg_session_configure(gg_session* s, int32_t mode, uint32_t lane_heap_byt
 int32_t gg_session_set_option(gg_session* s, int32_t option, int64_t value) {
   switch (option) {
     case GG_OPT_RX_MEMO_PER_LAUNCH: s->rx_memo_per_launch = value != 0; return 0;
+    case GG_OPT_DEFER_RECORDS: s->defer_recs = value != 0; return 0;
     default: return -1;
   }
 }
@@ -3245,10 +3231,10 @@ int64_t gg_session_stat(gg_session* s, int32_t what) {
       return c;
     }
     case 7: { int64_t c = 0; for (auto& t : s->tiles) if (t.err) c++; return c; }
-    case 8: return (int64_t)s->recs.size();
+    case 8: return (int64_t)std::max<size_t>(s->recs.size(), s->recs_total);
     case 9: return (int64_t)(arena_nodes(s) * sizeof(DNodeP) + s->docs.bytes.size() + s->docs.roots.size() * 12);
     case 10: for (auto& t : s->tiles) if (t.err) return t.err; return 0;
-    case 11: return (int64_t)s->recs.size() * (int64_t)sizeof(Rec);
+    case 11: return (int64_t)std::max<size_t>(s->recs.size(), s->recs_total) * (int64_t)sizeof(Rec);
     case 12: return (int64_t)s->rec_cap;
     case 13: return (int64_t)s->max_top;
     case 14: return (int64_t)s->nslots;

@@ -6,7 +6,9 @@
 // dev_free puts a block on its device's free list instead (the caller has synchronised every stream
 // that used it, as before a hipFree); dev_alloc takes a cached block of the same size class before
 // calling hipMalloc.  A hipMalloc that fails empties the device's list and tries once more.
-// GG_DEV_CACHE_GB bounds the bytes a device's list holds (default 48; 0 turns the cache off).
+// GG_DEV_CACHE_GB bounds the bytes a device's list holds (default 16; 0 turns the cache off).  Memory held
+// here is invisible to the HIP runtime and to torch's allocator in the same process, so the default stays
+// well under the 288 GB of one MI355X.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -27,7 +29,9 @@ struct DevCache {
   size_t cap = 0;
   DevCache() {
     const char* e = getenv("GG_DEV_CACHE_GB");
-    cap = (size_t)(e ? atof(e) : 48.0) * (1ull << 30);
+    // the cap is parsed as a double and scaled before the conversion (GG_DEV_CACHE_GB=0.5 is 512 MB)
+    const double gb = e ? atof(e) : 16.0;
+    cap = gb > 0 ? (size_t)(gb * (double)(1ull << 30)) : 0;
   }
 };
 

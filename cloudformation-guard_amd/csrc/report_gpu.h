@@ -49,13 +49,13 @@ struct RenderArgs {
   const uint32_t* col;
   const uint64_t* base;          // per document
   uint64_t n_nodes;              // arena nodes (bounds of every document reference)
-  // evaluation results (session_fetch's dense records)
+  // evaluation results, as the evaluation kernels left them in HBM (records contiguous or strided in
+  // their lane's chunk: TileOut.rec_off / pad1)
   const RProg* progs;
   uint32_t nfiles, max_top;
   const TileOut* tiles;
   const uint8_t* rule_status;
   const Rec* recs;
-  const uint32_t* rec_off;       // per tile: offset of its records in recs
   // not_applicable / compliant: the distinct top-level rule names of all files, sorted; rank r is held
   // by the (file, rule) pairs fk[first[r] .. first[r] + n[r]) (file << 16 | top rule index)
   const char* sname_text;

@@ -244,7 +244,7 @@ LOAD_STATS = ("kernel_ms", "nodes", "distinct_strings", "pool_bytes", "text_byte
               "refused_docs", "gen_ms")
 
 
-SESSION_OPTIONS = {"rx_memo_per_launch": 1}
+SESSION_OPTIONS = {"rx_memo_per_launch": 1, "defer_records": 2}
 
 
 def _load_result(rc, err, st):

@@ -181,7 +181,7 @@ int32_t gg_session_tile_status(gg_session *s, uint8_t *out, size_t n);
 double gg_session_last_kernel_ms(gg_session *s);
 int32_t gg_device_available(void);
 /* Frees the device blocks the library keeps for reuse on `device` (-1: every device).  Freed loader
- * temporaries and session buffers are cached per device (bounded by GG_DEV_CACHE_GB, default 48)
+ * temporaries and session buffers are cached per device (bounded by GG_DEV_CACHE_GB, default 16)
  * because hipFree waits for the whole device to go idle; this hands them back, as
  * torch.cuda.empty_cache() does for torch's allocator.  Returns the bytes released. */
 int64_t gg_device_cache_release(int32_t device);
@@ -196,6 +196,10 @@ int32_t gg_session_configure(gg_session *s, int32_t mode, uint32_t lane_heap_byt
  * is_match memo (2 bits per (pool string, regex), filled by the first evaluation that runs the DFA) before
  * every launch, so each launch pays its own first DFA runs; 0 (default) zeroes it once per upload. */
 #define GG_OPT_RX_MEMO_PER_LAUNCH 1
+/* GG_OPT_DEFER_RECORDS: 1 leaves the failure records in HBM where the evaluation wrote them at
+ * gg_session_fetch (statuses and tallies still come to the host); the device JSON reporter reads them
+ * there, and they are compacted and copied down only when a host writer needs them.  0 (default). */
+#define GG_OPT_DEFER_RECORDS 2
 int32_t gg_session_set_option(gg_session *s, int32_t option, int64_t value);
 int32_t gg_session_launch(gg_session *s, extern_err_t *err);  /* enqueue; no host sync */
 double gg_session_wait(gg_session *s, extern_err_t *err);     /* kernel ms of the last launch */

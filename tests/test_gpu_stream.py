@@ -2,12 +2,18 @@
 while the documents run in chunks on two alternating sessions -- the same bytes and exit code as the
 one-string cfn_guard_validate_batch_format call (structured.rs:99-133), whatever the chunk size."""
 import json
+import os
 
 import pytest
 
 import guard_amd
 import synth
+from guard_oracle import validate_structured as oracle_validate
+from guard_oracle.errors import GuardError, FFI_CODES
 from rulepack import rule_pack
+from test_gpu_parity import _nfa_docs
+
+G = os.path.join(os.path.dirname(__file__), "golden")
 
 pytestmark = pytest.mark.gpu
 
@@ -36,18 +42,47 @@ def test_stream_host_fallback_documents_and_parse_errors():
 def test_stream_empty_and_error():
     rules = rule_pack("cfg2")
     assert guard_amd.validate_structured_stream(rules, [], chunk_docs=4) == guard_amd.validate_structured(rules, [])
-    # an evaluation error (a key on a non-struct in a `keys` filter is fine; an unresolved type block aborts)
-    bad_rules = [("t.guard", "AWS::S3::Bucket { Properties.Missing.Deep == 1 }\nrule r when Resources.*.Type exists { Resources.*.Properties[ keys == /x/ ] !empty }")]
+    # a deterministic evaluation error in a later chunk: `empty` on an integer aborts the reference's
+    # evaluation (eval.rs:251-262); the streamed entry raises the oracle's code and message
+    bad_rules = [("t.guard", "rule r { Resources.*.Properties.Port empty }")]
     docs = synth.cfn_corpus(20, start=1, n_resources=4)
+    docs[13] = json.dumps({"Resources": {"b": {"Type": "AWS::S3::Bucket", "Properties": {"Port": 8080}}}})
     data = [("e%d.json" % i, d) for i, d in enumerate(docs)]
     try:
-        exp = guard_amd.validate_structured(bad_rules, data)
-    except guard_amd.GuardError as e:
-        with pytest.raises(guard_amd.GuardError) as g:
-            guard_amd.validate_structured_stream(bad_rules, data, chunk_docs=5)
-        assert (g.value.code, g.value.message) == (e.code, e.message)
-        return
-    assert guard_amd.validate_structured_stream(bad_rules, data, chunk_docs=5) == exp
+        oracle_validate(bad_rules, data, raise_errors=True)
+        raise AssertionError("the oracle did not abort")
+    except GuardError as e:
+        code, msg = FFI_CODES.get(e.kind, -1), e.display()
+    seen = []
+    with pytest.raises(guard_amd.GuardError) as g:
+        guard_amd.validate_structured_stream(bad_rules, data, write=seen.append, chunk_docs=5)
+    assert (g.value.code, g.value.message) == (code, msg)
+    with pytest.raises(guard_amd.GuardError) as g1:
+        guard_amd.validate_structured(bad_rules, data)
+    assert (g1.value.code, g1.value.message) == (code, msg)
+
+
+def test_stream_vs_oracle():
+    """the streamed bytes against the CPU oracle directly (not only against the one-string call, which
+    shares the device loader and reporter)"""
+    rules = rule_pack("cfg2")
+    docs = synth.cfn_corpus(70, start=500, n_resources=9) + synth.cfn_yaml_corpus(30, start=90, n_resources=5)
+    data = [("o%d.%s" % (i, "json" if i < 70 else "yaml"), d) for i, d in enumerate(docs)]
+    exp, ecode, _ = oracle_validate(rules, data)
+    assert guard_amd.validate_structured_stream(rules, data, chunk_docs=24) == (exp, ecode)
+
+
+def test_nfa_pack_through_stream_and_device_list():
+    """regexes past the DFA limits (the NFA kernel variant) through the streamed entry -- two sessions
+    alternating, their launches overlapping -- and through a device list [0, 0]: byte-equal to the oracle.
+    The variant runs in the default lane stack (no device-wide stack limit is raised for it)."""
+    p = os.path.join(G, "nfa_rulepack")
+    rules = [(f, open(os.path.join(p, f)).read()) for f in sorted(os.listdir(p)) if f.endswith(".guard")]
+    data = [("n%d.json" % i, d) for i, d in enumerate(_nfa_docs())]
+    exp, ecode, _ = oracle_validate(rules, data)
+    for chunk in (9, 40):
+        assert guard_amd.validate_structured_stream(rules, data, chunk_docs=chunk) == (exp, ecode), chunk
+    assert guard_amd.validate_structured_devices(rules, data, devices=[0, 0], output="json") == (exp, ecode)
 
 
 def test_stream_callback_failure_aborts():
