@@ -221,11 +221,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
       if (!c.err) for (uint32_t i = 0; i < P->n_slots; i++) u32a(c, c.memo)[i] = 3u;
       c.vtab = alloc_pers(c, (P->n_vars ? P->n_vars : 1) * 16);
       if (!c.err) for (uint32_t i = 0; i < P->n_vars; i++) u32a(c, c.vtab)[i * 4] = 0u;
+      c.kbase = alloc_pers(c, KDEPTH * KFRAME); c.kdepth = 0;
       push_frame(c, F_ROOT, NONE, A.docs.roots[doc], P->root_block);
       uint32_t fails = 0, passes = 0;
       uint8_t* rs = A.rule_status + (size_t)tile * A.max_top;
       for (uint32_t r = 0; r < P->n_top && !c.err; r++) {
-        uint32_t st = eval_rule(c, P->top_first + r, 0, NONE);
+        uint32_t st = run_rule(c, P->top_first + r);
         if (c.err) break;
         rs[r] = (uint8_t)st;
         if (st == ST_PASS) passes++; else if (st == ST_FAIL) fails++;
