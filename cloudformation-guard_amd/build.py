@@ -88,7 +88,7 @@ def build(verbose=False, variant=""):
     if variant == "stats":
         flags.append("-DGG_STATS")
     elif variant.startswith("ab"):
-        flags += shlex.split(os.environ.get("GG_AB_FLAGS", ""))
+        pass   # GG_AB_FLAGS go to the evaluator units only (below): an A/B rebuild compiles two files
     elif variant:
         raise ValueError("unknown build variant %r" % variant)
     os.makedirs(obj_dir, exist_ok=True)
@@ -96,7 +96,8 @@ def build(verbose=False, variant=""):
     for s in HOST_SRCS + HIP_SRCS:
         src = os.path.join(CSRC, s)
         obj = _obj(obj_dir, s)
-        cmd = [HIPCC, "--offload-arch=gfx950"] + flags + SRC_FLAGS.get(s, []) + ["-c", src, "-o", obj]
+        extra = shlex.split(os.environ.get("GG_AB_FLAGS", "")) if variant.startswith("ab") and s.startswith("eval_kernel") else []
+        cmd = [HIPCC, "--offload-arch=gfx950"] + flags + SRC_FLAGS.get(s, []) + extra + ["-c", src, "-o", obj]
         if _needs(src, obj, sorted(_includes(src)), cmd):
             jobs.append((s, obj, cmd))
 

@@ -23,6 +23,7 @@
 #include <thread>
 #include <vector>
 #include <unordered_map>
+#include <unordered_set>
 
 #include "../../include/cfn_guard_mi355x.h"
 #include "dev_cache.h"
@@ -52,6 +53,7 @@ __global__ void root_resources_kernel(const DNode* nodes, const uint64_t* base, 
                                       uint32_t* rmap, uint32_t* cnt);
 __global__ void pack_nodes_kernel(const DNode* in, DNodeP* out, uint32_t* klen, uint32_t* parent, uint64_t n, uint32_t* bad);
 __global__ void report_kernel(RenderArgs A, uint32_t write);
+__global__ void report_sarif_kernel(RenderArgs A, uint32_t write);
 __global__ void rec_block_sums_kernel(const TileOut* tiles, uint32_t n, uint32_t* bsum);
 __global__ void rec_scan_sums_kernel(uint32_t* bsum, uint32_t nb, uint32_t* total);
 __global__ void rec_compact_kernel(const TileOut* tiles, uint32_t n, const uint32_t* bsum, const Rec* src, Rec* dst,
@@ -1155,8 +1157,8 @@ void render_tables(gg_session* s) {
 // Per block of documents (two block sets in flight): the size pass, then the write pass at the offsets;
 // a copy thread moves each block to the sink in document order -- device runs by D2H, host-writer
 // documents between them -- while the device renders the next block.
-bool device_report_json(gg_session* s, size_t first, size_t count, size_t report_first, ReportSink& sink, ReportError& err,
-                        DevReportStats* stats) {
+bool device_report_text(gg_session* s, size_t first, size_t count, size_t report_first, ReportSink& sink, ReportError& err,
+                        DevReportStats* stats, int32_t fmt) {
   bind_device(s);
   render_tables(s);
   hipStream_t st = s->dv->stream;
@@ -1213,18 +1215,25 @@ bool device_report_json(gg_session* s, size_t first, size_t count, size_t report
             const auto h0 = std::chrono::steady_clock::now();
             ensure_host_arena(s);   // the host writer reads the arena's columns
             const size_t d = b.d0 + k;
-            TextBuf t;
-            if (d != report_first) t.append(",\n", 2);
-            t.append(2, ' ');
             std::vector<TileResult> trs(nf);
             std::vector<const TileResult*> tp(nf);
             for (size_t f = 0; f < nf; f++) {
               trs[f] = tile_view(s->tiles.data(), s->rule_status.data(), s->max_top, s->recs.data(), d * nf + f);
               tp[f] = &trs[f];
             }
-            if (!report_json_doc(s->docs, (uint32_t)d, progs, tp, t, cerr)) { failed = true; break; }
-            sink.write(t.data(), t.size());
-            S.bytes += t.size();
+            if (fmt == OUT_SARIF) {
+              std::string t;
+              if (!sarif_doc_results(s->docs, (uint32_t)d, progs, tp, t, cerr)) { failed = true; break; }
+              sink.write(t.data(), t.size());
+              S.bytes += t.size();
+            } else {
+              TextBuf t;
+              if (d != report_first) t.append(",\n", 2);
+              t.append(2, ' ');
+              if (!report_json_doc(s->docs, (uint32_t)d, progs, tp, t, cerr)) { failed = true; break; }
+              sink.write(t.data(), t.size());
+              S.bytes += t.size();
+            }
             S.host_docs++;
             S.host_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count();
             k++;
@@ -1312,7 +1321,8 @@ bool device_report_json(gg_session* s, size_t first, size_t count, size_t report
     A.names = R.names.p; A.name_off = R.name_off.p; A.sizes = R.sizes.p;
     const uint32_t blocks = (uint32_t)std::min<size_t>((nb + 255) / 256, (size_t)dev_ncu(s->device) * 8);
     HIPCHK(hipEventRecord(e0, st));
-    hipLaunchKernelGGL(report_kernel, dim3(blocks), dim3(256), 0, st, A, 0u);
+    auto kern = fmt == OUT_SARIF ? report_sarif_kernel : report_kernel;
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, st, A, 0u);
     HIPCHK(hipGetLastError());
     b.sizes.resize(nb);
     HIPCHK(hipMemcpyAsync(b.sizes.data(), R.sizes.p, nb * 8, hipMemcpyDeviceToHost, st));
@@ -1327,7 +1337,7 @@ bool device_report_json(gg_session* s, size_t first, size_t count, size_t report
     R.offs.alloc_grow(nb);
     HIPCHK(hipMemcpyAsync(R.offs.p, b.offs.data(), nb * 8, hipMemcpyHostToDevice, st));
     A.out = R.text.p; A.offsets = R.offs.p;
-    hipLaunchKernelGGL(report_kernel, dim3(blocks), dim3(256), 0, st, A, 1u);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, st, A, 1u);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(e1, st));
     HIPCHK(hipEventRecord(b.done, st));
@@ -1350,6 +1360,11 @@ bool device_report_json(gg_session* s, size_t first, size_t count, size_t report
   if (cex) std::rethrow_exception(cex);
   if (failed) { err = cerr; return false; }
   return true;
+}
+
+bool device_report_json(gg_session* s, size_t first, size_t count, size_t report_first, ReportSink& sink, ReportError& err,
+                        DevReportStats* stats) {
+  return device_report_text(s, first, count, report_first, sink, err, stats, OUT_JSON);
 }
 
 // One shard of a structured report: documents [first, first + count) of a fetched session.
@@ -1403,6 +1418,59 @@ bool shards_report(const std::vector<ShardView>& sh, std::string& out, int32_t& 
     else { sink.n = 0; sink.write("[]", 2); }
     *cstr = sink.take();
     if (anyfail && !(fmt == OUT_JUNIT && exit_code == 5)) exit_code = 19;
+    return true;
+  }
+  // GG_DEVICE_SARIF=0: the host writer for SARIF as well
+  bool sarif_dev = fmt == OUT_SARIF && cstr && !sh.empty() && !(getenv("GG_DEVICE_SARIF") && atoi(getenv("GG_DEVICE_SARIF")) == 0);
+  for (const ShardView& v : sh) sarif_dev = sarif_dev && (v.count == 0 || (device_report_on(v.s) && v.s->fetched_on_device));
+  if (sarif_dev) {
+    // SarifReport::new (sarif.rs:29-53, 185-203): the artifacts -- the FAILed documents' first-seen
+    // non-empty names, from the fetched statuses -- written here, every FAILed document's results rendered
+    // on its shard's device (report_gpu.hip rg::file_sarif) and joined in document order
+    std::vector<std::string> art;
+    std::unordered_set<std::string> seen;
+    for (const ShardView& v : sh) {
+      const size_t nf = v.s->progs.size();
+      for (size_t d = v.first; d < v.first + v.count; d++) {
+        uint32_t status = ST_SKIP;
+        for (size_t f = 0; f < nf; f++) {
+          const uint32_t st = v.s->tiles[d * nf + f].status;   // Status::and (rules/mod.rs:122-133)
+          if (status == ST_FAIL) continue;
+          status = status == ST_PASS ? (st == ST_FAIL ? ST_FAIL : ST_PASS) : st;
+        }
+        if (status != ST_FAIL) continue;
+        anyfail = true;
+        const std::string& name = v.s->docs.names[d];
+        if (!name.empty() && seen.insert(name).second) art.push_back(name);
+      }
+    }
+    std::string head, tail;
+    sarif_frame(art, head, tail);
+    BufferSink sink;
+    sink.write(head.data(), head.size());
+    // the results' first comma is dropped: "[\n        {" as serde's pretty printer writes it
+    struct DropFirst : ReportSink {
+      ReportSink& in;
+      char* last = nullptr;
+      uint64_t n = 0;
+      explicit DropFirst(ReportSink& s) : in(s) {}
+      char* reserve(size_t k) override { return last = in.reserve(k); }
+      void commit(size_t k) override {
+        if (!k) return;
+        if (n == 0) { memmove(last, last + 1, k - 1); in.commit(k - 1); }
+        else in.commit(k);
+        n += k;
+      }
+      size_t max_piece() const override { return in.max_piece(); }
+    } results(sink);
+    for (const ShardView& v : sh) {
+      if (!v.count || v.s->progs.empty()) continue;
+      if (!device_report_text(v.s, v.first, v.count, SIZE_MAX, results, err, nullptr, OUT_SARIF)) { exit_code = -1; return false; }
+    }
+    if (results.n) sink.write("\n      ", 7);
+    sink.write(tail.data(), tail.size());
+    *cstr = sink.take();
+    if (anyfail) exit_code = 19;
     return true;
   }
   std::vector<TextBuf> all_parts;
@@ -1843,18 +1911,13 @@ struct CallbackSink : ReportSink {
 };
 }  // namespace
 
-int32_t cfn_guard_validate_batch_stream(const validate_input_t* docs, size_t n_docs, const validate_input_t* rules,
-                                        size_t n_rules, size_t chunk_docs, cfn_guard_write_fn write, void* ctx,
-                                        int32_t* exit_code, extern_err_t* err) {
-  set_err(err, 0, "");
-  if (exit_code) *exit_code = 0;
+namespace {
+int32_t stream_single(int dev, const validate_input_t* docs, size_t n_docs, const validate_input_t* rules,
+                      size_t n_rules, size_t chunk_docs, cfn_guard_write_fn write, void* ctx,
+                      int32_t* exit_code, extern_err_t* err) {
   auto fail = [&](int32_t code, const std::string& msg) { set_err(err, code, msg); if (exit_code) *exit_code = -1; return -1; };
-  if (!write) return fail(18, "IllegalArguments: no write callback");
   try {
-    std::string why;
-    if (!ensure_device(why)) return fail(-1, why);
-    int dev = 0;
-    HIPCHK(hipGetDevice(&dev));
+    HIPCHK(hipSetDevice(dev));
     const size_t chunk = chunk_docs ? chunk_docs : (size_t)262144;
     const size_t nchunks = (n_docs + chunk - 1) / chunk;
     // blocks cached by earlier (larger) calls are of other sizes: freed now, while nothing of this call
@@ -2008,6 +2071,207 @@ int32_t cfn_guard_validate_batch_stream(const validate_input_t* docs, size_t n_d
       }
       cv.notify_all();
       reapers.emplace_back([&mark, k](gg_session* p) { delete p; mark("torn down", k); }, done.release());
+      if (k + 1 == nchunks) sink.write("\n]", 2);
+    }
+    if (sink.failed) return fail(-1, "the write callback failed");
+    if (exit_code) *exit_code = anyfail ? 19 : parse_code;
+    return 0;
+  } catch (std::exception& e) {
+    return fail(-1, e.what());
+  }
+}
+}  // namespace
+
+int32_t cfn_guard_validate_batch_stream(const validate_input_t* docs, size_t n_docs, const validate_input_t* rules,
+                                        size_t n_rules, size_t chunk_docs, cfn_guard_write_fn write, void* ctx,
+                                        int32_t* exit_code, extern_err_t* err) {
+  set_err(err, 0, "");
+  if (exit_code) *exit_code = 0;
+  if (!write) { set_err(err, 18, "IllegalArguments: no write callback"); if (exit_code) *exit_code = -1; return -1; }
+  std::string why;
+  int dev = 0;
+  if (!ensure_device(why, -1, &dev)) { set_err(err, -1, why); if (exit_code) *exit_code = -1; return -1; }
+  return stream_single(dev, docs, n_docs, rules, n_rules, chunk_docs, write, ctx, exit_code, err);
+}
+
+// ---------------------------------------------------------------- streamed, several devices ---
+// cfn_guard_validate_batch_stream with the chunks spread over a device list (SURVEY.md 8(b) n_gpus, 8(e)):
+// chunk k (chunk_docs documents) runs on pipeline k % ndev, a host thread bound to devices[k % ndev], which
+// loads, uploads, evaluates and fetches it and renders its JSON report on that device into a host buffer
+// of its own; this thread hands the buffers to `write` in chunk order (structured.rs:122-129: one writer,
+// documents in order).  A pipeline starts chunk k only once chunk k - 2 ndev has been written, so host
+// memory holds at most two chunks' reports per device.  Errors: the first in document order, as the
+// one-device stream (load error, erroring tile, report abort), after the chunks before it were written.
+namespace {
+// chunk k's report text (its "[\n" ... "\n]" unwrapped; ",\n" before it unless k == 0) into `sink`;
+// false + re for an abort
+bool stream_chunk_report(gg_session* s, size_t k, ReportSink& sink, ReportError& re, bool& anyfail) {
+  const size_t nf = s->progs.size(), nd = s->docs.ndocs();
+  for (size_t t = 0; t < nd * nf; t++) {
+    if (s->tiles[t].err) {
+      ensure_host_arena(s);
+      std::vector<const Program*> progs;
+      for (auto& p : s->progs) progs.push_back(&p->prog);
+      tile_error(s->docs, (uint32_t)(t / nf), *progs[t % nf], s->tiles[t], re);
+      return false;
+    }
+    if (s->tiles[t].status == ST_FAIL) anyfail = true;
+  }
+  if (nf && device_report_on(s) && s->fetched_on_device)
+    return device_report_json(s, 0, nd, k == 0 ? 0 : SIZE_MAX, sink, re, nullptr);
+  std::string out;
+  char* cs = nullptr;
+  int32_t code = 0;
+  if (!session_report(s, out, code, re, OUT_JSON, &cs)) return false;
+  std::string text = cs ? std::string(cs) : out;
+  if (cs) free(cs);
+  if (text.size() >= 4 && text.compare(0, 2, "[\n") == 0) {
+    if (k) sink.write(",\n", 2);
+    sink.write(text.data() + 2, text.size() - 4);
+  }
+  return true;
+}
+// chunk [first, first + count) loaded, evaluated and fetched on `dev`; kind / msg for a load error
+std::unique_ptr<gg_session> stream_chunk_session(int dev, const validate_input_t* docs, size_t n_docs, const validate_input_t* rules,
+                                                 size_t n_rules, size_t first, size_t count, std::string& kind, std::string& msg) {
+  std::unique_ptr<gg_session> ses(new gg_session());
+  ses->device = dev;
+  ses->defer_recs = true;   // the device report reads the records in HBM
+  for (size_t i = 0; i < n_rules; i++) {
+    std::string perr;
+    const std::string name = rules[i].file_name ? rules[i].file_name : "";
+    if (!add_rules(ses.get(), rules[i].content ? rules[i].content : "", name, perr))
+      ses->parse_errors.push_back("Parsing error handling rule file = " + name + ", Error = " + error_display("ParseError", perr) + "\n---");
+  }
+  if (!batch_device_load(ses.get(), docs, n_docs, first, count)) {
+    for (size_t i = first; i < first + count; i++) {
+      LoadError le;
+      const char* t = docs[i].content ? docs[i].content : "";
+      if (!load_document(ses->docs, t, strlen(t), docs[i].file_name ? docs[i].file_name : "", LOAD_LIBYAML, le)) {
+        kind = le.kind; msg = le.msg;
+        return ses;
+      }
+    }
+  }
+  if (ses->progs.empty()) {
+    ses->tiles.clear(); ses->rule_status.clear(); ses->recs.clear(); ses->evaluated = true;
+  } else {
+    session_upload(ses.get());
+    session_run(ses.get(), true);
+  }
+  return ses;
+}
+}  // namespace
+
+int32_t cfn_guard_validate_batch_stream_devices(const validate_input_t* docs, size_t n_docs, const validate_input_t* rules,
+                                                size_t n_rules, size_t chunk_docs, const int32_t* devices, size_t n_devices,
+                                                cfn_guard_write_fn write, void* ctx, int32_t* exit_code, extern_err_t* err) {
+  set_err(err, 0, "");
+  if (exit_code) *exit_code = 0;
+  auto fail = [&](int32_t code, const std::string& msg) { set_err(err, code, msg); if (exit_code) *exit_code = -1; return -1; };
+  if (!write) return fail(18, "IllegalArguments: no write callback");
+  try {
+    std::vector<int> devs;
+    std::string why;
+    if (devices) {
+      for (size_t i = 0; i < n_devices; i++) devs.push_back(devices[i]);
+    } else {
+      int n = 0;
+      if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+      for (int d = 0; d < n; d++) devs.push_back(d);
+    }
+    if (devs.empty()) return fail(-1, devices ? "IllegalArguments: an empty device list" : "no HIP device available (the MI355X path has no CPU fallback)");
+    for (int d : devs)
+      if (!ensure_device(why, d)) return fail(-1, why);
+    const size_t ndev = devs.size();
+    // one device: the one-device stream (its report copied out straight into the callback's staging)
+    if (ndev == 1) return stream_single(devs[0], docs, n_docs, rules, n_rules, chunk_docs, write, ctx, exit_code, err);
+    const size_t chunk = chunk_docs ? chunk_docs : (size_t)16384;
+    const size_t nchunks = (n_docs + chunk - 1) / chunk;
+    struct Out {
+      int state = 0;          // 0 pending, 1 ready, 2 failed
+      BufferSink text;
+      bool anyfail = false;
+      int32_t parse_code = 0;
+      std::string kind, msg;
+    };
+    std::vector<std::unique_ptr<Out>> outs(nchunks);
+    for (auto& o : outs) o.reset(new Out());
+    std::mutex mu;
+    std::condition_variable cv;
+    size_t written = 0;
+    bool stop = false;
+    std::vector<std::thread> pipes;
+    for (size_t p = 0; p < std::min(ndev, nchunks); p++) {
+      pipes.emplace_back([&, p]() {
+        for (size_t k = p; k < nchunks; k += ndev) {
+          {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return stop || k < 2 * ndev || written > k - 2 * ndev; });
+            if (stop) return;
+          }
+          Out& o = *outs[k];
+          std::string kind, msg;
+          try {
+            const size_t first = k * chunk, count = std::min(chunk, n_docs - first);
+            std::unique_ptr<gg_session> ses = stream_chunk_session(devs[p], docs, n_docs, rules, n_rules, first, count, kind, msg);
+            if (kind.empty()) {
+              o.parse_code = ses->parse_errors.empty() ? 0 : 5;
+              ReportError re;
+              if (!stream_chunk_report(ses.get(), k, o.text, re, o.anyfail)) { kind = re.kind; msg = re.msg; }
+            }
+          } catch (std::exception& e) { kind = "Internal"; msg = e.what(); }
+          {
+            std::lock_guard<std::mutex> lk(mu);
+            o.kind = kind; o.msg = msg;
+            o.state = kind.empty() ? 1 : 2;
+          }
+          cv.notify_all();
+          if (!kind.empty()) return;
+        }
+      });
+    }
+    struct JoinAll {
+      std::vector<std::thread>& v; std::mutex& mu; std::condition_variable& cv; bool& stop;
+      ~JoinAll() { { std::lock_guard<std::mutex> lk(mu); stop = true; } cv.notify_all(); for (auto& t : v) if (t.joinable()) t.join(); }
+    } join{pipes, mu, cv, stop};
+    char* stage = nullptr;
+    HIPCHK(hipHostMalloc((void**)&stage, 1u << 20, hipHostMallocDefault));
+    struct StageFree { char* p; ~StageFree() { if (p) hipHostFree(p); } } stage_free{stage};
+    CallbackSink sink(write, ctx, stage, 1u << 20);
+    int32_t parse_code = 0;
+    bool anyfail = false;
+    if (!n_docs) {
+      gg_session rs;
+      for (size_t i = 0; i < n_rules; i++) {
+        std::string perr;
+        if (!add_rules(&rs, rules[i].content ? rules[i].content : "", rules[i].file_name ? rules[i].file_name : "", perr))
+          parse_code = 5;
+      }
+      sink.write("[]", 2);
+    }
+    for (size_t k = 0; k < nchunks; k++) {
+      Out& o = *outs[k];
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return o.state != 0; });
+      }
+      if (o.state == 2) return fail(ffi_code(o.kind), error_display(o.kind, o.msg));
+      if (k == 0) { parse_code = o.parse_code; sink.write("[\n", 2); }
+      anyfail = anyfail || o.anyfail;
+      // the buffer goes to the callback as it is, in pieces of at most 256 MB (no staging copy); a
+      // failing callback ends the stream
+      for (size_t at = 0; at < o.text.n && !sink.failed; at += (size_t)256 << 20)
+        if (write(ctx, o.text.p + at, std::min(o.text.n - at, (size_t)256 << 20)) != 0) sink.failed = true;
+      sink.n += o.text.n;
+      if (sink.failed) return fail(-1, "the write callback failed");
+      free(o.text.p);
+      o.text.p = nullptr; o.text.n = o.text.cap = 0;
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        written = k + 1;
+      }
+      cv.notify_all();
       if (k + 1 == nchunks) sink.write("\n]", 2);
     }
     if (sink.failed) return fail(-1, "the write callback failed");

@@ -712,6 +712,223 @@ RN void tile_items(W& w, const Ctx& c, const RecSeq recs, uint32_t nrec) {
   while (sp && !w.fb) { close(w, ']'); close(w, '}'); close(w, '}'); sp--; }
 }
 
+// ------------------------------------------------------------------------------- SARIF ---
+// SarifResults::from (sarif.rs:127-160) for one tile: every message of every ClauseReport
+// (ClauseReport::get_message, eval_context.rs:1808-1826 -- a Rule's and a Disjunction's checks flattened,
+// a Block's and a Clause's own Messages) becomes a SarifResult in record order: ruleId from the enclosing
+// top-level Rule's name (extract_rule_id: the part before the first '.', upper-cased), level "error",
+// message.text = error_message + " " + custom_message (None as ""), one location in the data file at
+// Messages.location (a Binary clause's compared value; (0, 0) elsewhere), clamped to 1.  Each result is
+// preceded by ",\n" and the results array's indent; the host drops the report's first comma.
+RD void sarif_rule_id(W& w, const Ctx& c, uint32_t rule) {
+  if (rule == NONE) { raw(w, '"'); raw(w, '"'); return; }
+  if (rule >= c.P->n_rule_names) { w.fb = FB_REF; return; }
+  const RStr r = c.P->rule_names[rule];
+  raw(w, '"');
+  for (uint32_t k = 0; k < r.len; k++) {
+    const char ch = c.P->text[r.off + k];
+    if (ch == '.') break;
+    esc1(w, (unsigned char)(ch >= 'a' && ch <= 'z' ? ch - 32 : ch));
+  }
+  raw(w, '"');
+}
+// Messages.location of a compared value (the host's q_loc): (0, 0) without a node
+RD void sarif_loc(W& w, const Ctx& c, const QR& q, uint32_t& line, uint32_t& col) {
+  line = 0; col = 0;
+  if (q.node == NONE) return;
+  if (q.node & (SYN_BIT | KEY_BIT)) { w.fb = FB_REF; return; }
+  if (!(q.node & LIT_BIT) && c.dbase + q.node >= c.A->n_nodes) { w.fb = FB_REF; return; }
+  line = line_of(c, q.node); col = col_of(c, q.node);
+}
+// opens one result: ",\n", its indent, `{`, ruleId, level, message { text: "  -- the caller writes the text
+RD void sarif_open(W& w, const Ctx& c, uint32_t rule) {
+  raw(w, ','); raw(w, '\n'); spaces(w, 8);
+  w.depth = 0; w.base = 4; w.first = 0; w.esc = false; w.dotf = false; w.held = false;
+  open(w, '{');
+  key(w, "ruleId"); sarif_rule_id(w, c, rule);
+  key(w, "level"); jlit(w, "error");
+  key(w, "message"); open(w, '{');
+  key(w, "text"); sbeg(w);
+}
+// ... closes the text and writes the location
+RD void sarif_close(W& w, const char* uri, uint32_t urin, uint32_t line, uint32_t col) {
+  send(w);
+  close(w, '}');
+  key(w, "locations"); open(w, '[');
+  item(w); open(w, '{');
+  key(w, "physicalLocation"); open(w, '{');
+  key(w, "artifactLocation"); open(w, '{'); key(w, "uri"); jstr(w, uri, urin); close(w, '}');
+  key(w, "region"); open(w, '{');
+  key(w, "startLine"); tu64(w, line > 1 ? line : 1);
+  key(w, "startColumn"); tu64(w, col > 1 ? col : 1);
+  close(w, '}');
+  close(w, '}');
+  close(w, '}');
+  close(w, ']');
+  close(w, '}');
+}
+RN void tile_sarif(W& w, const Ctx& c, const RecSeq recs, uint32_t nrec, const char* uri, uint32_t urin) {
+  uint32_t closes[kMaxDepth];
+  uint32_t sp = 0;
+  uint32_t rule = NONE;   // the enclosing top-level Rule (its name index), NONE outside one
+  uint32_t i = 0;
+  while (i < nrec && !w.fb) {
+    const Rec rc = recs[i];
+    if (sp && rc.kind == closes[sp - 1]) {
+      i++;
+      if (--sp == 0) rule = NONE;
+      continue;
+    }
+    i++;
+    switch (rc.kind) {
+      case REC_RULE_OPEN:
+        if (sp == kMaxDepth) { w.fb = FB_DEPTH; return; }
+        if (sp == 0) rule = rc.clause;
+        closes[sp++] = REC_RULE_CLOSE;
+        break;
+      case REC_DISJ_OPEN:
+        if (sp == kMaxDepth) { w.fb = FB_DEPTH; return; }
+        closes[sp++] = REC_DISJ_CLOSE;
+        break;
+      case REC_BLOCK_EMPTY:
+        if (!clause_ok(w, c, rc.clause)) return;
+        sarif_open(w, c, rule);
+        tlit(w, "query for block clause did not retrieve any value ");
+        sarif_close(w, uri, urin, 0, 0);
+        break;
+      case REC_MISSING_BLOCK_VALUE:
+        if (!clause_ok(w, c, rc.clause)) return;
+        sarif_open(w, c, rule);
+        tlit(w, "Check was not compliant as property ["); remaining(w, c, rc.from);
+        tlit(w, "] is missing. Value traversed to ["); unresolved_display(w, c, rc.from); tput(w, ']');
+        tput(w, ' ');
+        sarif_close(w, uri, urin, 0, 0);
+        break;
+      case REC_UNARY: {
+        if (!clause_ok(w, c, rc.clause)) return;
+        const PClause pc = c.P->clauses[rc.clause];
+        const uint32_t op = pc.flags & 15u;
+        const bool neg = (pc.flags >> 4) & 1u;
+        sarif_open(w, c, rule);
+        if (qkind(rc.from) == QR_UNRESOLVED) {
+          tlit(w, "Check was not compliant as property ["); remaining(w, c, rc.from);
+          tlit(w, "] is missing. Value traversed to ["); unresolved_display(w, c, rc.from); tlit(w, "].");
+        } else {
+          tlit(w, "Check was not compliant as property ["); q_path_display(w, c, rc.from); tlit(w, "] ");
+          tlit(w, unary_msg(op, neg)); tput(w, '.');
+        }
+        tput(w, ' '); custom_text(w, c, pc);
+        sarif_close(w, uri, urin, 0, 0);
+        break;
+      }
+      case REC_NOVALUE_EMPTY: {
+        if (!clause_ok(w, c, rc.clause)) return;
+        const PClause pc = c.P->clauses[rc.clause];
+        sarif_open(w, c, rule);
+        tlit(w, "Check was not compliant as variable in context ["); tstr_tab(w, c, c.P->ctx, pc.d); tlit(w, "] was not empty");
+        tput(w, ' ');
+        if (pc.e != NONE && pc.e < c.P->n_msgs) {   // newlines become ';'
+          const RStr r = c.P->msgs[pc.e];
+          for (uint32_t k = 0; k < r.len; k++) { const char ch = c.P->text[r.off + k]; tput(w, ch == '\n' ? ';' : ch); }
+        }
+        sarif_close(w, uri, urin, 0, 0);
+        break;
+      }
+      case REC_DEPENDENT_RULE: {
+        if (!clause_ok(w, c, rc.clause)) return;
+        const PClause pc = c.P->clauses[rc.clause];
+        sarif_open(w, c, rule);
+        tlit(w, "Check was not compliant as dependent rule ["); tstr_tab(w, c, c.P->ctx, pc.f);
+        tlit(w, "] did not PASS. Context ["); tstr_tab(w, c, c.P->ctx, pc.d); tput(w, ']');
+        tput(w, ' '); custom_text(w, c, pc);
+        sarif_close(w, uri, urin, 0, 0);
+        break;
+      }
+      case REC_CMP: {
+        const bool mk = rc.clause == NONE;
+        if (!mk && !clause_ok(w, c, rc.clause)) return;
+        const PClause pc = mk ? PClause{} : c.P->clauses[rc.clause];
+        const uint32_t op = mk ? (rc.y & 15u) : (pc.flags & 15u);
+        const bool neg = mk ? ((rc.y >> 4) & 1u) : ((pc.flags >> 4) & 1u);
+        const bool from_unres = qkind(rc.from) == QR_UNRESOLVED;
+        if (!from_unres && rc.to.meta == 0xFFFFFFFFu) break;   // `to` absent: nothing reported (eval_context.rs:2283)
+        const bool to_unres = !from_unres && qkind(rc.to) == QR_UNRESOLVED;
+        uint32_t line, col;
+        sarif_loc(w, c, from_unres ? rc.from : rc.to, line, col);
+        sarif_open(w, c, rule);
+        if (from_unres || to_unres) {
+          const QR& u = from_unres ? rc.from : rc.to;
+          tlit(w, "Check was not compliant as property ["); remaining(w, c, u);
+          tlit(w, from_unres ? "] to compare from is missing. Value traversed to [" : "] to compare to is missing. Value traversed to [");
+          unresolved_display(w, c, u); tlit(w, "].");
+        } else {
+          tlit(w, "Check was not compliant as property value ["); pav_display(w, c, rc.from); tlit(w, "] ");
+          tlit(w, op_msg(op, neg)); tlit(w, " value ["); pav_display(w, c, rc.to); tlit(w, "].");
+        }
+        if (rc.x) { tlit(w, " Error = ["); nc_reason(w, c, rc); tput(w, ']'); }
+        tput(w, ' '); if (!mk) custom_text(w, c, pc);
+        sarif_close(w, uri, urin, line, col);
+        break;
+      }
+      case REC_IN: {
+        const bool mk = rc.clause == NONE;
+        if (!mk && !clause_ok(w, c, rc.clause)) return;
+        const PClause pc = mk ? PClause{} : c.P->clauses[rc.clause];
+        const uint32_t nto = rc.x;
+        const uint32_t l0 = i;
+        uint32_t have = 0;
+        while (have < nto && i < nrec && recs[i].kind == REC_LIST) { have += (have + 1 < nto) ? 2u : 1u; i++; }
+        auto to_at = [&](uint32_t k) -> QR { const Rec& lr = recs[l0 + k / 2]; return (k & 1u) ? lr.to : lr.from; };
+        uint32_t line, col;
+        sarif_loc(w, c, rc.from, line, col);
+        sarif_open(w, c, rule);
+        tlit(w, "Check was not compliant as property ["); q_path_display(w, c, rc.from); tlit(w, "] was not present in [");
+        w.dotf = true;   // the items joined by '.', then every '.' before a '[' dropped (reporter.cpp "fixed")
+        for (uint32_t k = 0; k < have; k++) {
+          const QR t = to_at(k);
+          if (k) tput(w, '.');
+          if (qkind(t) == QR_UNRESOLVED) { tlit(w, "(unresolved, "); unresolved_display(w, c, t); }
+          else { tlit(w, "(resolved, "); pav_display(w, c, t); }
+          tput(w, ')');
+        }
+        if (w.held) { w.held = false; emit(w, '.'); }
+        w.dotf = false;
+        tput(w, ']');
+        tput(w, ' ');
+        if (!mk && pc.e != NONE) tstr_tab(w, c, c.P->msgs, pc.e);
+        sarif_close(w, uri, urin, line, col);
+        break;
+      }
+      default:
+        break;
+    }
+  }
+}
+
+// one document's SarifResults: only a FAILed FileReport contributes (SarifRun::from, sarif.rs:29-51);
+// the artifact URI is the document name without one leading '/' (sanitize_path)
+RN void file_sarif(W& w, const RenderArgs& A, uint32_t doc) {
+  const uint32_t k = doc - A.doc0;
+  const uint32_t nf = A.nfiles;
+  uint32_t status = ST_SKIP;
+  for (uint32_t f = 0; f < nf; f++) {
+    const uint32_t st = A.tiles[(size_t)doc * nf + f].status;
+    if (status == ST_FAIL) continue;
+    if (status == ST_PASS) status = st == ST_FAIL ? ST_FAIL : ST_PASS;
+    else status = st;
+  }
+  if (status != ST_FAIL) return;
+  const char* uri = A.names + A.name_off[k];
+  uint32_t urin = (uint32_t)(A.name_off[k + 1] - A.name_off[k]);
+  if (urin && uri[0] == '/') { uri++; urin--; }
+  for (uint32_t f = 0; f < nf && !w.fb; f++) {
+    const size_t t = (size_t)doc * nf + f;
+    const TileOut to = A.tiles[t];
+    Ctx c{&A, &A.progs[f], A.base[doc]};
+    tile_sarif(w, c, RecSeq{A.recs + to.rec_off, to.pad1 == 1 ? 64u : 1u}, to.rec_n, uri, urin);
+  }
+}
+
 // one document's FileReport (write_file_report), preceded by ",\n" after the report's first document and
 // the array's two-space indent
 RN void file_report(W& w, const RenderArgs& A, uint32_t doc) {
@@ -771,6 +988,20 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) r
       w.p = A.out + A.offsets[k];
     }
     rg::file_report(w, A, A.doc0 + k);
+    if (!write) A.sizes[k] = w.fb ? (kHostDoc | w.fb) : w.n;
+  }
+}
+
+// The SARIF report's results (rg::file_sarif), one lane per document, in the same two passes; a kernel of
+// its own so the JSON writer's instantiation is unchanged.
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) report_sarif_kernel(RenderArgs A, uint32_t write) {
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < A.ndocs; k += gridDim.x * blockDim.x) {
+    rg::W w{};
+    if (write) {
+      if (A.sizes[k] & kHostDoc) continue;
+      w.p = A.out + A.offsets[k];
+    }
+    rg::file_sarif(w, A, A.doc0 + k);
     if (!write) A.sizes[k] = w.fb ? (kHostDoc | w.fb) : w.n;
   }
 }

@@ -1305,7 +1305,96 @@ const char* kSarifDescription =
 
 std::string sanitize_path(const std::string& p) { return !p.empty() && p[0] == '/' ? p.substr(1) : p; }
 
+// SarifResults::from (sarif.rs:127-160) of one FAILed FileReport: one result per message of every
+// not_compliant ClauseReport, in order
+void sarif_results(const J& fr, const std::string& name, J& results) {
+  for (auto& failure : field(fr, "not_compliant")->a) {
+    std::string rule_id;
+    if (failure.o[0].first == "Rule") {
+      std::string rn = field(failure.o[0].second, "name")->s;
+      rule_id = rn.substr(0, rn.find('.'));
+      for (auto& ch : rule_id) ch = (char)toupper((unsigned char)ch);
+    }
+    std::vector<const J*> msgs;
+    get_messages(failure, msgs);
+    for (const J* m : msgs) {
+      int64_t line = m->loc_line < 0 ? 0 : m->loc_line, col = m->loc_col < 0 ? 0 : m->loc_col;
+      const J* em = field(*m, "error_message");
+      const J* cm = field(*m, "custom_message");
+      std::string text = (em->t == J::Str ? em->s : std::string()) + " " + (cm->t == J::Str ? cm->s : std::string());
+      J res = J::obj();
+      res.add("ruleId", J::str(rule_id));
+      res.add("level", J::str("error"));
+      J mt = J::obj(); mt.add("text", J::str(text));
+      res.add("message", std::move(mt));
+      J art = J::obj(); art.add("uri", J::str(sanitize_path(name)));
+      J region = J::obj();
+      region.add("startLine", J::raw(std::to_string(std::max<int64_t>(line, 1))));
+      region.add("startColumn", J::raw(std::to_string(std::max<int64_t>(col, 1))));
+      J phys = J::obj(); phys.add("artifactLocation", std::move(art)); phys.add("region", std::move(region));
+      J l = J::obj(); l.add("physicalLocation", std::move(phys));
+      J locs = J::arr(); locs.push(std::move(l));
+      res.add("locations", std::move(locs));
+      results.push(std::move(res));
+    }
+  }
+}
+
+// the SARIF report (SarifReport::new, sarif.rs:185-203) with these artifacts and results
+J sarif_report(J artifacts, J results) {
+  J drv = J::obj();
+  drv.add("name", J::str("cfn-guard"));
+  drv.add("semanticVersion", J::str("3.1.2"));
+  drv.add("fullName", J::str("cfn-guard 3.1.2"));
+  drv.add("organization", J::str("Amazon Web Services"));
+  drv.add("downloadUri", J::str("https://github.com/aws-cloudformation/cloudformation-guard"));
+  drv.add("informationUri", J::str("https://github.com/aws-cloudformation/cloudformation-guard"));
+  J sd = J::obj(); sd.add("text", J::str(kSarifDescription));
+  drv.add("shortDescription", std::move(sd));
+  J tool = J::obj(); tool.add("driver", std::move(drv));
+  J run = J::obj();
+  run.add("tool", std::move(tool));
+  run.add("artifacts", std::move(artifacts));
+  run.add("results", std::move(results));
+  J runs = J::arr(); runs.push(std::move(run));
+  J rep = J::obj();
+  rep.add("$schema", J::str("https://docs.oasis-open.org/sarif/sarif/v2.1.0/errata01/os/schemas/sarif-schema-2.1.0.json"));
+  rep.add("version", J::str("2.1.0"));
+  rep.add("runs", std::move(runs));
+  return rep;
+}
+
 }  // namespace
+
+bool sarif_doc_results(const DocBatch& docs, uint32_t doc, const std::vector<const Program*>& progs,
+                       const std::vector<const TileResult*>& tiles, std::string& out, ReportError& err) {
+  J fr;
+  if (!build_file_report(docs, doc, progs, tiles, fr, nullptr, err)) return false;
+  if (field(fr, "status")->s != "FAIL") return true;
+  J results = J::arr();
+  sarif_results(fr, docs.names[doc], results);
+  for (const J& r : results.a) {
+    out += ",\n";
+    out.append(8, ' ');
+    pretty(r, 4, out);
+  }
+  return true;
+}
+
+void sarif_frame(const std::vector<std::string>& artifact_names, std::string& head, std::string& tail) {
+  J artifacts = J::arr();
+  for (const std::string& name : artifact_names) {
+    J loc = J::obj(); loc.add("uri", J::str(sanitize_path(name)));
+    J a = J::obj(); a.add("location", std::move(loc));
+    artifacts.push(std::move(a));
+  }
+  std::string all;
+  pretty(sarif_report(std::move(artifacts), J::arr()), 0, all);
+  static const char kMark[] = "\"results\": []";
+  const size_t at = all.rfind(kMark);
+  head = all.substr(0, at + sizeof(kMark) - 2);   // ... "results": [
+  tail = all.substr(at + sizeof(kMark) - 2);      // ]\n    }\n  ]\n}
+}
 
 struct ReportWriter::Impl {
   int32_t fmt;
@@ -1370,36 +1459,7 @@ bool ReportWriter::add(const DocBatch& docs, uint32_t doc, const std::vector<con
         I.artifacts.push(std::move(a));
         I.art_names.push_back(name);
       }
-      for (auto& failure : field(fr, "not_compliant")->a) {
-        std::string rule_id;
-        if (failure.o[0].first == "Rule") {
-          std::string rn = field(failure.o[0].second, "name")->s;
-          rule_id = rn.substr(0, rn.find('.'));
-          for (auto& ch : rule_id) ch = (char)toupper((unsigned char)ch);
-        }
-        std::vector<const J*> msgs;
-        get_messages(failure, msgs);
-        for (const J* m : msgs) {
-          int64_t line = m->loc_line < 0 ? 0 : m->loc_line, col = m->loc_col < 0 ? 0 : m->loc_col;
-          const J* em = field(*m, "error_message");
-          const J* cm = field(*m, "custom_message");
-          std::string text = (em->t == J::Str ? em->s : std::string()) + " " + (cm->t == J::Str ? cm->s : std::string());
-          J res = J::obj();
-          res.add("ruleId", J::str(rule_id));
-          res.add("level", J::str("error"));
-          J mt = J::obj(); mt.add("text", J::str(text));
-          res.add("message", std::move(mt));
-          J art = J::obj(); art.add("uri", J::str(sanitize_path(name)));
-          J region = J::obj();
-          region.add("startLine", J::raw(std::to_string(std::max<int64_t>(line, 1))));
-          region.add("startColumn", J::raw(std::to_string(std::max<int64_t>(col, 1))));
-          J phys = J::obj(); phys.add("artifactLocation", std::move(art)); phys.add("region", std::move(region));
-          J l = J::obj(); l.add("physicalLocation", std::move(phys));
-          J locs = J::arr(); locs.push(std::move(l));
-          res.add("locations", std::move(locs));
-          I.results.push(std::move(res));
-        }
-      }
+      sarif_results(fr, name, I.results);
       break;
     }
     case OUT_JUNIT: {
@@ -1632,27 +1692,8 @@ std::string ReportWriter::finish() {
       return I.yaml->buf;
     }
     case OUT_SARIF: {
-      J drv = J::obj();
-      drv.add("name", J::str("cfn-guard"));
-      drv.add("semanticVersion", J::str("3.1.2"));
-      drv.add("fullName", J::str("cfn-guard 3.1.2"));
-      drv.add("organization", J::str("Amazon Web Services"));
-      drv.add("downloadUri", J::str("https://github.com/aws-cloudformation/cloudformation-guard"));
-      drv.add("informationUri", J::str("https://github.com/aws-cloudformation/cloudformation-guard"));
-      J sd = J::obj(); sd.add("text", J::str(kSarifDescription));
-      drv.add("shortDescription", std::move(sd));
-      J tool = J::obj(); tool.add("driver", std::move(drv));
-      J run = J::obj();
-      run.add("tool", std::move(tool));
-      run.add("artifacts", std::move(I.artifacts));
-      run.add("results", std::move(I.results));
-      J runs = J::arr(); runs.push(std::move(run));
-      J rep = J::obj();
-      rep.add("$schema", J::str("https://docs.oasis-open.org/sarif/sarif/v2.1.0/errata01/os/schemas/sarif-schema-2.1.0.json"));
-      rep.add("version", J::str("2.1.0"));
-      rep.add("runs", std::move(runs));
       std::string out;
-      pretty(rep, 0, out);
+      pretty(sarif_report(std::move(I.artifacts), std::move(I.results)), 0, out);
       return out;
     }
     case OUT_JUNIT:

@@ -151,6 +151,14 @@ class ReportWriter {
   Impl* p_;
 };
 
+// SARIF around the device-rendered results (capi.cpp device_report_sarif): one FAILed document's
+// SarifResults, each as ",\n" + the results array's indent + the pretty object (the device writer's
+// layout; the report's first comma is dropped), nothing for another status; and the report's text before
+// and after the results' items for these artifacts (FAILed documents' first-seen non-empty names).
+bool sarif_doc_results(const DocBatch& docs, uint32_t doc, const std::vector<const Program*>& progs,
+                       const std::vector<const TileResult*>& tiles, std::string& out, ReportError& err);
+void sarif_frame(const std::vector<std::string>& artifact_names, std::string& head, std::string& tail);
+
 // The structured report of documents [first, first + ndocs) rendered on `nthreads` host threads over
 // contiguous document ranges; byte-identical to one ReportWriter fed in order.  tile(d, f) gives
 // document d's tile of program f.

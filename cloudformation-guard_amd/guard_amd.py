@@ -60,6 +60,12 @@ def lib():
                                                   WRITE_FN, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32),
                                                   ctypes.POINTER(ExternError)]
     L.cfn_guard_validate_batch_stream.restype = ctypes.c_int32
+    L.cfn_guard_validate_batch_stream_devices.argtypes = [ctypes.POINTER(ValidateInput), ctypes.c_size_t,
+                                                          ctypes.POINTER(ValidateInput), ctypes.c_size_t, ctypes.c_size_t,
+                                                          ctypes.POINTER(ctypes.c_int32), ctypes.c_size_t, WRITE_FN,
+                                                          ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32),
+                                                          ctypes.POINTER(ExternError)]
+    L.cfn_guard_validate_batch_stream_devices.restype = ctypes.c_int32
     L.gg_synth_texts.argtypes = [ctypes.c_uint64, ctypes.c_size_t, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]
     L.gg_synth_texts.restype = ctypes.c_void_p
     L.gg_texts_inputs.argtypes = [ctypes.c_void_p]
@@ -337,13 +343,16 @@ def validate_structured(rules, data, output="json", params=None):
 WRITE_FN = ctypes.CFUNCTYPE(ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
 
 
-def validate_structured_stream(rules, data, write=None, chunk_docs=0, inputs=None, n_docs=None, count_only=False):
+def validate_structured_stream(rules, data, write=None, chunk_docs=0, inputs=None, n_docs=None, count_only=False,
+                               devices=False):
     """cfn_guard_validate_batch_stream: the JSON report of validate_structured streamed to write(bytes) in
     document order, the documents evaluated in chunks of chunk_docs (0: 262144) on two alternating sessions.
     Returns (text or None, exit_code): the text when write is None (collected), else None.  Raises GuardError on
     an abort (the chunks written before it are a prefix to drop).  inputs / n_docs: a prepared
     ValidateInput array (SynthTexts.inputs) instead of data.  count_only: the text reaches host memory (the
-    library's pinned staging) and only its length is taken -- write(n) gets byte counts (measurement)."""
+    library's pinned staging) and only its length is taken -- write(n) gets byte counts (measurement).
+    devices: a list of HIP ordinals (or None: every visible device) for cfn_guard_validate_batch_stream_devices --
+    chunk k on devices[k % len(devices)], the same bytes; False (default): the one-device entry."""
     R = (ValidateInput * max(1, len(rules)))(*[ValidateInput(_b(t), _b(n)) for n, t in rules])
     if inputs is None:
         inputs = (ValidateInput * max(1, len(data)))(*[ValidateInput(_b(t), _b(n)) for n, t in data])
@@ -360,8 +369,14 @@ def validate_structured_stream(rules, data, write=None, chunk_docs=0, inputs=Non
     cbf = WRITE_FN(cb)
     code = ctypes.c_int32(0)
     err = ExternError()
-    lib().cfn_guard_validate_batch_stream(inputs, n_docs, R, len(rules), chunk_docs, cbf, None, ctypes.byref(code),
-                                          ctypes.byref(err))
+    if devices is False:
+        lib().cfn_guard_validate_batch_stream(inputs, n_docs, R, len(rules), chunk_docs, cbf, None, ctypes.byref(code),
+                                              ctypes.byref(err))
+    else:
+        dv = (ctypes.c_int32 * max(1, len(devices or [])))(*(devices or []))
+        lib().cfn_guard_validate_batch_stream_devices(inputs, n_docs, R, len(rules), chunk_docs,
+                                                      dv if devices is not None else None, len(devices or []), cbf,
+                                                      None, ctypes.byref(code), ctypes.byref(err))
     if err.code != 0:
         _raise(err)
     return (b"".join(parts).decode("utf-8") if write is None else None), code.value

@@ -4,9 +4,12 @@
  * guard-ffi/example/cfn_guard.h): same struct layouts, same error codes
  * (guard-ffi/src/errors.rs:12-38), same JSON bytes.
  * All entry points evaluate on the GPU; without a HIP device they fail with code -1.
- * One device per process: the HIP device current on the thread of the first call (a multi-GPU
- * job sets it per rank, e.g. torch.cuda.set_device(LOCAL_RANK)), or GG_DEVICE=<ordinal>.
- * Later calls may come from any host thread.
+ * Devices: the single-device entry points use the process default device -- the HIP device current on
+ * the thread of the first call (a one-process-per-GPU job sets it per rank, e.g.
+ * torch.cuda.set_device(LOCAL_RANK)), or GG_DEVICE=<ordinal>.  The *_devices / *_gpus entry points take
+ * a device list and shard the documents over it inside the library (one host thread per device); a
+ * session (gg_session_*) is bound to the device current when it first uploads.  Calls may come from any
+ * host thread, concurrently.
  */
 #ifndef CFN_GUARD_MI355X_H
 #define CFN_GUARD_MI355X_H
@@ -81,11 +84,23 @@ char *cfn_guard_validate_batch_devices(const validate_input_t *docs, size_t n_do
  * documents run in chunks of chunk_docs (0: 262144) on two alternating sessions (the next chunk loads and
  * evaluates while this one's report renders on the device), and the report's bytes go to write(ctx, data,
  * len) in order (a nonzero return aborts).  Returns 0 with *exit_code as the one-string call's, or -1 with
- * err on an abort -- after the chunks before the failing one were written (the caller drops that prefix). */
+ * err on an abort -- after the chunks before the failing one were written (the caller drops that prefix).
+ * Threads: `write` is called from the calling thread or from a thread the library owns (the device
+ * reporter's copy thread), never two calls at once, always in document order, and never after this
+ * function has returned. */
 typedef int32_t (*cfn_guard_write_fn)(void *ctx, const char *data, size_t len);
 int32_t cfn_guard_validate_batch_stream(const validate_input_t *docs, size_t n_docs, const validate_input_t *rules,
                                         size_t n_rules, size_t chunk_docs, cfn_guard_write_fn write, void *ctx,
                                         int32_t *exit_code, extern_err_t *err);
+/* The same stream over several GPUs of the process: chunk k (chunk_docs documents, 0 = 16384) is loaded,
+ * evaluated and rendered on devices[k % n_devices] (NULL: every visible device; ordinals may repeat), each
+ * device's pipeline on a host thread of its own; the reports reach `write` in document order from the
+ * calling thread.  Host memory holds at most two chunks' reports per device.  One device: exactly
+ * cfn_guard_validate_batch_stream on that device.  Same bytes, exit code and error behaviour. */
+int32_t cfn_guard_validate_batch_stream_devices(const validate_input_t *docs, size_t n_docs,
+                                                const validate_input_t *rules, size_t n_rules, size_t chunk_docs,
+                                                const int32_t *devices, size_t n_devices, cfn_guard_write_fn write,
+                                                void *ctx, int32_t *exit_code, extern_err_t *err);
 /* synthetic corpora as validate inputs (bench.py): format 0 JSON (synth.cfn_doc), 1 block-style YAML */
 typedef struct gg_texts gg_texts;
 gg_texts *gg_synth_texts(uint64_t first, size_t n, int32_t n_resources, int32_t format, int32_t nthreads);

@@ -139,3 +139,73 @@ def test_resident_arena_host_fallback_documents(monkeypatch):
     assert s.report("json") == (exp, ecode)
     assert n == len(exp.encode()) and code == ecode
     s.close()
+
+
+# ------------------------------------------------------------------------------ SARIF on the device ---
+def _sarif_both(rules, docs, prefix):
+    s = guard_amd.Session()
+    for name, text in rules:
+        s.add_rules(text, name)
+    s.add_docs(docs, ["%s-%d.json" % (prefix, i) for i in range(len(docs))])
+    s.eval(1)
+    s.set_device_report(True)
+    dev = s.report("sarif")
+    s.set_device_report(False)
+    host = s.report("sarif")
+    s.close()
+    assert dev == host
+    return dev
+
+
+@pytest.mark.parametrize("pack,corpus", [
+    ("cfg2", lambda: synth.cfn_corpus(300, start=177, n_resources=30)),
+    ("cfg3", lambda: synth.cfn_corpus(120, start=5100, n_resources=20)),
+    ("cfg4", lambda: synth.tf_corpus(8, start=19, n_resources=50)),
+    ("cfg5", lambda: synth.config_corpus(100, start=60)),
+])
+def test_device_sarif_equals_host_and_oracle(pack, corpus):
+    """SarifReport (sarif.rs:29-53, 127-160, 185-203) with every FAILed document's results rendered on the
+    device (report_gpu.hip rg::file_sarif): byte-identical with the host writer and the oracle"""
+    rules = rule_pack(pack)
+    docs = corpus()
+    out, code = _sarif_both(rules, docs, pack)
+    data = [("%s-%d.json" % (pack, i), d) for i, d in enumerate(docs)]
+    exp, ecode, _ = oracle_validate(rules, data, output="sarif")
+    assert (out, code) == (exp, ecode)
+
+
+@pytest.mark.parametrize("pack", ["capture_rulepack", "edge_rulepack", "ops_rulepack", "count_rulepack", "conv_rulepack",
+                                  "unicode_rulepack", "wordb_rulepack", "nfa_rulepack"])
+def test_device_sarif_packs_equal_host(pack):
+    _sarif_both(_pack_dir(pack), synth.cfn_corpus(60, start=4321, n_resources=12), pack)
+
+
+def test_device_sarif_host_fallback_documents_and_names():
+    """floats / Debug reasons send a document's results to the host writer at its position; repeated and
+    empty document names, and names with a leading '/', keep the reference's artifact dedupe and URIs"""
+    rules = [("f.guard", "rule r { Resources.*.Properties.Size == 10 }\nrule i { Resources.*.Properties.Items[5] exists }\n"
+                         "rule k { Resources.*.Properties.Meta.Foo exists <<custom\nmessage>> }")]
+    docs, names = [], []
+    for i in range(70):
+        size = 2.5 if i % 7 == 0 else (i if i % 5 else "s")
+        items = [1, 2] if i % 3 == 0 else [1, 2, 3, 4, 5, 6]
+        meta = 5 if i % 4 == 0 else {"Foo": 1}
+        docs.append(json.dumps({"Resources": {"a": {"Properties": {"Size": size, "Items": items, "Meta": meta}}}}))
+        names.append(["/abs/p%d.json" % (i % 9), "", "rel/q%d.json" % i][i % 3])
+    data = list(zip(names, docs))
+    exp, ecode, _ = oracle_validate(rules, data, output="sarif")
+    out, code = guard_amd.validate_structured(rules, data, output="sarif")
+    assert (out, code) == (exp, ecode)
+    for devices in ([0, 0], [0, 0, 0]):
+        assert guard_amd.validate_structured_devices(rules, data, devices=devices, output="sarif") == (exp, ecode)
+
+
+def test_device_sarif_golden():
+    gdir = os.path.join(G, "validate")
+    rules = [(f, open(os.path.join(gdir, "rules-dir", f)).read())
+             for f in sorted(os.listdir(os.path.join(gdir, "rules-dir"))) if f.endswith(".guard")]
+    dn = "s3-public-read-prohibited-template-non-compliant.yaml"
+    out, code = guard_amd.validate_structured(rules, [("some/path", open(os.path.join(gdir, "data-dir", dn)).read())],
+                                              output="sarif")
+    assert code == 19
+    assert out == open(os.path.join(gdir, "structured.sarif")).read()

@@ -125,3 +125,41 @@ def test_device_block_cache_reuse_and_release():
     assert guard_amd.validate_structured(rules, b) == exp_b
     assert guard_amd.release_device_cache(0) > 0
     assert guard_amd.release_device_cache(-1) == 0
+
+
+@pytest.mark.parametrize("devices,chunk", [([0, 0], 7), ([0, 0, 0], 32), ([0], 16), (None, 50)])
+def test_stream_devices_equals_one_device_and_oracle(devices, chunk):
+    """cfn_guard_validate_batch_stream_devices: chunks spread over a device list (ordinals repeat on the
+    one-GPU box: separate pipelines, sessions and streams on one device), written in document order -- the
+    one-device stream's bytes and the oracle's"""
+    rules = rule_pack("cfg2")
+    docs = synth.cfn_corpus(110, start=300, n_resources=7) + synth.cfn_yaml_corpus(25, start=40, n_resources=5)
+    data = [("m%d.%s" % (i, "json" if i < 110 else "yaml"), d) for i, d in enumerate(docs)]
+    exp, ecode, _ = oracle_validate(rules, data)
+    assert guard_amd.validate_structured_stream(rules, data, chunk_docs=chunk) == (exp, ecode)
+    assert guard_amd.validate_structured_stream(rules, data, chunk_docs=chunk, devices=devices) == (exp, ecode)
+
+
+def test_stream_devices_errors_and_empty():
+    rules = rule_pack("cfg2")
+    assert (guard_amd.validate_structured_stream(rules, [], chunk_docs=4, devices=[0, 0])
+            == guard_amd.validate_structured(rules, []))
+    bad_rules = [("t.guard", "rule r { Resources.*.Properties.Port empty }")]
+    docs = synth.cfn_corpus(30, start=2, n_resources=4)
+    docs[21] = json.dumps({"Resources": {"b": {"Type": "AWS::S3::Bucket", "Properties": {"Port": 8080}}}})
+    data = [("x%d.json" % i, d) for i, d in enumerate(docs)]
+    with pytest.raises(guard_amd.GuardError) as g1:
+        guard_amd.validate_structured_stream(bad_rules, data, chunk_docs=4)
+    with pytest.raises(guard_amd.GuardError) as g2:
+        guard_amd.validate_structured_stream(bad_rules, data, chunk_docs=4, devices=[0, 0])
+    assert (g1.value.code, g1.value.message) == (g2.value.code, g2.value.message)
+    seen = []
+
+    def write(b):
+        seen.append(b)
+        if len(seen) > 1:
+            raise RuntimeError("disk full")
+    with pytest.raises(guard_amd.GuardError):
+        guard_amd.validate_structured_stream(rule_pack("cfg2"), data, write=write, chunk_docs=5, devices=[0, 0])
+    with pytest.raises(guard_amd.GuardError):
+        guard_amd.validate_structured_stream(rules, data, chunk_docs=5, devices=[])
