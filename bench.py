@@ -211,6 +211,10 @@ def main():
     ap.add_argument("--e2e-stream", type=int, default=262144,
                     help="also time the streamed batch entry (cfn_guard_validate_batch_stream) over the same synthetic "
                          "texts with this many documents per chunk (0: off; cfg2/cfg3 at N=1 only)")
+    ap.add_argument("--e2e-devices-docs", type=int, default=262144,
+                    help="also time the streamed batch entry over every visible device (cfn_guard_validate_batch_stream_"
+                         "devices) with this many synthetic documents per device (0: off; cfg2/cfg3 at N=1 only)")
+    ap.add_argument("--e2e-devices-chunk", type=int, default=16384, help="documents per chunk of the multi-device stream")
     ap.add_argument("--e2e-report-docs", type=int, default=0,
                     help="documents whose structured report is rendered for e2e (0: all, the default); a sample's "
                          "report time is scaled to the whole job")
@@ -474,6 +478,38 @@ def main():
                               "texts resident in host memory: load + upload + evaluation + fetch + device-rendered "
                               "report to host memory, chunked and overlapped; text generation (gen_s) not included"}
 
+    e2e_devices = None
+    if (rank == 0 and world == 1 and not args.no_e2e and args.e2e_devices_docs and args.workload in ("cfg2", "cfg3")
+            and args.loader == "device"):
+        # the in-library multi-GPU path (SURVEY.md 8(b) n_gpus): one process drives every visible device, each
+        # device a pipeline of its own over chunks k = d (mod devices), the report written in document order
+        # (counted); weak scaling, --e2e-devices-docs per device
+        ndev = max(1, torch.cuda.device_count())
+        nd = args.e2e_devices_docs * ndev
+        log("e2e devices: %d documents over %d device(s), chunks of %d" % (nd, ndev, args.e2e_devices_chunk))
+        t0 = time.time()
+        dv_texts = guard_amd.SynthTexts(first, nd, n_resources=args.resources, fmt=args.format, threads=threads)
+        t_gen_d = time.time() - t0
+        nb = [0]
+
+        def _count_d(n):
+            nb[0] += n
+        try:
+            t0 = time.time()
+            _, dv_code = guard_amd.validate_structured_stream(rules, None, write=_count_d, chunk_docs=args.e2e_devices_chunk,
+                                                              inputs=dv_texts.inputs, n_docs=dv_texts.n, count_only=True,
+                                                              devices=list(range(ndev)))
+            t_dv = time.time() - t0
+        finally:
+            dv_texts.close()
+        e2e_devices = {"value": round(nd * nfiles / t_dv, 1), "unit": "evals/s", "devices": ndev, "docs": nd,
+                       "docs_per_device": args.e2e_devices_docs, "chunk_docs": args.e2e_devices_chunk,
+                       "seconds": round(t_dv, 3), "report_bytes": nb[0], "report_GBps": round(nb[0] / t_dv / 1e9, 3),
+                       "exit_code": dv_code, "gen_s": round(t_gen_d, 3),
+                       "note": "cfn_guard_validate_batch_stream_devices over every visible device from one process "
+                               "(load + upload + evaluation + fetch + device-rendered JSON report to host memory, in "
+                               "document order); text generation (gen_s) not included"}
+
     total_units = ntiles * world * args.steps
     value = total_units / elapsed
     if args.workload == "cfg5":
@@ -521,6 +557,8 @@ def main():
         line["e2e"] = e2e
         if e2e_stream is not None:
             line["e2e_stream"] = e2e_stream
+        if e2e_devices is not None:
+            line["e2e_stream_devices"] = e2e_devices
         if gather is not None:
             line["report_gather"] = gather
         print(json.dumps(line), flush=True)

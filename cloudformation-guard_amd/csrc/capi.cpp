@@ -129,10 +129,17 @@ struct Devices {
     if (hipSetDevice(d) != hipSuccess) { why = "hipSetDevice failed"; return false; }
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, d) == hipSuccess) D.ncu = prop.multiProcessorCount;
-    // the evaluator recurses (eval_conj <-> clauses, filters, rule references): 16 KB of lane stack.  32 KB
-    // cannot be had with several queues live (HSA_STATUS_ERROR_OUT_OF_RESOURCES in the concurrent-caller
-    // test); GG_STACK_BYTES overrides
+#if GG_MACHINE
+    // the machine evaluator does not recurse (eval_machine.inc: an explicit continuation stack in the lane
+    // heap): every kernel's private segment is static (~0.6 KB per lane) and the runtime sizes scratch from
+    // it, so the device-wide stack limit is left at its default (GG_STACK_BYTES sets one, diagnostics only)
+    if (getenv("GG_STACK_BYTES")) hipDeviceSetLimit(hipLimitStackSize, default_stack_bytes());
+#else
+    // the recursive evaluator (eval_recursive.inc: eval_conj <-> clauses, filters, rule references) needs a
+    // dynamic lane stack: 16 KB for every kernel variant, the NFA one included (its simulation is a leaf
+    // call, eval_core.inc nfa_match_*), set once and never raised; GG_STACK_BYTES overrides
     hipDeviceSetLimit(hipLimitStackSize, default_stack_bytes());
+#endif
     D.ready = true;
     return true;
   }

@@ -221,7 +221,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
       if (!c.err) for (uint32_t i = 0; i < P->n_slots; i++) u32a(c, c.memo)[i] = 3u;
       c.vtab = alloc_pers(c, (P->n_vars ? P->n_vars : 1) * 16);
       if (!c.err) for (uint32_t i = 0; i < P->n_vars; i++) u32a(c, c.vtab)[i * 4] = 0u;
+#if GG_MACHINE
       c.kbase = alloc_pers(c, KDEPTH * KFRAME); c.kdepth = 0;
+#endif
       push_frame(c, F_ROOT, NONE, A.docs.roots[doc], P->root_block);
       uint32_t fails = 0, passes = 0;
       uint8_t* rs = A.rule_status + (size_t)tile * A.max_top;

@@ -809,6 +809,9 @@ RN void tile_sarif(W& w, const Ctx& c, const RecSeq recs, uint32_t nrec, const c
         const PClause pc = c.P->clauses[rc.clause];
         const uint32_t op = pc.flags & 15u;
         const bool neg = (pc.flags >> 4) & 1u;
+        // eval_context.rs:2231-2234: an unresolved value's location, Location::default() otherwise
+        uint32_t line = 0, col = 0;
+        if (qkind(rc.from) == QR_UNRESOLVED) sarif_loc(w, c, rc.from, line, col);
         sarif_open(w, c, rule);
         if (qkind(rc.from) == QR_UNRESOLVED) {
           tlit(w, "Check was not compliant as property ["); remaining(w, c, rc.from);
@@ -818,7 +821,7 @@ RN void tile_sarif(W& w, const Ctx& c, const RecSeq recs, uint32_t nrec, const c
           tlit(w, unary_msg(op, neg)); tput(w, '.');
         }
         tput(w, ' '); custom_text(w, c, pc);
-        sarif_close(w, uri, urin, 0, 0);
+        sarif_close(w, uri, urin, line, col);
         break;
       }
       case REC_NOVALUE_EMPTY: {

@@ -60,12 +60,13 @@ def lib():
                                                   WRITE_FN, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32),
                                                   ctypes.POINTER(ExternError)]
     L.cfn_guard_validate_batch_stream.restype = ctypes.c_int32
-    L.cfn_guard_validate_batch_stream_devices.argtypes = [ctypes.POINTER(ValidateInput), ctypes.c_size_t,
-                                                          ctypes.POINTER(ValidateInput), ctypes.c_size_t, ctypes.c_size_t,
-                                                          ctypes.POINTER(ctypes.c_int32), ctypes.c_size_t, WRITE_FN,
-                                                          ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32),
-                                                          ctypes.POINTER(ExternError)]
-    L.cfn_guard_validate_batch_stream_devices.restype = ctypes.c_int32
+    if hasattr(L, "cfn_guard_validate_batch_stream_devices"):   # (absent from builds older than round 5: GG_LIB A/B)
+        L.cfn_guard_validate_batch_stream_devices.argtypes = [ctypes.POINTER(ValidateInput), ctypes.c_size_t,
+                                                              ctypes.POINTER(ValidateInput), ctypes.c_size_t,
+                                                              ctypes.c_size_t, ctypes.POINTER(ctypes.c_int32),
+                                                              ctypes.c_size_t, WRITE_FN, ctypes.c_void_p,
+                                                              ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ExternError)]
+        L.cfn_guard_validate_batch_stream_devices.restype = ctypes.c_int32
     L.gg_synth_texts.argtypes = [ctypes.c_uint64, ctypes.c_size_t, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]
     L.gg_synth_texts.restype = ctypes.c_void_p
     L.gg_texts_inputs.argtypes = [ctypes.c_void_p]
