@@ -208,6 +208,8 @@ def main():
     ap.add_argument("--rx-memo", choices=("per-launch", "warm"), default="per-launch",
                     help="regex is_match memo: zeroed before every launch, or kept warm across launches")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--stream-count", default="native", choices=["native", "py"],
+                    help="the streamed legs' write callback: the library's native byte counter, or a Python callback per piece")
     ap.add_argument("--e2e-stream", type=int, default=262144,
                     help="also time the streamed batch entry (cfn_guard_validate_batch_stream) over the same synthetic "
                          "texts with this many documents per chunk (0: off; cfg2/cfg3 at N=1 only)")
@@ -466,7 +468,7 @@ def main():
             t0 = time.time()
             _, st_code = guard_amd.validate_structured_stream(rules, None, write=_count, chunk_docs=args.e2e_stream,
                                                               inputs=st_texts.inputs, n_docs=st_texts.n,
-                                                              count_only=True)
+                                                              count_only=args.stream_count)
             t_stream = time.time() - t0
         finally:
             st_texts.close()
@@ -479,14 +481,16 @@ def main():
                               "report to host memory, chunked and overlapped; text generation (gen_s) not included"}
 
     e2e_devices = None
-    if (rank == 0 and world == 1 and not args.no_e2e and args.e2e_devices_docs and args.workload in ("cfg2", "cfg3")
-            and args.loader == "device"):
-        # the in-library multi-GPU path (SURVEY.md 8(b) n_gpus): one process drives every visible device, each
-        # device a pipeline of its own over chunks k = d (mod devices), the report written in document order
-        # (counted); weak scaling, --e2e-devices-docs per device
-        ndev = max(1, torch.cuda.device_count())
+    if (rank == 0 and not args.no_e2e and args.e2e_devices_docs and args.workload in ("cfg2", "cfg3")
+            and args.loader == "device" and torch.cuda.device_count() >= world):
+        # the in-library multi-GPU path (SURVEY.md 8(b) n_gpus): one process (rank 0, after the ranks' timed
+        # region) drives devices 0 .. N-1 of an N-rank run, each device a pipeline of its own over chunks
+        # k = d (mod N), the report written in document order (counted by the library's native callback);
+        # weak scaling, --e2e-devices-docs per device.  One device: the one-device stream entry's chunks
+        ndev = world
         nd = args.e2e_devices_docs * ndev
-        log("e2e devices: %d documents over %d device(s), chunks of %d" % (nd, ndev, args.e2e_devices_chunk))
+        dchunk = args.e2e_devices_chunk if ndev > 1 else args.e2e_stream
+        log("e2e devices: %d documents over %d device(s), chunks of %d" % (nd, ndev, dchunk))
         t0 = time.time()
         dv_texts = guard_amd.SynthTexts(first, nd, n_resources=args.resources, fmt=args.format, threads=threads)
         t_gen_d = time.time() - t0
@@ -496,17 +500,17 @@ def main():
             nb[0] += n
         try:
             t0 = time.time()
-            _, dv_code = guard_amd.validate_structured_stream(rules, None, write=_count_d, chunk_docs=args.e2e_devices_chunk,
-                                                              inputs=dv_texts.inputs, n_docs=dv_texts.n, count_only=True,
+            _, dv_code = guard_amd.validate_structured_stream(rules, None, write=_count_d, chunk_docs=dchunk,
+                                                              inputs=dv_texts.inputs, n_docs=dv_texts.n, count_only="native",
                                                               devices=list(range(ndev)))
             t_dv = time.time() - t0
         finally:
             dv_texts.close()
         e2e_devices = {"value": round(nd * nfiles / t_dv, 1), "unit": "evals/s", "devices": ndev, "docs": nd,
-                       "docs_per_device": args.e2e_devices_docs, "chunk_docs": args.e2e_devices_chunk,
+                       "docs_per_device": args.e2e_devices_docs, "chunk_docs": dchunk,
                        "seconds": round(t_dv, 3), "report_bytes": nb[0], "report_GBps": round(nb[0] / t_dv / 1e9, 3),
                        "exit_code": dv_code, "gen_s": round(t_gen_d, 3),
-                       "note": "cfn_guard_validate_batch_stream_devices over every visible device from one process "
+                       "note": "cfn_guard_validate_batch_stream_devices over devices 0..N-1 from one process (rank 0) "
                                "(load + upload + evaluation + fetch + device-rendered JSON report to host memory, in "
                                "document order); text generation (gen_s) not included"}
 

@@ -2170,6 +2170,42 @@ std::unique_ptr<gg_session> stream_chunk_session(int dev, const validate_input_t
 }
 }  // namespace
 
+namespace {
+// A chunk's report lands by D2H in pinned host blocks (a device-to-pageable copy is staged through
+// the runtime's bounce buffers at a fraction of the PCIe rate) and goes to the callback from there;
+// written blocks are recycled, so after the first chunks no block is allocated or pinned again.
+struct PinnedPool {
+  static constexpr size_t kBlock = (size_t)64 << 20;
+  std::mutex mu;
+  std::vector<char*> all, avail;
+  char* get() {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      if (!avail.empty()) { char* p = avail.back(); avail.pop_back(); return p; }
+    }
+    char* p = nullptr;
+    HIPCHK(hipHostMalloc((void**)&p, kBlock, hipHostMallocDefault));
+    std::lock_guard<std::mutex> lk(mu);
+    all.push_back(p);
+    return p;
+  }
+  void put(char* p) { std::lock_guard<std::mutex> lk(mu); avail.push_back(p); }
+  ~PinnedPool() { for (char* p : all) hipHostFree(p); }
+};
+struct ChainSink : ReportSink {
+  PinnedPool& pool;
+  std::vector<std::pair<char*, size_t>> blocks;   // (block, bytes used)
+  uint64_t n = 0;
+  explicit ChainSink(PinnedPool& p) : pool(p) {}
+  char* reserve(size_t k) override {
+    if (blocks.empty() || blocks.back().second + k > PinnedPool::kBlock) blocks.push_back({pool.get(), 0});
+    return blocks.back().first + blocks.back().second;
+  }
+  void commit(size_t k) override { blocks.back().second += k; n += k; }
+  size_t max_piece() const override { return PinnedPool::kBlock; }
+};
+}  // namespace
+
 int32_t cfn_guard_validate_batch_stream_devices(const validate_input_t* docs, size_t n_docs, const validate_input_t* rules,
                                                 size_t n_rules, size_t chunk_docs, const int32_t* devices, size_t n_devices,
                                                 cfn_guard_write_fn write, void* ctx, int32_t* exit_code, extern_err_t* err) {
@@ -2195,15 +2231,17 @@ int32_t cfn_guard_validate_batch_stream_devices(const validate_input_t* docs, si
     if (ndev == 1) return stream_single(devs[0], docs, n_docs, rules, n_rules, chunk_docs, write, ctx, exit_code, err);
     const size_t chunk = chunk_docs ? chunk_docs : (size_t)16384;
     const size_t nchunks = (n_docs + chunk - 1) / chunk;
+    PinnedPool pool;
     struct Out {
       int state = 0;          // 0 pending, 1 ready, 2 failed
-      BufferSink text;
+      ChainSink text;
+      explicit Out(PinnedPool& p) : text(p) {}
       bool anyfail = false;
       int32_t parse_code = 0;
       std::string kind, msg;
     };
     std::vector<std::unique_ptr<Out>> outs(nchunks);
-    for (auto& o : outs) o.reset(new Out());
+    for (auto& o : outs) o.reset(new Out(pool));
     std::mutex mu;
     std::condition_variable cv;
     size_t written = 0;
@@ -2266,14 +2304,15 @@ int32_t cfn_guard_validate_batch_stream_devices(const validate_input_t* docs, si
       if (o.state == 2) return fail(ffi_code(o.kind), error_display(o.kind, o.msg));
       if (k == 0) { parse_code = o.parse_code; sink.write("[\n", 2); }
       anyfail = anyfail || o.anyfail;
-      // the buffer goes to the callback as it is, in pieces of at most 256 MB (no staging copy); a
+      // the pinned blocks go to the callback as they are (no staging copy), then back to the pool; a
       // failing callback ends the stream
-      for (size_t at = 0; at < o.text.n && !sink.failed; at += (size_t)256 << 20)
-        if (write(ctx, o.text.p + at, std::min(o.text.n - at, (size_t)256 << 20)) != 0) sink.failed = true;
+      for (auto& b : o.text.blocks) {
+        if (!sink.failed && b.second && write(ctx, b.first, b.second) != 0) sink.failed = true;
+        pool.put(b.first);
+      }
+      o.text.blocks.clear();
       sink.n += o.text.n;
       if (sink.failed) return fail(-1, "the write callback failed");
-      free(o.text.p);
-      o.text.p = nullptr; o.text.n = o.text.cap = 0;
       {
         std::lock_guard<std::mutex> lk(mu);
         written = k + 1;
@@ -2957,6 +2996,13 @@ int64_t gg_session_report_json_device(gg_session* s, size_t max_docs, int32_t* e
     }
     return bytes;
   } catch (std::exception& e) { set_err(err, -1, e.what()); return -1; }
+}
+
+// a native write callback for cfn_guard_validate_batch_stream(_devices) that counts the bytes into *(uint64_t*)ctx
+// and drops them (measurement: the report reaches host memory with no consumer cost on the path)
+int32_t gg_count_write(void* ctx, const char*, size_t len) {
+  if (ctx) *(uint64_t*)ctx += len;
+  return 0;
 }
 
 int32_t gg_session_set_device_report(gg_session* s, int32_t on) { s->device_report = on < 0 ? -1 : (on ? 1 : 0); return 0; }

@@ -351,7 +351,8 @@ def validate_structured_stream(rules, data, write=None, chunk_docs=0, inputs=Non
     Returns (text or None, exit_code): the text when write is None (collected), else None.  Raises GuardError on
     an abort (the chunks written before it are a prefix to drop).  inputs / n_docs: a prepared
     ValidateInput array (SynthTexts.inputs) instead of data.  count_only: the text reaches host memory (the
-    library's pinned staging) and only its length is taken -- write(n) gets byte counts (measurement).
+    library's pinned staging) and only its length is taken -- write(n) gets byte counts (measurement); "native":
+    the library's counting callback (gg_count_write) takes them, write(total) is called once at the end.
     devices: a list of HIP ordinals (or None: every visible device) for cfn_guard_validate_batch_stream_devices --
     chunk k on devices[k % len(devices)], the same bytes; False (default): the one-device entry."""
     R = (ValidateInput * max(1, len(rules)))(*[ValidateInput(_b(t), _b(n)) for n, t in rules])
@@ -367,19 +368,28 @@ def validate_structured_stream(rules, data, write=None, chunk_docs=0, inputs=Non
             return 0
         except Exception:
             return 1
-    cbf = WRITE_FN(cb)
+    counted = ctypes.c_uint64(0)
+    ctx = None
+    if count_only == "native":
+        # the library's own counting callback (gg_count_write): no Python call per piece; write(total) at the end
+        cbf = ctypes.cast(lib().gg_count_write, WRITE_FN)
+        ctx = ctypes.cast(ctypes.byref(counted), ctypes.c_void_p)
+    else:
+        cbf = WRITE_FN(cb)
     code = ctypes.c_int32(0)
     err = ExternError()
     if devices is False:
-        lib().cfn_guard_validate_batch_stream(inputs, n_docs, R, len(rules), chunk_docs, cbf, None, ctypes.byref(code),
+        lib().cfn_guard_validate_batch_stream(inputs, n_docs, R, len(rules), chunk_docs, cbf, ctx, ctypes.byref(code),
                                               ctypes.byref(err))
     else:
         dv = (ctypes.c_int32 * max(1, len(devices or [])))(*(devices or []))
         lib().cfn_guard_validate_batch_stream_devices(inputs, n_docs, R, len(rules), chunk_docs,
                                                       dv if devices is not None else None, len(devices or []), cbf,
-                                                      None, ctypes.byref(code), ctypes.byref(err))
+                                                      ctx, ctypes.byref(code), ctypes.byref(err))
     if err.code != 0:
         _raise(err)
+    if count_only == "native" and write is not None:
+        write(counted.value)
     return (b"".join(parts).decode("utf-8") if write is None else None), code.value
 
 

@@ -28,6 +28,16 @@ def test_free_string_null_is_noop():
     guard_amd.lib().cfn_guard_free_string(None)
 
 
+def test_native_count_callback_counts_and_accepts():
+    # gg_count_write: the measurement sink of the streamed entries (bench --stream-count native)
+    fn = ctypes.cast(guard_amd.lib().gg_count_write, guard_amd.WRITE_FN)
+    n = ctypes.c_uint64(5)
+    buf = ctypes.create_string_buffer(b"abcdef")
+    assert fn(ctypes.cast(ctypes.byref(n), ctypes.c_void_p), ctypes.cast(buf, ctypes.c_void_p), 6) == 0
+    assert n.value == 11
+    assert fn(None, None, 3) == 0
+
+
 @pytest.mark.skipif(guard_amd.lib().gg_device_available() > 0, reason="GPU present")
 def test_no_cpu_fallback():
     with pytest.raises(guard_amd.GuardError) as ei:
