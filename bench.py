@@ -208,6 +208,7 @@ def main():
     ap.add_argument("--rx-memo", choices=("per-launch", "warm"), default="per-launch",
                     help="regex is_match memo: zeroed before every launch, or kept warm across launches")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--e2e-sarif", type=int, default=1, help="also time the e2e job with the SARIF report (device results)")
     ap.add_argument("--stream-count", default="native", choices=["native", "py"],
                     help="the streamed legs' write callback: the library's native byte counter, or a Python callback per piece")
     ap.add_argument("--e2e-stream", type=int, default=262144,
@@ -413,6 +414,7 @@ def main():
                       "error": gerr}
 
     e2e = None
+    e2e_sarif = None
     if rank == 0 and world == 1 and not args.no_e2e:
         rdocs = min(ndocs, args.e2e_report_docs) if args.e2e_report_docs else ndocs
         log("e2e: structured report of %d of %d documents" % (rdocs, ndocs))
@@ -448,6 +450,20 @@ def main():
                        "synthetic text generation (gen_s) is not part of the job%s"
                        % (("device %s loader: text H2D, parse, intern index to the host (the arena stays in HBM)" % args.format.upper()) if args.loader == "device"
                           else "host loader threads", " (inside load_s with --loader host)" if gen_in_load else "")}
+
+        if args.reporter == "device" and args.e2e_sarif and hasattr(sess, "report_sarif_device"):
+            # the same job with the SARIF report (row N2): artifacts and frame on the host, every FAILed
+            # document's results rendered on the device from the same records, copied out and counted
+            t0 = time.time()
+            sr_bytes, sr_code, sr_stats = sess.report_sarif_device(rdocs)
+            t_sr_sample = time.time() - t0
+            t_sr = t_sr_sample * ndocs / max(1, rdocs)
+            e2e_sarif = {"value": round(ntiles / (t_load_job + t_upload + t_eval + t_sr), 1), "unit": "evals/s",
+                         "report_s": round(t_sr, 3), "report_bytes_rendered": sr_bytes,
+                         "report_GBps": round(sr_bytes / t_sr_sample / 1e9, 3), "exit_code": sr_code,
+                         "device_reporter": sr_stats,
+                         "note": "e2e with -o sarif: load, upload and evaluation as e2e, the SARIF report rendered on "
+                                 "the device (results) and host (artifacts, frame), copied to host memory and discarded"}
 
     e2e_stream = None
     if (rank == 0 and world == 1 and not args.no_e2e and args.e2e_stream and args.workload in ("cfg2", "cfg3")
@@ -559,6 +575,8 @@ def main():
         }
         line["cpu_baseline"] = cpu
         line["e2e"] = e2e
+        if e2e_sarif is not None:
+            line["e2e_sarif"] = e2e_sarif
         if e2e_stream is not None:
             line["e2e_stream"] = e2e_stream
         if e2e_devices is not None:

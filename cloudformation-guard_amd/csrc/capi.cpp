@@ -2998,6 +2998,64 @@ int64_t gg_session_report_json_device(gg_session* s, size_t max_docs, int32_t* e
   } catch (std::exception& e) { set_err(err, -1, e.what()); return -1; }
 }
 
+// The SARIF report of the first max_docs documents (0: all): the artifact list and frame on the host, every
+// FAILed document's results rendered on the device (report_sarif_kernel), copied to host memory and dropped
+// (measurement, as gg_session_report_json_device).  Returns the report's byte count.
+int64_t gg_session_report_sarif_device(gg_session* s, size_t max_docs, int32_t* exit_code, double* stats, extern_err_t* err) {
+  set_err(err, 0, "");
+  if (!s->evaluated || !s->fetched_on_device) { set_err(err, -1, "session not evaluated and fetched on a device"); return -1; }
+  try {
+    std::vector<const Program*> progs;
+    for (auto& p : s->progs) progs.push_back(&p->prog);
+    const size_t nf = progs.size(), nd = max_docs ? std::min(max_docs, s->docs.ndocs()) : s->docs.ndocs();
+    for (size_t t = 0; t < nd * nf; t++)
+      if (s->tiles[t].err) {
+        ensure_host_arena(s);
+        ReportError re;
+        tile_error(s->docs, (uint32_t)(t / nf), *progs[t % nf], s->tiles[t], re);
+        set_err(err, ffi_code(re.kind), error_display(re.kind, re.msg));
+        if (exit_code) *exit_code = -1;
+        return -1;
+      }
+    // SarifReport::new (sarif.rs:29-53): the FAILed documents' first-seen non-empty names
+    std::vector<std::string> art;
+    std::unordered_set<std::string> seen;
+    bool anyfail = false;
+    for (size_t d = 0; d < nd; d++) {
+      uint32_t status = ST_SKIP;
+      for (size_t f = 0; f < nf; f++) {
+        const uint32_t st = s->tiles[d * nf + f].status;
+        if (status == ST_FAIL) continue;
+        status = status == ST_PASS ? (st == ST_FAIL ? ST_FAIL : ST_PASS) : st;
+      }
+      if (status != ST_FAIL) continue;
+      anyfail = true;
+      const std::string& name = s->docs.names[d];
+      if (!name.empty() && seen.insert(name).second) art.push_back(name);
+    }
+    std::string head, tail;
+    sarif_frame(art, head, tail);
+    bind_device(s);
+    render_tables(s);
+    CountingSink sink(s->dv->pinned, DeviceBufs::kPinnedBytes);
+    DevReportStats st;
+    ReportError re;
+    if (nf && !device_report_text(s, 0, nd, SIZE_MAX, sink, re, &st, OUT_SARIF)) {
+      set_err(err, ffi_code(re.kind), error_display(re.kind, re.msg));
+      if (exit_code) *exit_code = -1;
+      return -1;
+    }
+    // the results' first comma is dropped (serde's "[\n        {"), "\n      " closes a non-empty list
+    const int64_t bytes = (int64_t)(head.size() + tail.size() + (sink.n ? sink.n - 1 + 7 : 0));
+    if (exit_code) *exit_code = anyfail ? 19 : (s->parse_errors.empty() ? 0 : 5);
+    if (stats) {
+      stats[0] = (double)st.device_docs; stats[1] = (double)st.host_docs; stats[2] = st.size_ms; stats[3] = st.write_ms;
+      stats[4] = st.d2h_ms; stats[5] = st.host_ms; stats[6] = (double)st.bytes; stats[7] = (double)art.size();
+    }
+    return bytes;
+  } catch (std::exception& e) { set_err(err, -1, e.what()); return -1; }
+}
+
 // a native write callback for cfn_guard_validate_batch_stream(_devices) that counts the bytes into *(uint64_t*)ctx
 // and drops them (measurement: the report reaches host memory with no consumer cost on the path)
 int32_t gg_count_write(void* ctx, const char*, size_t len) {

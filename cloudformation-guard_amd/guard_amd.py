@@ -93,6 +93,9 @@ def lib():
     L.gg_session_report_json_device.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int32),
                                                 ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ExternError)]
     L.gg_session_report_json_device.restype = ctypes.c_int64
+    if hasattr(L, "gg_session_report_sarif_device"):
+        L.gg_session_report_sarif_device.argtypes = L.gg_session_report_json_device.argtypes
+        L.gg_session_report_sarif_device.restype = ctypes.c_int64
     L.gg_session_set_device_report.argtypes = [ctypes.c_void_p, ctypes.c_int32]
     L.gg_session_set_device_report.restype = ctypes.c_int32
     L.gg_session_set_device.argtypes = [ctypes.c_void_p, ctypes.c_int32]
@@ -631,6 +634,18 @@ class Session:
             _raise(err)
         keys = ("device_docs", "host_docs", "size_ms", "write_ms", "d2h_ms", "host_ms", "body_bytes")
         return n, code.value, dict(zip(keys, list(st)[:7]))
+
+    def report_sarif_device(self, max_docs=0):
+        """the SARIF report of the first max_docs documents (0: all): results rendered on the device, copied to
+        host memory and discarded: (bytes, exit code, stats)"""
+        code = ctypes.c_int32(0)
+        st = (ctypes.c_double * 8)()
+        err = ExternError()
+        n = lib().gg_session_report_sarif_device(self.s, max_docs, ctypes.byref(code), st, ctypes.byref(err))
+        if err.code != 0:
+            _raise(err)
+        keys = ("device_docs", "host_docs", "size_ms", "write_ms", "d2h_ms", "host_ms", "body_bytes", "artifacts")
+        return n, code.value, dict(zip(keys, list(st)))
 
     def set_device_report(self, on):
         """JSON reports rendered on the device (True), on host threads (False), or per GG_DEVICE_REPORT (None)"""

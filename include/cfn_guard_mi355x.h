@@ -242,6 +242,8 @@ int64_t gg_session_report_bytes(gg_session *s, int32_t output_format, size_t max
  * device); stats (may be NULL, 8 doubles): device documents, host documents, size-pass ms, write-pass ms,
  * copy-out ms, host-writer ms, body bytes, 0. */
 int64_t gg_session_report_json_device(gg_session *s, size_t max_docs, int32_t *exit_code, double *stats, extern_err_t *err);
+/* the SARIF report (artifacts + frame on the host, FAILed documents' results rendered on the device), counted */
+int64_t gg_session_report_sarif_device(gg_session *s, size_t max_docs, int32_t *exit_code, double *stats, extern_err_t *err);
 /* JSON reports of this session (gg_session_report*, the batch entry points): 1 rendered on the device
  * (default, GG_DEVICE_REPORT=0 turns it off), 0 on host threads, -1 back to the environment's choice. */
 int32_t gg_session_set_device_report(gg_session *s, int32_t on);

@@ -152,8 +152,11 @@ def _sarif_both(rules, docs, prefix):
     dev = s.report("sarif")
     s.set_device_report(False)
     host = s.report("sarif")
+    # the counted entry the bench's e2e SARIF leg times: the same byte count and exit code
+    n, code, st = s.report_sarif_device()
     s.close()
     assert dev == host
+    assert n == len(host[0].encode()) and code == host[1]
     return dev
 
 
