@@ -27,6 +27,7 @@
 
 #include "../../include/cfn_guard_mi355x.h"
 #include "dev_cache.h"
+#include "host_pinned.h"
 #include "doc_loader.h"
 #include "eval_device.h"
 #include "host_format.h"
@@ -314,7 +315,7 @@ struct DeviceBufs {
   explicit DeviceBufs(int d) : device(d) { HIPCHK(hipSetDevice(d)); HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking)); }
   ~DeviceBufs() {
     hipSetDevice(device);
-    if (pinned) hipHostFree(pinned);
+    if (pinned) pinned_free(pinned);
     if (copy_stream) hipStreamDestroy(copy_stream);
     for (auto& pr : evq) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
     if (stream) hipStreamDestroy(stream);
@@ -1152,7 +1153,10 @@ void render_tables(gg_session* s) {
     }
     s->marks_on_device = true;
   }
-  if (!s->dv->pinned) HIPCHK(hipHostMalloc((void**)&s->dv->pinned, DeviceBufs::kPinnedBytes, hipHostMallocDefault));
+  if (!s->dv->pinned) {
+    s->dv->pinned = (char*)pinned_alloc(DeviceBufs::kPinnedBytes, s->device);
+    if (!s->dv->pinned) throw std::runtime_error("pinned host staging: allocation failed");
+  }
   HIPCHK(hipStreamSynchronize(st));
   s->rtab_ready = true;
 }
@@ -1931,8 +1935,9 @@ int32_t stream_single(int dev, const validate_input_t* docs, size_t n_docs, cons
     // runs, so that the chunks' own blocks fit under the cache bound and are reused from chunk 3 on
     dev_cache_flush(dev);
     char* stage = nullptr;
-    HIPCHK(hipHostMalloc((void**)&stage, DeviceBufs::kPinnedBytes, hipHostMallocDefault));
-    struct StageFree { char* p; ~StageFree() { if (p) hipHostFree(p); } } stage_free{stage};
+    stage = (char*)pinned_alloc(DeviceBufs::kPinnedBytes, dev);
+    if (!stage) throw std::runtime_error("pinned host staging: allocation failed");
+    struct StageFree { char* p; ~StageFree() { pinned_free(p); } } stage_free{stage};
     CallbackSink sink(write, ctx, stage, DeviceBufs::kPinnedBytes);
     // producer / consumer over two slots
     struct Slot {
@@ -2183,14 +2188,16 @@ struct PinnedPool {
       std::lock_guard<std::mutex> lk(mu);
       if (!avail.empty()) { char* p = avail.back(); avail.pop_back(); return p; }
     }
-    char* p = nullptr;
-    HIPCHK(hipHostMalloc((void**)&p, kBlock, hipHostMallocDefault));
+    int dev = 0;
+    HIPCHK(hipGetDevice(&dev));
+    char* p = (char*)pinned_alloc(kBlock, dev);   // on the node of the calling pipeline's device
+    if (!p) throw std::runtime_error("pinned host block: allocation failed");
     std::lock_guard<std::mutex> lk(mu);
     all.push_back(p);
     return p;
   }
   void put(char* p) { std::lock_guard<std::mutex> lk(mu); avail.push_back(p); }
-  ~PinnedPool() { for (char* p : all) hipHostFree(p); }
+  ~PinnedPool() { for (char* p : all) pinned_free(p); }
 };
 struct ChainSink : ReportSink {
   PinnedPool& pool;

@@ -1,0 +1,86 @@
+// Pinned host memory on the NUMA node of a device (the DMA staging of report copies and text uploads).
+//
+// hipHostMalloc places its pages wherever the calling thread happens to run: on a two-socket host a
+// staging buffer on the far socket moves every device-to-host byte across the inter-socket link as well
+// as PCIe.  pinned_alloc maps the pages itself, binds them to the device's node (the PCI device's
+// numa_node in sysfs), touches them there and registers them with the runtime; without a known node, or
+// when any step fails, it falls back to hipHostMalloc.  GG_PINNED_NUMA=0 turns the placement off (A/B).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <numaif.h>
+#include <sys/mman.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <unordered_map>
+
+namespace gg {
+
+// the NUMA node of HIP device `dev` (-1: unknown / single node)
+inline int device_numa_node(int dev) {
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, sizeof(bus), dev) != hipSuccess) return -1;
+  for (char* p = bus; *p; p++) *p = (char)tolower(*p);
+  char path[160];
+  snprintf(path, sizeof(path), "/sys/bus/pci/devices/%s/numa_node", bus);
+  FILE* f = fopen(path, "r");
+  if (!f) return -1;
+  int node = -1;
+  if (fscanf(f, "%d", &node) != 1) node = -1;
+  fclose(f);
+  return node;
+}
+
+struct PinnedRegistry {
+  std::mutex mu;
+  std::unordered_map<void*, size_t> mapped;   // pinned_alloc'd by mmap + hipHostRegister: bytes
+  static PinnedRegistry& get() { static PinnedRegistry r; return r; }
+};
+
+inline void* pinned_alloc(size_t bytes, int dev) {
+  const char* e = getenv("GG_PINNED_NUMA");
+  const int node = (e && atoi(e) == 0) ? -1 : device_numa_node(dev);
+  if (node >= 0 && node < 64) {
+    void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (p != MAP_FAILED) {
+      unsigned long mask = 1ul << node;
+      bool ok = syscall(SYS_mbind, p, bytes, MPOL_BIND, &mask, 64ul, 0u) == 0;
+      if (ok) memset(p, 0, bytes);   // first touch: the pages are allocated on the node now
+      if (ok) ok = hipHostRegister(p, bytes, hipHostRegisterDefault) == hipSuccess;
+      if (ok) {
+        PinnedRegistry& r = PinnedRegistry::get();
+        std::lock_guard<std::mutex> lk(r.mu);
+        r.mapped[p] = bytes;
+        return p;
+      }
+      munmap(p, bytes);
+    }
+  }
+  void* q = nullptr;
+  if (hipHostMalloc(&q, bytes, hipHostMallocDefault) != hipSuccess) return nullptr;
+  return q;
+}
+
+inline void pinned_free(void* p) {
+  if (!p) return;
+  size_t bytes = 0;
+  {
+    PinnedRegistry& r = PinnedRegistry::get();
+    std::lock_guard<std::mutex> lk(r.mu);
+    auto it = r.mapped.find(p);
+    if (it != r.mapped.end()) { bytes = it->second; r.mapped.erase(it); }
+  }
+  if (bytes) {
+    (void)hipHostUnregister(p);
+    munmap(p, bytes);
+  } else {
+    (void)hipHostFree(p);
+  }
+}
+
+}  // namespace gg

@@ -31,6 +31,7 @@
 #define GG_POW5_QUAL __constant__
 #include "eisel_lemire.h"
 #include "dev_cache.h"
+#include "host_pinned.h"
 
 #include <algorithm>
 #include <chrono>
@@ -700,8 +701,10 @@ struct Staging {
   hipEvent_t ev[2] = {nullptr, nullptr};
   int threads = 1;
   Staging() {
-    JCHK(hipHostMalloc(&pin[0], kChunk, hipHostMallocDefault));
-    JCHK(hipHostMalloc(&pin[1], kChunk, hipHostMallocDefault));
+    int dev = 0;
+    JCHK(hipGetDevice(&dev));
+    for (int i = 0; i < 2; i++)
+      if (!(pin[i] = pinned_alloc(kChunk, dev))) throw std::runtime_error("pinned host staging: allocation failed");
     JCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     JCHK(hipEventCreateWithFlags(&ev[0], hipEventDisableTiming));
     JCHK(hipEventCreateWithFlags(&ev[1], hipEventDisableTiming));
@@ -709,7 +712,7 @@ struct Staging {
   }
   ~Staging() {
     if (s) { hipStreamSynchronize(s); hipStreamDestroy(s); }
-    for (int i = 0; i < 2; i++) { if (pin[i]) hipHostFree(pin[i]); if (ev[i]) hipEventDestroy(ev[i]); }
+    for (int i = 0; i < 2; i++) { pinned_free(pin[i]); if (ev[i]) hipEventDestroy(ev[i]); }
   }
   // fn(t, nthreads) on `threads` host threads
   template <typename F>
