@@ -45,6 +45,7 @@ struct PinnedRegistry {
 inline void* pinned_alloc(size_t bytes, int dev) {
   const char* e = getenv("GG_PINNED_NUMA");
   const int node = (e && atoi(e) == 0) ? -1 : device_numa_node(dev);
+  if (getenv("GG_PINNED_TRACE")) fprintf(stderr, "[pinned] %zu bytes for device %d: NUMA node %d\n", bytes, dev, node);
   if (node >= 0 && node < 64) {
     void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
     if (p != MAP_FAILED) {

@@ -7,6 +7,7 @@
 #   ktrace:<cfg>   rocprofv3 --kernel-trace --stats of bench.py --workload <cfg> (5 timed steps)
 #   pmc:<cfg>      FETCH_SIZE / WRITE_SIZE passes (tools/pmc_traffic.sh)
 #   lds:<cfg>      SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE / SQ_INSTS_LDS pass
+#   ldsnfa         the same counters over the NFA rule pack (tools/nfa_probe.py)
 # Outputs under gpurun_out/$TAG.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
@@ -43,6 +44,10 @@ for step in $STEPS; do
          --output-format csv -d $O/lds_$W -o run -- python3 $R/bench.py --workload $W --docs $(docs_of $W) --steps 1 \
          --warmup 1 --no-cpu-baseline --no-e2e > $O/lds_$W.log 2>&1) || { tail -8 $O/lds_$W.log; exit 1; }
       echo "lds $W done";;
+    ldsnfa)
+      (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS --kernel-trace \
+         --output-format csv -d $O/lds_nfa -o run -- python3 $R/tools/nfa_probe.py 200000 > $O/lds_nfa.log 2>&1) || { tail -8 $O/lds_nfa.log; exit 1; }
+      echo "lds nfa done";;
     *) echo "unknown step $step"; exit 2;;
   esac
 done
