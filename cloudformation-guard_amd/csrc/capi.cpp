@@ -1935,9 +1935,9 @@ int32_t stream_single(int dev, const validate_input_t* docs, size_t n_docs, cons
     // runs, so that the chunks' own blocks fit under the cache bound and are reused from chunk 3 on
     dev_cache_flush(dev);
     char* stage = nullptr;
-    stage = (char*)pinned_alloc(DeviceBufs::kPinnedBytes, dev);
+    stage = (char*)pinned_get(DeviceBufs::kPinnedBytes, dev);
     if (!stage) throw std::runtime_error("pinned host staging: allocation failed");
-    struct StageFree { char* p; ~StageFree() { pinned_free(p); } } stage_free{stage};
+    struct StageFree { char* p; int d; ~StageFree() { pinned_put(p, DeviceBufs::kPinnedBytes, d); } } stage_free{stage, dev};
     CallbackSink sink(write, ctx, stage, DeviceBufs::kPinnedBytes);
     // producer / consumer over two slots
     struct Slot {
@@ -2182,7 +2182,8 @@ namespace {
 struct PinnedPool {
   static constexpr size_t kBlock = (size_t)64 << 20;
   std::mutex mu;
-  std::vector<char*> all, avail;
+  std::vector<std::pair<char*, int>> all;   // every block of the call, with its device
+  std::vector<char*> avail;
   char* get() {
     {
       std::lock_guard<std::mutex> lk(mu);
@@ -2190,14 +2191,14 @@ struct PinnedPool {
     }
     int dev = 0;
     HIPCHK(hipGetDevice(&dev));
-    char* p = (char*)pinned_alloc(kBlock, dev);   // on the node of the calling pipeline's device
+    char* p = (char*)pinned_get(kBlock, dev);   // on the node of the calling pipeline's device
     if (!p) throw std::runtime_error("pinned host block: allocation failed");
     std::lock_guard<std::mutex> lk(mu);
-    all.push_back(p);
+    all.push_back({p, dev});
     return p;
   }
   void put(char* p) { std::lock_guard<std::mutex> lk(mu); avail.push_back(p); }
-  ~PinnedPool() { for (char* p : all) pinned_free(p); }
+  ~PinnedPool() { for (auto& b : all) pinned_put(b.first, kBlock, b.second); }
 };
 struct ChainSink : ReportSink {
   PinnedPool& pool;
