@@ -55,6 +55,7 @@ __global__ void root_resources_kernel(const DNode* nodes, const uint64_t* base, 
 __global__ void pack_nodes_kernel(const DNode* in, DNodeP* out, uint32_t* klen, uint32_t* parent, uint64_t n, uint32_t* bad);
 __global__ void report_kernel(RenderArgs A, uint32_t write);
 __global__ void report_sarif_kernel(RenderArgs A, uint32_t write);
+void d2h_push(void* dst, const void* src, size_t bytes, hipStream_t st, int blocks);
 __global__ void rec_block_sums_kernel(const TileOut* tiles, uint32_t n, uint32_t* bsum);
 __global__ void rec_scan_sums_kernel(uint32_t* bsum, uint32_t nb, uint32_t* total);
 __global__ void rec_compact_kernel(const TileOut* tiles, uint32_t n, const uint32_t* bsum, const Rec* src, Rec* dst,
@@ -323,7 +324,10 @@ struct DeviceBufs {
   // every device buffer back to the device block cache (the stream, events and pinned staging stay)
   void release_device() {
     d_nodes.release(); d_klen.release(); d_parent.release(); d_line.release(); d_col.release(); d_rtab.release(); d_rprogs.release();
-    for (auto& r : rset) { r.names.release(); r.text.release(); r.name_off.release(); r.sizes.release(); r.offs.release(); }
+    // GG_KEEP_RENDER=1 (diagnostic): the report's text buffers stay with the set (copy-out rate A/B)
+    static const bool keep_render = getenv("GG_KEEP_RENDER") && atoi(getenv("GG_KEEP_RENDER")) != 0;
+    if (!keep_render)
+      for (auto& r : rset) { r.names.release(); r.text.release(); r.name_off.release(); r.sizes.release(); r.offs.release(); }
     d_bytes.release(); d_roots.release(); d_base.release(); d_res_map.release(); d_tix_off.release(); d_order.release(); d_tix.release();
     d_progs.release(); d_rx_memo.release(); d_heaps.release(); d_lane_heaps.release(); d_retry.release(); d_big_heaps.release();
     d_retry2.release(); d_tiles.release(); d_rule_status.release(); d_recs.release(); d_recs_dense.release(); d_dense_off.release();
@@ -1180,6 +1184,9 @@ bool device_report_text(gg_session* s, size_t first, size_t count, size_t report
   for (auto& p : s->progs) progs.push_back(&p->prog);
   const size_t nf = progs.size();
   const size_t kBlock = getenv("GG_DREPORT_BLOCK") ? (size_t)std::max(1, atoi(getenv("GG_DREPORT_BLOCK"))) : 65536;
+  // GG_D2H_PUSH=<blocks>: the copy-out by a shader kernel of that many workgroups (d2h_push) instead of
+  // the copy engine
+  const int push_blocks = getenv("GG_D2H_PUSH") ? std::max(0, atoi(getenv("GG_D2H_PUSH"))) : 0;
   DevReportStats local;
   DevReportStats& S = stats ? *stats : local;
   // GG_DREPORT_TRACE=1: per-block wall-clock spans of the render and the copy-out on stderr (overlap check)
@@ -1257,7 +1264,15 @@ bool device_report_text(gg_session* s, size_t first, size_t count, size_t report
           uint64_t at = b.offs[k];
           while (bytes) {
             const size_t piece = (size_t)std::min<uint64_t>(bytes, sink.max_piece());
-            HIPCHK(hipMemcpyAsync(sink.reserve(piece), R.text.p + at, piece, hipMemcpyDeviceToHost, cst));
+            char* dst = sink.reserve(piece);
+            void* ddst = nullptr;
+            if (push_blocks && ((uintptr_t)dst & 15u) == 0 && hipHostGetDevicePointer(&ddst, dst, 0) == hipSuccess && ddst) {
+              d2h_push(ddst, R.text.p + at, piece, cst, push_blocks);
+              HIPCHK(hipGetLastError());
+            } else {
+              (void)hipGetLastError();
+              HIPCHK(hipMemcpyAsync(dst, R.text.p + at, piece, hipMemcpyDeviceToHost, cst));
+            }
             HIPCHK(hipStreamSynchronize(cst));
             sink.commit(piece);
             at += piece; bytes -= piece; S.bytes += piece;

@@ -52,3 +52,51 @@ void device_segmented_order(const unsigned long long* key, uint32_t* order, uint
 }
 
 }  // namespace gg
+
+namespace gg {
+namespace {
+// Device-to-host copy by the shader (GG_D2H_PUSH=1): each thread reads 16 bytes of the device text (from a
+// 4-byte aligned base, funnel-shifted when the source is not 16-byte aligned) and writes them to the pinned
+// destination with one 16-byte nontemporal store; the last partial group is written byte by byte.  The
+// SDMA engine a copy queue lands on was measured at 27 to 57 GB/s from process to process
+// (profiles/r05zb_*); the shader path does not depend on it.
+__global__ void __launch_bounds__(256) d2h_push_kernel(const uint32_t* __restrict__ src_base, uint32_t shift_bits,
+                                                      const unsigned char* __restrict__ src, uint4* dst,
+                                                      size_t n16, size_t nbytes) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  const size_t nwords = (nbytes + (shift_bits >> 3) + 3) / 4;   // readable words from src_base
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) {
+    const size_t w = 4 * i;
+    uint32_t a[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) a[k] = (w + k < nwords) ? src_base[w + k] : 0u;
+    uint4 o;
+    if (shift_bits) {
+      o.x = __builtin_amdgcn_alignbit(a[1], a[0], shift_bits);
+      o.y = __builtin_amdgcn_alignbit(a[2], a[1], shift_bits);
+      o.z = __builtin_amdgcn_alignbit(a[3], a[2], shift_bits);
+      o.w = __builtin_amdgcn_alignbit(a[4], a[3], shift_bits);
+    } else {
+      o = make_uint4(a[0], a[1], a[2], a[3]);
+    }
+    __builtin_nontemporal_store(o.x, &dst[i].x);
+    __builtin_nontemporal_store(o.y, &dst[i].y);
+    __builtin_nontemporal_store(o.z, &dst[i].z);
+    __builtin_nontemporal_store(o.w, &dst[i].w);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    for (size_t b = n16 * 16; b < nbytes; b++) ((unsigned char*)dst)[b] = src[b];
+}
+}  // namespace
+
+// bytes from device `src` to pinned host `dst` (device-accessible), enqueued on `st`
+void d2h_push(void* dst, const void* src, size_t bytes, hipStream_t st, int blocks) {
+  if (!bytes) return;
+  const uintptr_t s = (uintptr_t)src;
+  const uint32_t* base = (const uint32_t*)(s & ~(uintptr_t)3);
+  const uint32_t shift_bits = (uint32_t)(s & 3) * 8;
+  const size_t n16 = bytes / 16;
+  hipLaunchKernelGGL(d2h_push_kernel, dim3(blocks), dim3(256), 0, st, base, shift_bits, (const unsigned char*)src,
+                     (uint4*)dst, n16, bytes);
+}
+}  // namespace gg
