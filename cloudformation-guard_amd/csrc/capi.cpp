@@ -285,6 +285,10 @@ struct DeviceBufs {
     DBuf<uint64_t> name_off, sizes, offs;
   } rset[2];
   hipStream_t copy_stream = nullptr;
+  // shader copy-out (d2h_push) with CU masks: the copy kernel on push_stream's CUs, the report's render
+  // kernels on render_stream's (the rest), so the two do not share a CU (GG_PUSH_CUS)
+  hipStream_t push_stream = nullptr, render_stream = nullptr;
+  int push_cus = -1;
   char* pinned = nullptr;       // host staging for report text (kPinnedBytes)
   static constexpr size_t kPinnedBytes = (size_t)256 << 20;
   DBuf<char> d_bytes;
@@ -318,6 +322,8 @@ struct DeviceBufs {
     hipSetDevice(device);
     if (pinned) pinned_free(pinned);
     if (copy_stream) hipStreamDestroy(copy_stream);
+    if (push_stream) hipStreamDestroy(push_stream);
+    if (render_stream) hipStreamDestroy(render_stream);
     for (auto& pr : evq) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
     if (stream) hipStreamDestroy(stream);
   }
@@ -362,7 +368,9 @@ DeviceBufs* acquire_bufs(int d) {
 void release_bufs(DeviceBufs* b) {
   if (!b) return;
   hipSetDevice(b->device);
-  if (hipStreamSynchronize(b->stream) == hipSuccess && (!b->copy_stream || hipStreamSynchronize(b->copy_stream) == hipSuccess)) {
+  if (hipStreamSynchronize(b->stream) == hipSuccess && (!b->copy_stream || hipStreamSynchronize(b->copy_stream) == hipSuccess) &&
+      (!b->push_stream || hipStreamSynchronize(b->push_stream) == hipSuccess) &&
+      (!b->render_stream || hipStreamSynchronize(b->render_stream) == hipSuccess)) {
     // a larger set (a batch job) keeps only its stream, events and pinned staging: its device buffers go
     // to the block cache, where the next batch's allocations find them (deleting the set would
     // hipHostFree the staging, which waits for the device to go idle)
@@ -1173,20 +1181,50 @@ void render_tables(gg_session* s) {
 // a copy thread moves each block to the sink in document order -- device runs by D2H, host-writer
 // documents between them -- while the device renders the next block.
 bool device_report_text(gg_session* s, size_t first, size_t count, size_t report_first, ReportSink& sink, ReportError& err,
-                        DevReportStats* stats, int32_t fmt) {
+                        DevReportStats* stats, int32_t fmt, int push_default = 0) {
   bind_device(s);
   render_tables(s);
   hipStream_t st = s->dv->stream;
   if (!s->dv->copy_stream) HIPCHK(hipStreamCreateWithFlags(&s->dv->copy_stream, hipStreamNonBlocking));
   hipStream_t cst = s->dv->copy_stream;
+  // GG_D2H_PUSH=<workgroups>: the copy-out by a shader kernel (d2h_push) instead of the copy engine; the
+  // streamed entries default to it (push_default): their copy engines were measured at 27 GB/s where the
+  // shader copy holds 50-54 (profiles/r05zc_report_ab_push*.log).  0 = the copy engine.
+  const int push_blocks = getenv("GG_D2H_PUSH") ? std::max(0, atoi(getenv("GG_D2H_PUSH"))) : push_default;
+  if (push_blocks) {
+    // GG_PUSH_CUS=<n>: the copy kernel confined to n CUs and the render kernels to the others
+    const int cus = getenv("GG_PUSH_CUS") ? std::max(0, atoi(getenv("GG_PUSH_CUS"))) : 0;
+    const int ncu = dev_ncu(s->device);
+    if (cus > 0 && cus < ncu) {
+      if (s->dv->push_cus != cus) {
+        if (s->dv->push_stream) { HIPCHK(hipStreamSynchronize(s->dv->push_stream)); HIPCHK(hipStreamDestroy(s->dv->push_stream)); }
+        if (s->dv->render_stream) { HIPCHK(hipStreamSynchronize(s->dv->render_stream)); HIPCHK(hipStreamDestroy(s->dv->render_stream)); }
+        std::vector<uint32_t> pm((ncu + 31) / 32, 0u), rm((ncu + 31) / 32, 0u);
+        // the copy CUs spread over the mask (every ncu / cus-th CU), the render kernels on the rest
+        const int step = ncu / cus;
+        for (int c = 0; c < ncu; c++) {
+          if (c % step == 0 && c / step < cus) pm[c / 32] |= 1u << (c % 32);
+          else rm[c / 32] |= 1u << (c % 32);
+        }
+        HIPCHK(hipExtStreamCreateWithCUMask(&s->dv->push_stream, (uint32_t)pm.size(), pm.data()));
+        HIPCHK(hipExtStreamCreateWithCUMask(&s->dv->render_stream, (uint32_t)rm.size(), rm.data()));
+        s->dv->push_cus = cus;
+      }
+      // the render stream starts after everything already queued on the session's buffer stream
+      hipEvent_t ready;
+      HIPCHK(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+      HIPCHK(hipEventRecord(ready, st));
+      HIPCHK(hipStreamWaitEvent(s->dv->render_stream, ready, 0));
+      HIPCHK(hipEventDestroy(ready));
+      st = s->dv->render_stream;
+      cst = s->dv->push_stream;
+    }
+  }
   const int dev = s->device;
   std::vector<const Program*> progs;
   for (auto& p : s->progs) progs.push_back(&p->prog);
   const size_t nf = progs.size();
   const size_t kBlock = getenv("GG_DREPORT_BLOCK") ? (size_t)std::max(1, atoi(getenv("GG_DREPORT_BLOCK"))) : 65536;
-  // GG_D2H_PUSH=<blocks>: the copy-out by a shader kernel of that many workgroups (d2h_push) instead of
-  // the copy engine
-  const int push_blocks = getenv("GG_D2H_PUSH") ? std::max(0, atoi(getenv("GG_D2H_PUSH"))) : 0;
   DevReportStats local;
   DevReportStats& S = stats ? *stats : local;
   // GG_DREPORT_TRACE=1: per-block wall-clock spans of the render and the copy-out on stderr (overlap check)
@@ -1388,9 +1426,11 @@ bool device_report_text(gg_session* s, size_t first, size_t count, size_t report
   return true;
 }
 
+// the streamed entries' shader copy-out (device_report_text push_default): workgroups of d2h_push
+static constexpr int kStreamPushBlocks = 32;
 bool device_report_json(gg_session* s, size_t first, size_t count, size_t report_first, ReportSink& sink, ReportError& err,
-                        DevReportStats* stats) {
-  return device_report_text(s, first, count, report_first, sink, err, stats, OUT_JSON);
+                        DevReportStats* stats, int push_default = 0) {
+  return device_report_text(s, first, count, report_first, sink, err, stats, OUT_JSON, push_default);
 }
 
 // One shard of a structured report: documents [first, first + count) of a fetched session.
@@ -2072,7 +2112,7 @@ int32_t stream_single(int dev, const validate_input_t* docs, size_t n_docs, cons
       if (k == 0) sink.write("[\n", 2);
       ReportError re;
       if (nf && device_report_on(s) && s->fetched_on_device) {
-        if (!device_report_json(s, 0, nd, k == 0 ? 0 : SIZE_MAX, sink, re, nullptr)) return fail(ffi_code(re.kind), error_display(re.kind, re.msg));
+        if (!device_report_json(s, 0, nd, k == 0 ? 0 : SIZE_MAX, sink, re, nullptr, kStreamPushBlocks)) return fail(ffi_code(re.kind), error_display(re.kind, re.msg));
       } else {
         // host writer for this chunk: its "[\n" ... "\n]" unwrapped, joined with ",\n"
         std::string out;
@@ -2145,7 +2185,7 @@ bool stream_chunk_report(gg_session* s, size_t k, ReportSink& sink, ReportError&
     if (s->tiles[t].status == ST_FAIL) anyfail = true;
   }
   if (nf && device_report_on(s) && s->fetched_on_device)
-    return device_report_json(s, 0, nd, k == 0 ? 0 : SIZE_MAX, sink, re, nullptr);
+    return device_report_json(s, 0, nd, k == 0 ? 0 : SIZE_MAX, sink, re, nullptr, kStreamPushBlocks);
   std::string out;
   char* cs = nullptr;
   int32_t code = 0;
