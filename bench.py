@@ -177,6 +177,18 @@ def generate_docs(workload, first, n, n_resources, procs):
     return [d for p in parts for d in p]
 
 
+def _stream_leg(workload, first, docs, resources, fmt, chunk, devices, threads):
+    """a streamed C-ABI leg in a child process (tools/stream_leg.py): the entry as a caller process uses it, with
+    none of this process's sessions, caches or copy queues; the child is started, not exec'd"""
+    import subprocess
+    cmd = [sys.executable, os.path.join(ROOT, "tools", "stream_leg.py"), workload, str(first), str(docs), str(resources),
+           fmt, str(chunk), str(devices), str(threads)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+    if r.returncode != 0:
+        raise RuntimeError("stream leg failed (%d): %s" % (r.returncode, r.stderr[-2000:]))
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
 def load_pmc(workload):
     """HBM bytes per launch of the dominant kernel from the newest profiles/pmc_r<NN>.json recorded for
     this exact workload (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes), else None"""
@@ -209,8 +221,6 @@ def main():
                     help="regex is_match memo: zeroed before every launch, or kept warm across launches")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--e2e-sarif", type=int, default=1, help="also time the e2e job with the SARIF report (device results)")
-    ap.add_argument("--stream-count", default="native", choices=["native", "py"],
-                    help="the streamed legs' write callback: the library's native byte counter, or a Python callback per piece")
     ap.add_argument("--e2e-stream", type=int, default=262144,
                     help="also time the streamed batch entry (cfn_guard_validate_batch_stream) over the same synthetic "
                          "texts with this many documents per chunk (0: off; cfg2/cfg3 at N=1 only)")
@@ -466,37 +476,34 @@ def main():
                                  "the device (results) and host (artifacts, frame), copied to host memory and discarded"}
 
     e2e_stream = None
+    leg = None
     if (rank == 0 and world == 1 and not args.no_e2e and args.e2e_stream and args.workload in ("cfg2", "cfg3")
             and args.loader == "device"):
         # the drop-in batch entry end to end: cfn_guard_validate_batch_stream over the same templates as
         # validate inputs, chunks of --e2e-stream documents on two alternating sessions (the next chunk's text
         # H2D, parse and evaluation overlap this chunk's device render and report D2H); the bytes reach host
         # memory (the library's pinned staging) and are counted
-        log("e2e stream: %d documents in chunks of %d" % (count, args.e2e_stream))
-        t0 = time.time()
-        st_texts = guard_amd.SynthTexts(first, count, n_resources=args.resources, fmt=args.format, threads=threads)
-        t_gen_s = time.time() - t0
-        nbytes = [0]
-
-        def _count(n):
-            nbytes[0] += n
+        log("e2e stream: %d documents in chunks of %d (a process of its own)" % (count, args.e2e_stream))
         try:
-            t0 = time.time()
-            _, st_code = guard_amd.validate_structured_stream(rules, None, write=_count, chunk_docs=args.e2e_stream,
-                                                              inputs=st_texts.inputs, n_docs=st_texts.n,
-                                                              count_only=args.stream_count)
-            t_stream = time.time() - t0
-        finally:
-            st_texts.close()
+            leg = _stream_leg(args.workload, first, count, args.resources, args.format, args.e2e_stream, 0, threads)
+        except Exception as e:   # the leg is reported as failed; the line still prints
+            leg = {"error": str(e)[-500:]}
+    if e2e_stream is None and leg is not None and "error" in leg:
+        e2e_stream = {"value": None, "error": leg["error"]}
+    elif leg is not None:
+        t_stream, t_gen_s, st_code = leg["seconds"], leg["gen_s"], leg["exit_code"]
+        nbytes = [leg["report_bytes"]]
         e2e_stream = {"value": round(ntiles / t_stream, 1), "unit": "evals/s", "seconds": round(t_stream, 3),
                       "chunk_docs": args.e2e_stream, "report_bytes": nbytes[0],
                       "report_GBps": round(nbytes[0] / t_stream / 1e9, 3), "exit_code": st_code,
                       "gen_s": round(t_gen_s, 3),
-                      "note": "cfn_guard_validate_batch_stream (the C ABI batch entry, JSON) over the same synthetic "
-                              "texts resident in host memory: load + upload + evaluation + fetch + device-rendered "
-                              "report to host memory, chunked and overlapped; text generation (gen_s) not included"}
+                      "note": "cfn_guard_validate_batch_stream (the C ABI batch entry, JSON) in a process of its own over "
+                              "the same synthetic texts resident in host memory: load + upload + evaluation + fetch + "
+                              "device-rendered report to host memory (shader copy-out), chunked and overlapped, counted "
+                              "by the library's native callback; text generation (gen_s) not included"}
 
     e2e_devices = None
+    leg = None
     if (rank == 0 and not args.no_e2e and args.e2e_devices_docs and args.workload in ("cfg2", "cfg3")
             and args.loader == "device" and torch.cuda.device_count() >= world):
         # the in-library multi-GPU path (SURVEY.md 8(b) n_gpus): one process (rank 0, after the ranks' timed
@@ -507,26 +514,20 @@ def main():
         nd = args.e2e_devices_docs * ndev
         dchunk = args.e2e_devices_chunk if ndev > 1 else args.e2e_stream
         log("e2e devices: %d documents over %d device(s), chunks of %d" % (nd, ndev, dchunk))
-        t0 = time.time()
-        dv_texts = guard_amd.SynthTexts(first, nd, n_resources=args.resources, fmt=args.format, threads=threads)
-        t_gen_d = time.time() - t0
-        nb = [0]
-
-        def _count_d(n):
-            nb[0] += n
         try:
-            t0 = time.time()
-            _, dv_code = guard_amd.validate_structured_stream(rules, None, write=_count_d, chunk_docs=dchunk,
-                                                              inputs=dv_texts.inputs, n_docs=dv_texts.n, count_only="native",
-                                                              devices=list(range(ndev)))
-            t_dv = time.time() - t0
-        finally:
-            dv_texts.close()
+            leg = _stream_leg(args.workload, first, nd, args.resources, args.format, dchunk, ndev, threads)
+        except Exception as e:
+            leg = {"error": str(e)[-500:]}
+    if leg is not None and "error" in leg:
+        e2e_devices = {"value": None, "devices": ndev, "error": leg["error"]}
+    elif leg is not None:
+        t_dv, t_gen_d, dv_code = leg["seconds"], leg["gen_s"], leg["exit_code"]
+        nb = [leg["report_bytes"]]
         e2e_devices = {"value": round(nd * nfiles / t_dv, 1), "unit": "evals/s", "devices": ndev, "docs": nd,
                        "docs_per_device": args.e2e_devices_docs, "chunk_docs": dchunk,
                        "seconds": round(t_dv, 3), "report_bytes": nb[0], "report_GBps": round(nb[0] / t_dv / 1e9, 3),
                        "exit_code": dv_code, "gen_s": round(t_gen_d, 3),
-                       "note": "cfn_guard_validate_batch_stream_devices over devices 0..N-1 from one process (rank 0) "
+                       "note": "cfn_guard_validate_batch_stream_devices over devices 0..N-1 from one child process of rank 0 "
                                "(load + upload + evaluation + fetch + device-rendered JSON report to host memory, in "
                                "document order); text generation (gen_s) not included"}
 
