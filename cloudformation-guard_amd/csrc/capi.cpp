@@ -414,6 +414,7 @@ struct gg_session {
   uint32_t max_top = 1;
   uint32_t nslots = 0;            // wave-mode grid
   uint32_t lane_slots = 0;        // lane-mode grid (waves)
+  uint32_t lane_docs = 64;        // lane mode: documents per batch (session_upload)
   uint32_t heap_bytes = 512 * 1024;
   static constexpr uint32_t kWaveFrames = 16 * 1024, kWaveRecs = 64 * 1024;
   // large-heap pass (rare: documents with thousands of failing clause values or deep nesting)
@@ -732,7 +733,15 @@ void session_upload(gg_session* s) {
     if (w <= gg_session::kMaxLdsProgWords) s->lds_prog_words = std::max(s->lds_prog_words, (w + 3u) & ~3u);
   }
   size_t ntiles = s->docs.ndocs() * s->progs.size();
-  size_t nbatches = (s->docs.ndocs() + 63) / 64 * s->progs.size();
+  const bool large_docs = s->docs.ndocs() && arena_nodes(s) / s->docs.ndocs() > 4096;
+  // Documents per lane batch: 64 (a wave's lanes), or 16 for a launch of few large documents (cfg4: 8192
+  // Terraform plans of ~60 K nodes fill 256 waves, one per CU, each walking 64 plans whose list lengths and
+  // filter outcomes differ from lane to lane -- the wave runs the union of their paths).  16 documents per
+  // wave quarter the divergence and give each CU four waves.  GG_LANE_DOCS overrides (A/B).
+  s->lane_docs = 64;
+  if (large_docs && (s->docs.ndocs() + 63) / 64 * s->progs.size() < (size_t)dev_ncu(s->device) * 4) s->lane_docs = 16;
+  if (const char* e = getenv("GG_LANE_DOCS")) s->lane_docs = (uint32_t)std::min(64, std::max(1, atoi(e)));
+  size_t nbatches = (s->docs.ndocs() + s->lane_docs - 1) / s->lane_docs * s->progs.size();
   // wave mode: all tiles (mode 1) or only the lane kernel's overflow tiles (mode 0)
   size_t wave_slots = s->mode == 1 ? (size_t)dev_ncu(s->device) * 8 : (size_t)dev_ncu(s->device) * 2;
   uint32_t slots = (uint32_t)std::min<size_t>(std::max<size_t>(ntiles, 1), wave_slots);
@@ -748,10 +757,9 @@ void session_upload(gg_session* s) {
   // budget unused while their tiles outgrow 64 KB (hundreds of records, long QR lists) and fall back to
   // the wave kernel one tile per wave: such launches get 256 KB lane heaps with 96 KB of record staging
   // while the heaps stay within kLaneHeapBudget
-  static constexpr size_t kLaneHeapBudget = (size_t)8 << 30;
+  static constexpr size_t kLaneHeapBudget = (size_t)24 << 30;
   s->lane_heap_bytes = s->lane_heap_set ? s->lane_heap_set : 64u * 1024u;
   s->lane_recs_bytes = 24576;
-  const bool large_docs = s->docs.ndocs() && arena_nodes(s) / s->docs.ndocs() > 4096;
   if (!s->lane_heap_set && large_docs && s->lane_slots && (size_t)s->lane_slots * 64 * (256u << 10) <= kLaneHeapBudget) {
     s->lane_heap_bytes = 256u << 10;
     s->lane_recs_bytes = 2048u * (uint32_t)sizeof(Rec);
@@ -824,6 +832,7 @@ void session_launch(gg_session* s) {
   A.retry_count = s->dv->d_counters.p + 3;
   A.xcd_cursor = s->dv->d_counters.p + 16;
   A.lane_heaps = s->dv->d_lane_heaps.p; A.lane_heap_bytes = s->lane_heap_bytes; A.lane_recs_bytes = s->lane_recs_bytes;
+  A.lane_docs = s->lane_docs;
   A.retry_list = s->mode == 1 ? nullptr : s->dv->d_retry.p;
   A.wave_frames_bytes = gg_session::kWaveFrames; A.wave_recs_bytes = gg_session::kWaveRecs;
   A.retry2_list = s->dv->d_retry2.p; A.retry2_count = s->dv->d_counters.p + 4;

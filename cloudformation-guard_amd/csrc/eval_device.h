@@ -94,6 +94,7 @@ struct LaunchArgs {
   uint32_t lds_prog_words;    // program staging window (dynamic LDS, words; multiple of 4)
   uint32_t rec_chunk;         // lane mode: record slots per lane reserved per batch (direct writes; 0: off)
   uint32_t lane_recs_bytes;   // lane mode: record staging bytes per lane (a multiple of 48; after the 4 KB frames)
+  uint32_t lane_docs;         // lane mode: documents per batch (lanes 0 .. lane_docs-1 of a wave; 64 or fewer)
   unsigned long long* stats;   // stats build variant: [0,8) counters, [8] tiles, [9,18) cycles per category
 };
 

@@ -154,7 +154,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
   // on XCD b % 8.  Each XCD owns a contiguous eighth of the 64-document chunks and hands out its
   // batches chunk-major, file-minor: the rules files of one chunk run back to back on the same
   // XCD, so the chunk's arena lines fetched by the first file are L2 hits for the others.
-  const uint32_t nchunks = (A.docs.ndocs + 63u) / 64u;
+  // a batch is lane_docs consecutive documents (64, or fewer for launches of few large documents: fewer
+  // lanes of a wave diverge, and more waves share the CUs)
+  const uint32_t L = A.lane_docs ? A.lane_docs : 64u;
+  const uint32_t nchunks = (A.docs.ndocs + L - 1u) / L;
   const uint32_t xcd = blockIdx.x & 7u;
   const uint32_t c0 = (uint32_t)(((uint64_t)nchunks * xcd) / 8u), c1 = (uint32_t)(((uint64_t)nchunks * (xcd + 1u)) / 8u);
   const uint32_t nbatches = (c1 - c0) * A.nfiles;
@@ -191,8 +194,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
     if (b >= nbatches) break;
     const uint32_t file = b % A.nfiles, chunk = c0 + b / A.nfiles;
 #endif
-    const uint32_t pos = chunk * 64u + lane;
-    const bool active = pos < A.docs.ndocs;
+    const uint32_t pos = chunk * L + lane;
+    const bool active = lane < L && pos < A.docs.ndocs;
     const uint32_t doc = (A.order && active) ? A.order[pos] : pos;
     if (file != staged) { P = stage_program(&A.progs[file], &g_prog, s_blob, A.lds_prog_words); staged = file; }
     const uint32_t tile = doc * A.nfiles + file;
