@@ -32,11 +32,14 @@ corpus = None
 if PACK == "cfg5":
     import synth  # noqa: E402
     corpus = synth.config_corpus(ndocs, start=0)
+elif PACK == "cfg4":
+    import synth  # noqa: E402
+    corpus = synth.tf_bench_corpus(ndocs, start=0)
 for name, text in FILES:
     s = guard_amd.Session()
     s.add_rules(text, name)
     if corpus is not None:
-        s.add_docs(corpus, ["snapshot-%d.json" % i for i in range(ndocs)], threads=16)
+        s.add_docs(corpus, ["%s-%d.json" % ("plan" if PACK == "cfg4" else "snapshot", i) for i in range(ndocs)], threads=16)
     else:
         s.add_synthetic(0, ndocs, threads=16)
     s.upload()
