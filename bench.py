@@ -475,6 +475,17 @@ def main():
                          "note": "e2e with -o sarif: load, upload and evaluation as e2e, the SARIF report rendered on "
                                  "the device (results) and host (artifacts, frame), copied to host memory and discarded"}
 
+    # the session's counters for the line, then its device memory back (the streamed legs run in a child
+    # process next to this one: they get the device this process no longer needs)
+    sess_stats = {"nodes": sess.stat(2), "pool_bytes": sess.stat(3), "retried": sess.stat(16), "mode": sess.stat(20)}
+    sess.close()
+    sess = None
+    if rank == 0:
+        guard_amd.release_device_cache(-1)
+        counts = None
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+
     e2e_stream = None
     leg = None
     if (rank == 0 and world == 1 and not args.no_e2e and args.e2e_stream and args.workload in ("cfg2", "cfg3")
@@ -565,13 +576,13 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic},
             "detail": {"kernel_ms_mean": round(k_mean_ms, 3), "kernel_ms": [round(x, 3) for x in kms],
                        "alg_bytes_per_launch": b_alg, "arena_bytes": arena, "record_bytes": rec_bytes,
-                       "nodes": sess.stat(2), "pool_bytes": sess.stat(3),
+                       "nodes": sess_stats["nodes"], "pool_bytes": sess_stats["pool_bytes"],
                        "tiles_fail_pass_skip_err": [n_fail, n_pass, n_skip, n_err],
                        "loader": args.loader, "load_s": round(t_load, 2), "host_threads": threads,
                        "upload_s": round(t_upload, 2), "device_loader": load_stats,
                        "rule_tallies_sum": tally_sum, "rule_tallies_fetched": int(sum(tally)),
-                       "lane_tiles_retried_in_wave_mode": sess.stat(16),
-                       "kernel_mode": sess.stat(20), "regex_memo": args.rx_memo,
+                       "lane_tiles_retried_in_wave_mode": sess_stats["retried"],
+                       "kernel_mode": sess_stats["mode"], "regex_memo": args.rx_memo,
                        "host": host_info()},
         }
         line["cpu_baseline"] = cpu
@@ -585,7 +596,6 @@ def main():
         if gather is not None:
             line["report_gather"] = gather
         print(json.dumps(line), flush=True)
-    sess.close()
     if dist is not None:
         dist.destroy_process_group()
 
