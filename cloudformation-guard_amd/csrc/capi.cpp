@@ -2081,10 +2081,61 @@ int32_t stream_single(int dev, const validate_input_t* docs, size_t n_docs, cons
       std::thread& t; std::mutex& mu; std::condition_variable& cv; bool& stop;
       ~Join() { { std::lock_guard<std::mutex> lk(mu); stop = true; } cv.notify_all(); if (t.joinable()) t.join(); }
     } join{producer, mu, cv, stop};
-    // a reported chunk's session is torn down on a thread of its own (its host columns and index take
-    // tens of ms to free), so the next chunk's report starts at once
-    std::vector<std::thread> reapers;
-    struct JoinAll { std::vector<std::thread>& v; ~JoinAll() { for (auto& t : v) if (t.joinable()) t.join(); } } join_reapers{reapers};
+    // Chunk k's report runs on a thread of its own, so chunk k + 1's report renders its first blocks on the
+    // device while chunk k's last blocks copy out (within one chunk the render of the first block and the copy of
+    // the last one ran alone).  The bytes stay in document order: a report's sink waits for its turn before it
+    // takes the staging (OrderedSink), and the turn passes when the previous chunk's report has returned.  The
+    // report thread then frees the chunk's slot for the producer and tears the session down.
+    struct Turn {
+      std::mutex m;
+      std::condition_variable cv;
+      size_t turn = 0;
+      bool abort = false;
+    } turn;
+    struct OrderedSink : ReportSink {
+      ReportSink& in;
+      Turn& t;
+      size_t k;
+      bool mine = false;
+      OrderedSink(ReportSink& s, Turn& tt, size_t kk) : in(s), t(tt), k(kk) {}
+      char* reserve(size_t n) override {
+        if (!mine) {
+          std::unique_lock<std::mutex> lk(t.m);
+          t.cv.wait(lk, [&] { return t.turn == k || t.abort; });
+          if (t.abort) throw std::runtime_error("stream aborted");
+          mine = true;
+        }
+        return in.reserve(n);
+      }
+      void commit(size_t n) override { in.commit(n); }
+      size_t max_piece() const override { return in.max_piece(); }
+    };
+    struct ChunkReport {
+      std::thread th;
+      bool ok = true;
+      ReportError re;
+      std::string internal;
+    };
+    std::vector<std::unique_ptr<ChunkReport>> reps(nchunks);
+    struct JoinReports {
+      std::vector<std::unique_ptr<ChunkReport>>& v; Turn& t;
+      ~JoinReports() {
+        { std::lock_guard<std::mutex> lk(t.m); t.abort = true; }
+        t.cv.notify_all();
+        for (auto& r : v) if (r && r->th.joinable()) r->th.join();
+      }
+    } join_reports{reps, turn};
+    // the first failed chunk report in document order (joining every report before it), or -1
+    auto first_failure = [&](size_t upto) -> int32_t {
+      for (size_t j = 0; j < upto; j++) {
+        if (!reps[j]) continue;
+        if (reps[j]->th.joinable()) reps[j]->th.join();
+        if (!reps[j]->internal.empty()) return fail(-1, reps[j]->internal);
+        if (!reps[j]->ok) return fail(ffi_code(reps[j]->re.kind), error_display(reps[j]->re.kind, reps[j]->re.msg));
+      }
+      if (sink.failed) return fail(-1, "the write callback failed");
+      return 0;
+    };
     bool anyfail = false;
     if (!n_docs) {
       // no documents: "[]", exit 5 when a rules file does not parse (as the one-string call)
@@ -2103,12 +2154,16 @@ int32_t stream_single(int dev, const validate_input_t* docs, size_t n_docs, cons
         cv.wait(lk, [&] { return sl.state != 0 && sl.k == k; });
       }
       mark("report start", k);
-      if (sl.state == 2) return fail(ffi_code(sl.kind), error_display(sl.kind, sl.msg));
+      if (sl.state == 2) {
+        if (first_failure(k)) return -1;
+        return fail(ffi_code(sl.kind), error_display(sl.kind, sl.msg));
+      }
       gg_session* s = sl.s.get();
       if (k == 0) parse_code = s->parse_errors.empty() ? 0 : 5;
       const size_t nf = s->progs.size(), nd = s->docs.ndocs();
       for (size_t t = 0; t < nd * nf; t++) {
         if (s->tiles[t].err) {
+          if (first_failure(k)) return -1;
           ensure_host_arena(s);
           std::vector<const Program*> progs;
           for (auto& p : s->progs) progs.push_back(&p->prog);
@@ -2119,36 +2174,54 @@ int32_t stream_single(int dev, const validate_input_t* docs, size_t n_docs, cons
         if (s->tiles[t].status == ST_FAIL) anyfail = true;
       }
       if (k == 0) sink.write("[\n", 2);
-      ReportError re;
-      if (nf && device_report_on(s) && s->fetched_on_device) {
-        if (!device_report_json(s, 0, nd, k == 0 ? 0 : SIZE_MAX, sink, re, nullptr, kStreamPushBlocks)) return fail(ffi_code(re.kind), error_display(re.kind, re.msg));
-      } else {
-        // host writer for this chunk: its "[\n" ... "\n]" unwrapped, joined with ",\n"
-        std::string out;
-        char* cs = nullptr;
-        int32_t code = 0;
-        if (!session_report(s, out, code, re, OUT_JSON, &cs)) return fail(ffi_code(re.kind), error_display(re.kind, re.msg));
-        std::string text = cs ? std::string(cs) : out;
-        if (cs) free(cs);
-        if (text.size() >= 4 && text.compare(0, 2, "[\n") == 0) {
-          if (k) sink.write(",\n", 2);
-          sink.write(text.data() + 2, text.size() - 4);
+      reps[k].reset(new ChunkReport());
+      ChunkReport* cr = reps[k].get();
+      cr->th = std::thread([&, k, s, cr, nf, nd]() {
+        OrderedSink osink(sink, turn, k);
+        try {
+          HIPCHK(hipSetDevice(dev));
+          if (nf && device_report_on(s) && s->fetched_on_device) {
+            cr->ok = device_report_json(s, 0, nd, k == 0 ? 0 : SIZE_MAX, osink, cr->re, nullptr, kStreamPushBlocks);
+          } else {
+            // host writer for this chunk: its "[\n" ... "\n]" unwrapped, joined with ",\n"
+            std::string out;
+            char* cs = nullptr;
+            int32_t code = 0;
+            cr->ok = session_report(s, out, code, cr->re, OUT_JSON, &cs);
+            if (cr->ok) {
+              std::string text = cs ? std::string(cs) : out;
+              if (text.size() >= 4 && text.compare(0, 2, "[\n") == 0) {
+                if (k) osink.write(",\n", 2);
+                osink.write(text.data() + 2, text.size() - 4);
+              }
+            }
+            if (cs) free(cs);
+          }
+        } catch (std::exception& e) {
+          cr->internal = e.what();
         }
-      }
-      if (sink.failed) return fail(-1, "the write callback failed");
-      mark("reported", k);
-      std::unique_ptr<gg_session> done;
-      {
-        std::lock_guard<std::mutex> lk(mu);
-        done = std::move(sl.s);
-        sl.state = 0;
-        sl.k = SIZE_MAX;
-        reported = k + 1;
-      }
-      cv.notify_all();
-      reapers.emplace_back([&mark, k](gg_session* p) { delete p; mark("torn down", k); }, done.release());
-      if (k + 1 == nchunks) sink.write("\n]", 2);
+        mark("reported", k);
+        {
+          std::lock_guard<std::mutex> lk(turn.m);
+          if (cr->ok && cr->internal.empty()) turn.turn = k + 1;
+          else turn.abort = true;   // the chunks after a failed one are not written
+        }
+        turn.cv.notify_all();
+        std::unique_ptr<gg_session> done;
+        {
+          std::lock_guard<std::mutex> lk(mu);
+          done = std::move(slot[k & 1].s);
+          slot[k & 1].state = 0;
+          slot[k & 1].k = SIZE_MAX;
+          reported = k + 1;
+        }
+        cv.notify_all();
+        done.reset();
+        mark("torn down", k);
+      });
     }
+    if (first_failure(nchunks)) return -1;
+    if (nchunks) sink.write("\n]", 2);
     if (sink.failed) return fail(-1, "the write callback failed");
     if (exit_code) *exit_code = anyfail ? 19 : parse_code;
     return 0;
