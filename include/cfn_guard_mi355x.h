@@ -85,8 +85,8 @@ char *cfn_guard_validate_batch_devices(const validate_input_t *docs, size_t n_do
  * evaluates while this one's report renders on the device), and the report's bytes go to write(ctx, data,
  * len) in order (a nonzero return aborts).  Returns 0 with *exit_code as the one-string call's, or -1 with
  * err on an abort -- after the chunks before the failing one were written (the caller drops that prefix).
- * Threads: `write` is called from the calling thread or from a thread the library owns (the device
- * reporter's copy thread), never two calls at once, always in document order, and never after this
+ * Threads: `write` is called from the calling thread or from threads the library owns (a chunk's report
+ * thread or its copy thread), never two calls at once, always in document order, and never after this
  * function has returned. */
 typedef int32_t (*cfn_guard_write_fn)(void *ctx, const char *data, size_t len);
 int32_t cfn_guard_validate_batch_stream(const validate_input_t *docs, size_t n_docs, const validate_input_t *rules,
