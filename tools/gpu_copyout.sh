@@ -3,6 +3,7 @@
 # (each step under its own time limit; the first failure ends the call).  Outputs under gpurun_out/$TAG.
 #   stream      tools/stream_probe.py on 1M cfg2 texts: native vs Python callback, chunked vs one chunk,
 #               shader copy-out vs copy engine (GG_D2H_PUSH=0), CU-masked variants (GG_PUSH_CUS)
+#   blocks      the streamed entry with 64 K / 128 K / 32 K documents per report block (render occupancy)
 #   report_ab   tools/report_ab.py (session vs streamed report in one process) under $VARIANTS, each an
 #               env assignment or "default" (e.g. VARIANTS="default GG_D2H_PUSH=32 GPU_MAX_HW_QUEUES=16")
 #   rate        tools/report_rate.py: repeated reports of one session, idle pauses, copy engine vs blit
@@ -27,6 +28,8 @@ case $mode in
     probe native_1chunk "1000000 1000000 native" GG_STREAM_TRACE=1
     probe sdma "1000000 262144 native" GG_D2H_PUSH=0
     for c in 16 32; do probe cus$c "1000000 262144 native" GG_PUSH_CUS=$c; done;;
+  blocks)
+    for b in 65536 131072 32768; do probe block$b "1000000 262144 native" GG_DREPORT_BLOCK=$b; done;;
   report_ab)
     for v in ${VARIANTS:-default}; do
       e=$v; [ "$v" = default ] && e=GG_NONE=0
@@ -62,6 +65,6 @@ case $mode in
     GG_LIB=$R/cloudformation-guard_amd/libcfnguard_mi355x_stats.so PACK=cfg4 timeout -k 10 300 python -u tools/kernel_stats.py 2048 \
       > $O/kernel_stats_cfg4.json 2> $O/kernel_stats_cfg4.err || { tail -20 $O/kernel_stats_cfg4.err; exit 1; }
     head -c 1500 $O/kernel_stats_cfg4.json;;
-  *) echo "usage: gpu_copyout.sh stream|report_ab|rate|frag|numa|push_tests|cfg4_batch|stats_cfg4"; exit 2;;
+  *) echo "usage: gpu_copyout.sh stream|blocks|report_ab|rate|frag|numa|push_tests|cfg4_batch|stats_cfg4"; exit 2;;
 esac
 echo "[copyout] $(date +%T) done"
