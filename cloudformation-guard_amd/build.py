@@ -142,11 +142,15 @@ def build(verbose=False, variant=""):
         # also pull conda's older libstdc++ in front of the one libamdhip64 needs.  Built artefact,
         # not tracked (.gitignore), shipped to the GPU box with the tree.
         shutil.copyfile(os.path.join(YAML_LIB, "libyaml-0.so.2"), local_yaml)
+        # linked beside the library and renamed over it: a reader (a test run, a snapshot of the tree) never
+        # sees a half-written library
+        tmp = out + ".tmp"
         cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC"] + objs + [
-            "-o", out, local_yaml, "-Wl,-rpath,$ORIGIN", "-lpthread"]
+            "-o", tmp, local_yaml, "-Wl,-rpath,$ORIGIN", "-lpthread"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError("link failed:\n" + r.stderr[-4000:])
+        os.replace(tmp, out)
     return out
 
 

@@ -1189,6 +1189,8 @@ void render_tables(gg_session* s) {
 // Per block of documents (two block sets in flight): the size pass, then the write pass at the offsets;
 // a copy thread moves each block to the sink in document order -- device runs by D2H, host-writer
 // documents between them -- while the device renders the next block.
+// the streamed entries' shader copy-out (device_report_text push_default): workgroups of d2h_push
+static constexpr int kStreamPushBlocks = 32;
 bool device_report_text(gg_session* s, size_t first, size_t count, size_t report_first, ReportSink& sink, ReportError& err,
                         DevReportStats* stats, int32_t fmt, int push_default = 0) {
   bind_device(s);
@@ -1257,6 +1259,11 @@ bool device_report_text(gg_session* s, size_t first, size_t count, size_t report
   ReportError cerr;
   std::exception_ptr cex;
   std::thread copier([&]() {
+    // GG_D2H_ADAPT=0: no switch from a slow copy engine to the shader copy (A/B)
+    int use_push = push_blocks;
+    const bool adapt = !push_blocks && !(getenv("GG_D2H_ADAPT") && atoi(getenv("GG_D2H_ADAPT")) == 0);
+    uint64_t engine_bytes = 0;
+    double engine_ms = 0;
     try {
       HIPCHK(hipSetDevice(dev));
       for (;;) {
@@ -1313,14 +1320,24 @@ bool device_report_text(gg_session* s, size_t first, size_t count, size_t report
             const size_t piece = (size_t)std::min<uint64_t>(bytes, sink.max_piece());
             char* dst = sink.reserve(piece);
             void* ddst = nullptr;
-            if (push_blocks && ((uintptr_t)dst & 15u) == 0 && hipHostGetDevicePointer(&ddst, dst, 0) == hipSuccess && ddst) {
-              d2h_push(ddst, R.text.p + at, piece, cst, push_blocks);
+            const auto p0 = std::chrono::steady_clock::now();
+            bool engine = false;
+            if (use_push && ((uintptr_t)dst & 15u) == 0 && hipHostGetDevicePointer(&ddst, dst, 0) == hipSuccess && ddst) {
+              d2h_push(ddst, R.text.p + at, piece, cst, use_push);
               HIPCHK(hipGetLastError());
             } else {
               (void)hipGetLastError();
               HIPCHK(hipMemcpyAsync(dst, R.text.p + at, piece, hipMemcpyDeviceToHost, cst));
+              engine = true;
             }
             HIPCHK(hipStreamSynchronize(cst));
+            if (engine && adapt) {
+              // the copy engine's rate over the report's first GB decides: a slow queue (27 GB/s against
+              // 53, profiles/r05x_report_ab.log) hands the rest of the report to the shader copy
+              engine_bytes += piece;
+              engine_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - p0).count();
+              if (engine_bytes >= (1ull << 30) && engine_bytes / std::max(engine_ms, 1e-3) < 35e6) use_push = kStreamPushBlocks;
+            }
             sink.commit(piece);
             at += piece; bytes -= piece; S.bytes += piece;
           }
@@ -1435,8 +1452,6 @@ bool device_report_text(gg_session* s, size_t first, size_t count, size_t report
   return true;
 }
 
-// the streamed entries' shader copy-out (device_report_text push_default): workgroups of d2h_push
-static constexpr int kStreamPushBlocks = 32;
 bool device_report_json(gg_session* s, size_t first, size_t count, size_t report_first, ReportSink& sink, ReportError& err,
                         DevReportStats* stats, int push_default = 0) {
   return device_report_text(s, first, count, report_first, sink, err, stats, OUT_JSON, push_default);
