@@ -2168,6 +2168,16 @@ int32_t stream_single(int dev, const validate_input_t* docs, size_t n_docs, cons
         std::unique_lock<std::mutex> lk(mu);
         cv.wait(lk, [&] { return sl.state != 0 && sl.k == k; });
       }
+      // chunk k's slot was freed by chunk k - 2's report at its end: that thread is done; join it now (at most
+      // three report threads exist at a time, however many chunks) and keep only a failed one's result
+      if (k >= 2 && reps[k - 2]) {
+        if (reps[k - 2]->th.joinable()) reps[k - 2]->th.join();
+        if (!reps[k - 2]->ok || !reps[k - 2]->internal.empty()) {
+          if (first_failure(k - 1)) return -1;
+        } else {
+          reps[k - 2].reset();
+        }
+      }
       mark("report start", k);
       if (sl.state == 2) {
         if (first_failure(k)) return -1;
