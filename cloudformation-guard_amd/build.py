@@ -3,9 +3,7 @@
 The library holds the host loader/compiler/reporter (C++) and the HIP evaluation kernel; it
 links libyaml 0.2.5 (the reference's YAML engine, via unsafe-libyaml) from /opt/conda/lib.
 
-Variants: "" = the product library (the recursive evaluator, eval_recursive.inc); "machine" = the same
-library with the evaluator over an explicit continuation stack (eval_machine.inc, GG_MACHINE=1:
-libcfnguard_mi355x_machine.so, loaded when GG_LIB points at it); "stats" = diagnostic build with evaluator counters
+Variants: "" = the product library; "stats" = diagnostic build with evaluator counters
 (libcfnguard_mi355x_stats.so, loaded only when GG_LIB points at it); "ab" = an A/B build of the
 product sources with extra compile flags from $GG_AB_FLAGS (libcfnguard_mi355x_ab.so).  Every
 object records the exact command that produced it (<obj>.cmd), so a flag change rebuilds it.
@@ -89,10 +87,6 @@ def build(verbose=False, variant=""):
     flags = list(FLAGS)
     if variant == "stats":
         flags.append("-DGG_STATS")
-    elif variant == "machine":
-        # the evaluator over an explicit continuation stack (eval_machine.inc): no recursion, static kernel
-        # stack; interprocedural register allocation is safe without recursion and measured best for it
-        flags.append("-DGG_MACHINE=1")
     elif variant.startswith("ab"):
         pass   # GG_AB_FLAGS go to the evaluator units only (below): an A/B rebuild compiles two files
     elif variant:
@@ -101,9 +95,7 @@ def build(verbose=False, variant=""):
     # the units a variant changes (the rest are the product build's objects, shared: the device report
     # alone compiles for ~8 minutes); stats touches every kernel's counters, so it rebuilds everything
     own = None
-    if variant == "machine":
-        own = {"eval_kernel.hip", "eval_kernel_nfa.hip", "capi.cpp"}   # capi.cpp: the stack-limit policy
-    elif variant.startswith("ab"):
+    if variant.startswith("ab"):
         own = {"eval_kernel.hip", "eval_kernel_nfa.hip"}
     jobs = []
     objs = []
@@ -115,8 +107,6 @@ def build(verbose=False, variant=""):
         else:
             obj = _obj(obj_dir, s)
             extra = shlex.split(os.environ.get("GG_AB_FLAGS", "")) if variant.startswith("ab") and s.startswith("eval_kernel") else []
-            if variant == "machine" and s.startswith("eval_kernel"):
-                extra = ["-mllvm", "-enable-ipra=true"]
             cmd = [HIPCC, "--offload-arch=gfx950"] + flags + SRC_FLAGS.get(s, []) + extra + ["-c", src, "-o", obj]
         objs.append(obj)
         if _needs(src, obj, sorted(_includes(src)), cmd):

@@ -108,9 +108,16 @@ static constexpr int kMaxDevices = 64;
 static size_t default_stack_bytes() {
   return getenv("GG_STACK_BYTES") ? (size_t)atol(getenv("GG_STACK_BYTES")) : (size_t)16384;
 }
+// The evaluator checks its lane stack pointer where it recurses (eval_core.inc stack_low); between two
+// checks a call chain can grow the stack by at most this much.  tools/stack_budget.py derives the bound from
+// the product ISA (per-function frames and call edges; round 6: 1056 B, the wave kernel's eval_conj ->
+// parameterized rule -> eval_rule -> eval_conj chain, 1104 B in the NFA variant) and checks that this margin
+// covers it.
+static constexpr size_t kStackMargin = 3072;
 struct DeviceState {
   bool ready = false;
   int ncu = 256;
+  uint32_t stack_guard = 16384 - (uint32_t)kStackMargin;
 };
 struct Devices {
   std::mutex mu;
@@ -131,17 +138,14 @@ struct Devices {
     if (hipSetDevice(d) != hipSuccess) { why = "hipSetDevice failed"; return false; }
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, d) == hipSuccess) D.ncu = prop.multiProcessorCount;
-#if GG_MACHINE
-    // the machine evaluator does not recurse (eval_machine.inc: an explicit continuation stack in the lane
-    // heap): every kernel's private segment is static (~0.6 KB per lane) and the runtime sizes scratch from
-    // it, so the device-wide stack limit is left at its default (GG_STACK_BYTES sets one, diagnostics only)
-    if (getenv("GG_STACK_BYTES")) hipDeviceSetLimit(hipLimitStackSize, default_stack_bytes());
-#else
     // the recursive evaluator (eval_recursive.inc: eval_conj <-> clauses, filters, rule references) needs a
     // dynamic lane stack: 16 KB for every kernel variant, the NFA one included (its simulation is a leaf
-    // call, eval_core.inc nfa_match_*), set once and never raised; GG_STACK_BYTES overrides
+    // call, eval_core.inc nfa_match_*), set once and never raised; GG_STACK_BYTES overrides.  The kernels'
+    // stack guard is what the runtime actually granted minus kStackMargin.
     hipDeviceSetLimit(hipLimitStackSize, default_stack_bytes());
-#endif
+    size_t granted = 0;
+    if (hipDeviceGetLimit(&granted, hipLimitStackSize) != hipSuccess || !granted) granted = default_stack_bytes();
+    D.stack_guard = granted > kStackMargin + 1024 ? (uint32_t)(granted - kStackMargin) : 1024u;
     D.ready = true;
     return true;
   }
@@ -157,6 +161,7 @@ struct Devices {
 };
 Devices g_devs;
 int dev_ncu(int d) { return g_devs.dev[d >= 0 && d < kMaxDevices ? d : 0].ncu; }
+uint32_t dev_stack_guard(int d) { return g_devs.dev[d >= 0 && d < kMaxDevices ? d : 0].stack_guard; }
 
 template <class T>
 struct DBuf {
@@ -833,6 +838,7 @@ void session_launch(gg_session* s) {
   A.xcd_cursor = s->dv->d_counters.p + 16;
   A.lane_heaps = s->dv->d_lane_heaps.p; A.lane_heap_bytes = s->lane_heap_bytes; A.lane_recs_bytes = s->lane_recs_bytes;
   A.lane_docs = s->lane_docs;
+  A.stack_guard = dev_stack_guard(s->device);
   A.retry_list = s->mode == 1 ? nullptr : s->dv->d_retry.p;
   A.wave_frames_bytes = gg_session::kWaveFrames; A.wave_recs_bytes = gg_session::kWaveRecs;
   A.retry2_list = s->dv->d_retry2.p; A.retry2_count = s->dv->d_counters.p + 4;
@@ -1035,6 +1041,9 @@ struct ReportSink {
   virtual char* reserve(size_t n) = 0;
   virtual void commit(size_t n) = 0;
   virtual size_t max_piece() const { return SIZE_MAX; }
+  // reserve() hands out page-locked host memory: the device report's copy-out may switch from the copy
+  // engine to the shader copy (d2h_push reads the host pointer's device mapping) -- never for pageable memory
+  virtual bool pinned() const { return false; }
   void write(const char* p, size_t n) {
     while (n) {
       const size_t k = std::min(n, max_piece());
@@ -1071,6 +1080,7 @@ struct CountingSink : ReportSink {
   char* reserve(size_t) override { return stage; }
   void commit(size_t k) override { n += k; }
   size_t max_piece() const override { return stage_bytes; }
+  bool pinned() const override { return true; }   // DeviceBufs::pinned staging
 };
 
 struct DevReportStats { uint64_t device_docs = 0, host_docs = 0, bytes = 0; double size_ms = 0, write_ms = 0, d2h_ms = 0, host_ms = 0; };
@@ -1261,7 +1271,7 @@ bool device_report_text(gg_session* s, size_t first, size_t count, size_t report
   std::thread copier([&]() {
     // GG_D2H_ADAPT=0: no switch from a slow copy engine to the shader copy (A/B)
     int use_push = push_blocks;
-    const bool adapt = !push_blocks && !(getenv("GG_D2H_ADAPT") && atoi(getenv("GG_D2H_ADAPT")) == 0);
+    const bool adapt = !push_blocks && sink.pinned() && !(getenv("GG_D2H_ADAPT") && atoi(getenv("GG_D2H_ADAPT")) == 0);
     uint64_t engine_bytes = 0;
     double engine_ms = 0;
     try {
@@ -1552,6 +1562,7 @@ bool shards_report(const std::vector<ShardView>& sh, std::string& out, int32_t& 
         n += k;
       }
       size_t max_piece() const override { return in.max_piece(); }
+      bool pinned() const override { return in.pinned(); }
     } results(sink);
     for (const ShardView& v : sh) {
       if (!v.count || v.s->progs.empty()) continue;
@@ -1993,6 +2004,7 @@ struct CallbackSink : ReportSink {
   uint64_t n = 0;
   CallbackSink(cfn_guard_write_fn f, void* c, char* st, size_t sb) : fn(f), ctx(c), stage(st), stage_bytes(sb) {}
   char* reserve(size_t) override { return stage; }
+  bool pinned() const override { return true; }   // pinned_get staging
   void commit(size_t k) override {
     if (!failed && k && fn(ctx, stage, k) != 0) failed = true;
     n += k;
@@ -2124,6 +2136,7 @@ int32_t stream_single(int dev, const validate_input_t* docs, size_t n_docs, cons
       }
       void commit(size_t n) override { in.commit(n); }
       size_t max_piece() const override { return in.max_piece(); }
+      bool pinned() const override { return in.pinned(); }
     };
     struct ChunkReport {
       std::thread th;
@@ -2227,9 +2240,15 @@ int32_t stream_single(int dev, const validate_input_t* docs, size_t n_docs, cons
         }
         mark("reported", k);
         {
-          std::lock_guard<std::mutex> lk(turn.m);
-          if (cr->ok && cr->internal.empty()) turn.turn = k + 1;
-          else turn.abort = true;   // the chunks after a failed one are not written
+          // the turn passes strictly in chunk order: a chunk that wrote nothing (and so never waited in
+          // OrderedSink::reserve) still waits for its predecessor before handing the turn on
+          std::unique_lock<std::mutex> lk(turn.m);
+          if (cr->ok && cr->internal.empty()) {
+            turn.cv.wait(lk, [&] { return turn.turn == k || turn.abort; });
+            if (!turn.abort) turn.turn = k + 1;
+          } else {
+            turn.abort = true;   // the chunks after a failed one are not written
+          }
         }
         turn.cv.notify_all();
         std::unique_ptr<gg_session> done;
@@ -2373,6 +2392,7 @@ struct ChainSink : ReportSink {
   }
   void commit(size_t k) override { blocks.back().second += k; n += k; }
   size_t max_piece() const override { return PinnedPool::kBlock; }
+  bool pinned() const override { return true; }
 };
 }  // namespace
 
@@ -3835,6 +3855,8 @@ int64_t gg_device_cache_release(int32_t device) {
     released += (int64_t)dev_cache_held(d);
     dev_cache_flush(d);
   }
+  // the streamed entries' pinned staging blocks (host_pinned.h PinnedCache)
+  released += (int64_t)pinned_cache_flush(device);
   return released;
 }
 

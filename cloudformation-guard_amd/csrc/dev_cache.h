@@ -4,8 +4,11 @@
 // loads chunk k+1 and tears down chunk k-1's session while chunk k's report kernels and copies run on
 // another thread: every hipFree of a loader temporary or a session buffer waited for that report.
 // dev_free puts a block on its device's free list instead (the caller has synchronised every stream
-// that used it, as before a hipFree); dev_alloc takes a cached block of the same size class before
-// calling hipMalloc.  A hipMalloc that fails empties the device's list and tries once more.
+// that used it, as before a hipFree); dev_free_on(p, stream) is for a caller that may still have work
+// queued on `stream` (an exception unwinding past a loader pass): it records an event there, and the block
+// is handed out again only once that event has completed -- the ordering hipFree enforced device-wide,
+// enforced per block.  dev_alloc takes a cached block of the same size class whose fence (if any) has
+// passed before calling hipMalloc.  A hipMalloc that fails empties the device's list and tries once more.
 // GG_DEV_CACHE_GB bounds the bytes a device's list holds (default 16; 0 turns the cache off).  Memory held
 // here is invisible to the HIP runtime and to torch's allocator in the same process, so the default stays
 // well under the 288 GB of one MI355X.
@@ -22,8 +25,10 @@ namespace gg {
 
 struct DevCache {
   static constexpr int kDevs = 64;
+  struct Block { void* p; hipEvent_t fence; };   // fence: null, or the event the block waits for
   std::mutex mu;
-  std::multimap<size_t, void*> free_list[kDevs];
+  std::multimap<size_t, Block> free_list[kDevs];
+  std::vector<hipEvent_t> spare_events[kDevs];
   size_t held[kDevs] = {};
   std::unordered_map<void*, std::pair<int, size_t>> live;   // block -> (device, class bytes)
   size_t cap = 0;
@@ -59,14 +64,17 @@ inline size_t dev_cache_held(int dev) {
 
 inline void dev_cache_flush(int dev) {
   DevCache& C = dev_cache();
-  std::vector<void*> out;
+  std::vector<DevCache::Block> out;
   {
     std::lock_guard<std::mutex> lk(C.mu);
     for (auto& kv : C.free_list[dev]) out.push_back(kv.second);
     C.free_list[dev].clear();
     C.held[dev] = 0;
   }
-  for (void* p : out) (void)hipFree(p);
+  for (auto& b : out) {
+    if (b.fence) { (void)hipEventSynchronize(b.fence); (void)hipEventDestroy(b.fence); }
+    (void)hipFree(b.p);
+  }
 }
 
 inline hipError_t dev_alloc(void** out, size_t bytes) {
@@ -77,9 +85,13 @@ inline hipError_t dev_alloc(void** out, size_t bytes) {
   {
     std::lock_guard<std::mutex> lk(C.mu);
     auto& fl = C.free_list[dev];
-    auto it = fl.lower_bound(c);
-    if (it != fl.end() && it->first == c) {
-      *out = it->second;
+    for (auto it = fl.lower_bound(c); it != fl.end() && it->first == c; ++it) {
+      // a fenced block is taken only once the work queued before its dev_free_on has completed
+      if (it->second.fence) {
+        if (hipEventQuery(it->second.fence) != hipSuccess) { (void)hipGetLastError(); continue; }
+        C.spare_events[dev].push_back(it->second.fence);
+      }
+      *out = it->second.p;
       C.held[dev] -= c;
       fl.erase(it);
       C.live[*out] = {dev, c};
@@ -108,8 +120,9 @@ inline hipError_t dev_alloc(T** out, size_t bytes) {
   return e;
 }
 
-// p: from dev_alloc (or null); no stream may still use it
-inline void dev_free(void* p) {
+// p: from dev_alloc (or null).  fenced: work that may use p is still queued on `stream` (the device current
+// on this thread): the block is cached behind an event recorded there; otherwise no stream may still use it.
+inline void dev_free_impl(void* p, bool fenced, hipStream_t stream) {
   if (!p) return;
   DevCache& C = dev_cache();
   {
@@ -120,14 +133,28 @@ inline void dev_free(void* p) {
       const size_t c = it->second.second;
       C.live.erase(it);
       if (C.held[dev] + c <= C.cap) {
-        C.free_list[dev].emplace(c, p);
+        hipEvent_t ev = nullptr;
+        if (fenced) {
+          if (!C.spare_events[dev].empty()) { ev = C.spare_events[dev].back(); C.spare_events[dev].pop_back(); }
+          else if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) ev = nullptr;
+          if (!ev || hipEventRecord(ev, stream) != hipSuccess) {
+            // no fence could be placed: hipFree's device-wide wait instead of a block of unknown state
+            if (ev) (void)hipEventDestroy(ev);
+            (void)hipGetLastError();
+            goto release;
+          }
+        }
+        C.free_list[dev].emplace(c, DevCache::Block{p, ev});
         C.held[dev] += c;
         return;
       }
     }
   }
+release:
   (void)hipFree(p);
 }
+inline void dev_free(void* p) { dev_free_impl(p, false, nullptr); }
+inline void dev_free_on(void* p, hipStream_t stream) { dev_free_impl(p, true, stream); }
 
 // p: from dev_alloc (or null), possibly still in use by queued work: hipFree's device-wide wait
 inline void dev_free_sync(void* p) {

@@ -108,7 +108,7 @@ __device__ __attribute__((always_inline)) inline void tile_ptrs_wave(CtxT& c, co
                                                                      uint32_t doc, uint8_t* heap, uint32_t frames_bytes,
                                                                      uint32_t recs_bytes) {
   c.P = (decltype(c.P))P; c.dn = A.docs.nodes + A.docs.base[doc]; c.kl = A.docs.klen + A.docs.base[doc]; c.db = A.docs.bytes; c.heap = heap;
-  c.fcap = frames_bytes; c.rcap = recs_bytes;
+  c.fcap = frames_bytes; c.rcap = recs_bytes; c.sguard = A.stack_guard;
   c.resmap = A.docs.res_map ? A.docs.res_map[doc] : NONE;
   c.tix = c.resmap != NONE ? A.docs.tix + A.docs.tix_off[doc] : nullptr;
   c.type_key = A.docs.type_key;
@@ -168,7 +168,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
   if (lane == 0) {
     g_wave.heap = heap; g_wave.nodes = A.docs.nodes; g_wave.klen = A.docs.klen; g_wave.db = A.docs.bytes;
     g_wave.tix = A.docs.tix; g_wave.fcap = FRAMES_BYTES; g_wave.rcap = A.lane_recs_bytes; g_wave.type_key = A.docs.type_key;
-    g_wave.recs = A.recs; g_wave.rchunk = A.rec_chunk;
+    g_wave.recs = A.recs; g_wave.rchunk = A.rec_chunk; g_wave.sguard = A.stack_guard;
   }
   __syncthreads();
   uint32_t staged = NONE;
@@ -224,9 +224,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
       if (!c.err) for (uint32_t i = 0; i < P->n_slots; i++) u32a(c, c.memo)[i] = 3u;
       c.vtab = alloc_pers(c, (P->n_vars ? P->n_vars : 1) * 16);
       if (!c.err) for (uint32_t i = 0; i < P->n_vars; i++) u32a(c, c.vtab)[i * 4] = 0u;
-#if GG_MACHINE
-      c.kbase = alloc_pers(c, KDEPTH * KFRAME); c.kdepth = 0;
-#endif
       push_frame(c, F_ROOT, NONE, A.docs.roots[doc], P->root_block);
       uint32_t fails = 0, passes = 0;
       uint8_t* rs = A.rule_status + (size_t)tile * A.max_top;
@@ -257,7 +254,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
     base = __shfl(base, 0);
     if (active) {
       uint32_t off = base + incl - need;
-      bool retry = c.err == E_HEAP || c.err == E_RECORDS || c.err == E_DEPTH;
+      bool retry = c.err == E_HEAP || c.err == E_RECORDS || c.err == E_DEPTH;   // not E_STACK: wave frames are larger
       if (retry) A.retry_list[atomicAdd(A.retry_count, 1u)] = tile;
       if (need && off + need > A.rec_cap) { c.err = E_RECORDS; n = 0; }
       const uint32_t naux = n ? c.naux : 0, nrec = n - naux;

@@ -217,7 +217,7 @@ enum ErrKind : uint32_t {
   E_OK = 0, E_UNSUPPORTED = 1, E_HEAP = 2, E_EMPTY_INCOMPATIBLE = 3, E_TYPEBLOCK_UNRESOLVED = 4,
   E_VAR_MISSING = 5, E_RULE_MISSING = 6, E_INTERP_NON_STRING = 7, E_INTERP_QUERY = 8,
   E_PARAM_MISSING = 9, E_PARAM_ARITY = 10, E_NO_RHS = 11, E_RECORDS = 12, E_DEPTH = 13,
-  E_REGEX_UNSUPPORTED = 14,
+  E_REGEX_UNSUPPORTED = 14, E_STACK = 15,
 };
 
 // per-tile result header written by the kernel

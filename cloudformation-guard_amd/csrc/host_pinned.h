@@ -5,6 +5,8 @@
 // as PCIe.  pinned_alloc maps the pages itself, binds them to the device's node (the PCI device's
 // numa_node in sysfs), touches them there and registers them with the runtime; without a known node, or
 // when any step fails, it falls back to hipHostMalloc.  GG_PINNED_NUMA=0 turns the placement off (A/B).
+// The policy is MPOL_PREFERRED: a node short of free memory places the pages elsewhere instead of
+// making the first touch reclaim or fail there.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -50,7 +52,7 @@ inline void* pinned_alloc(size_t bytes, int dev) {
     void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
     if (p != MAP_FAILED) {
       unsigned long mask = 1ul << node;
-      bool ok = syscall(SYS_mbind, p, bytes, MPOL_BIND, &mask, 64ul, 0u) == 0;
+      bool ok = syscall(SYS_mbind, p, bytes, MPOL_PREFERRED, &mask, 64ul, 0u) == 0;
       if (ok) memset(p, 0, bytes);   // first touch: the pages are allocated on the node now
       if (ok) ok = hipHostRegister(p, bytes, hipHostRegisterDefault) == hipSuccess;
       if (ok) {
@@ -87,13 +89,21 @@ inline void pinned_free(void* p) {
 // Process-wide cache of pinned blocks by (device, size): the streamed entries take their staging and chunk
 // blocks here and give them back at the end of the call instead of unpinning them (pinning 256 MB costs
 // ~0.1 s, and the report copy-out of the sessions after a call that unpinned its staging was measured at
-// half the rate, profiles/r05x_report_ab.log).  At most kPinnedCacheBytes per device stay cached.
+// half the rate, profiles/r05x_report_ab.log).  At most GG_PINNED_CACHE_GB per device stay cached (default
+// 1: the one-device stream's 256 MB staging plus a device-list stream's working set of 64 MB blocks); page-
+// locked memory is invisible to the rest of the host, so gg_device_cache_release hands it back too
+// (pinned_cache_flush).
 struct PinnedCache {
-  static constexpr size_t kPinnedCacheBytes = (size_t)8 << 30;
+  size_t cap;
   std::mutex mu;
   std::unordered_map<uint64_t, std::vector<void*>> free;   // (device << 48 | bytes) -> blocks
   std::unordered_map<int, size_t> cached;                  // device -> bytes in `free`
-  static PinnedCache& get() { static PinnedCache c; return c; }
+  PinnedCache() {
+    const char* e = getenv("GG_PINNED_CACHE_GB");
+    const double gb = e ? atof(e) : 1.0;
+    cap = gb > 0 ? (size_t)(gb * (double)(1ull << 30)) : 0;
+  }
+  static PinnedCache& get() { static PinnedCache* c = new PinnedCache; return *c; }
 };
 inline void* pinned_get(size_t bytes, int dev) {
   PinnedCache& c = PinnedCache::get();
@@ -114,13 +124,32 @@ inline void pinned_put(void* p, size_t bytes, int dev) {
   PinnedCache& c = PinnedCache::get();
   {
     std::lock_guard<std::mutex> lk(c.mu);
-    if (c.cached[dev] + bytes <= PinnedCache::kPinnedCacheBytes) {
+    if (c.cached[dev] + bytes <= c.cap) {
       c.free[((uint64_t)dev << 48) | bytes].push_back(p);
       c.cached[dev] += bytes;
       return;
     }
   }
   pinned_free(p);
+}
+// unpins and frees the cached blocks of `dev` (-1: every device); returns the bytes released
+inline size_t pinned_cache_flush(int dev) {
+  PinnedCache& c = PinnedCache::get();
+  std::vector<void*> out;
+  size_t bytes = 0;
+  {
+    std::lock_guard<std::mutex> lk(c.mu);
+    for (auto it = c.free.begin(); it != c.free.end();) {
+      const int d = (int)(it->first >> 48);
+      if (dev >= 0 && d != dev) { ++it; continue; }
+      const size_t b = (size_t)(it->first & ((1ull << 48) - 1));
+      for (void* p : it->second) { out.push_back(p); bytes += b; }
+      c.cached[d] = 0;
+      it = c.free.erase(it);
+    }
+  }
+  for (void* p : out) pinned_free(p);
+  return bytes;
 }
 
 }  // namespace gg

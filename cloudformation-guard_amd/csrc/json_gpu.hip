@@ -674,13 +674,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GG_JSO
   }
 }
 
+// the loader's passes run on the null stream; a pass may still be queued when an error unwinds the
+// loader, so every array goes back to the block cache behind a fence on that stream (dev_cache.h)
 template <typename T>
 struct DevArr {
   T* p = nullptr;
   size_t n = 0;
-  ~DevArr() { dev_free(p); }
+  ~DevArr() { dev_free_on(p, nullptr); }
   void alloc(size_t count) {
-    dev_free(p);
+    dev_free_on(p, nullptr);
     p = nullptr;
     n = count;
     JCHK(dev_alloc(&p, std::max<size_t>(count, 1) * sizeof(T)));

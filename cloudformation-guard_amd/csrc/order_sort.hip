@@ -31,10 +31,12 @@ void device_segmented_order(const unsigned long long* key, uint32_t* order, uint
   unsigned long long* keys_out = nullptr;
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
+  // fenced on `st`: an error thrown between the launches and the final synchronisation leaves work queued
   struct Free {
     void** p[4];
-    ~Free() { for (auto q : p) gg::dev_free(*q); }
-  } fr{{(void**)&vals_in, (void**)&d_seg, (void**)&keys_out, &tmp}};
+    hipStream_t s;
+    ~Free() { for (auto q : p) gg::dev_free_on(*q, s); }
+  } fr{{(void**)&vals_in, (void**)&d_seg, (void**)&keys_out, &tmp}, st};
   chk(gg::dev_alloc(&vals_in, (size_t)n * 4), "order values");
   chk(gg::dev_alloc(&keys_out, (size_t)n * 8), "order keys");
   chk(gg::dev_alloc(&d_seg, (size_t)(nseg + 1) * 4), "order segments");

@@ -1034,6 +1034,10 @@ void tile_error(const DocBatch& docs, uint32_t doc, const Program& prog, const T
     case E_HEAP: err.kind = "Unsupported"; err.msg = "MI355X path: per-tile scratch heap exhausted"; break;
     case E_RECORDS: err.kind = "Unsupported"; err.msg = "MI355X path: failure-record buffer exhausted"; break;
     case E_DEPTH: err.kind = "Unsupported"; err.msg = "MI355X path: evaluation depth limit exceeded"; break;
+    case E_STACK:
+      err.kind = "Unsupported";
+      err.msg = "MI355X path: evaluation depth limit exceeded (rules nest deeper than the device lane stack)";
+      break;
     default: {
       if (t.err_a == 2) {
         // a filter on a map after a step other than `*`, `[*]` or a key (e.g. `x[0][ ... ]`): the

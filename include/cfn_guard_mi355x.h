@@ -198,7 +198,9 @@ int32_t gg_device_available(void);
 /* Frees the device blocks the library keeps for reuse on `device` (-1: every device).  Freed loader
  * temporaries and session buffers are cached per device (bounded by GG_DEV_CACHE_GB, default 16)
  * because hipFree waits for the whole device to go idle; this hands them back, as
- * torch.cuda.empty_cache() does for torch's allocator.  Returns the bytes released. */
+ * torch.cuda.empty_cache() does for torch's allocator.  The streamed entries' page-locked host staging
+ * blocks (bounded by GG_PINNED_CACHE_GB per device, default 1) are unpinned and freed too.  Returns the
+ * bytes released (device and host). */
 int64_t gg_device_cache_release(int32_t device);
 
 /* Asynchronous evaluation on a caller stream (bench.py passes a non-default torch stream).  NULL

@@ -15,10 +15,9 @@ NAMES = ["node_reads", "heap_accesses", "query_calls", "clause_evals", "frames",
 TIMES = ["eval_rule", "query_retrieval", "binary_operation", "unary_operation", "rec_push", "filter_test",
          "resolve_variable", "push_frame", "tile_total"]
 # entries of the noinline evaluator functions per tile (stats slots 18..31; eval_core.inc FCALL)
-# machine counters per tile (stats slots 18..31; eval_machine.inc FCALL): loop iterations the lane was live
-# in, iterations it stepped in (the wave ran its key), steps with a walk, frames pushed
-FCALLS = ["iter_live", "iter_step", "walk_steps", "frames_pushed", "fc4", "fc5", "fc6", "fc7", "fc8", "fc9", "fc10",
-          "fc11", "fc12", "fc13"]
+FCALLS = ["eval_conj", "eval_rule", "block_clause", "type_block", "param_call", "misc_call", "query_retrieval",
+          "walk_run", "compare_op", "resolve_variable", "resolve_function", "map_key_filter", "key_var_step",
+          "filter_test"]
 ndocs = int(sys.argv[1]) if len(sys.argv) > 1 else 20000
 out = {}
 PACK = os.environ.get("PACK", "cfg2")
