@@ -420,6 +420,7 @@ struct gg_session {
   uint32_t nslots = 0;            // wave-mode grid
   uint32_t lane_slots = 0;        // lane-mode grid (waves)
   uint32_t lane_docs = 64;        // lane mode: documents per batch (session_upload)
+  uint32_t lane_group = 1;        // lane mode: lanes per document (64 / lane_docs in lane groups, else 1)
   uint32_t heap_bytes = 512 * 1024;
   static constexpr uint32_t kWaveFrames = 16 * 1024, kWaveRecs = 64 * 1024;
   // large-heap pass (rare: documents with thousands of failing clause values or deep nesting)
@@ -739,13 +740,30 @@ void session_upload(gg_session* s) {
   }
   size_t ntiles = s->docs.ndocs() * s->progs.size();
   const bool large_docs = s->docs.ndocs() && arena_nodes(s) / s->docs.ndocs() > 4096;
-  // Documents per lane batch: 64 (a wave's lanes), or 16 for a launch of few large documents (cfg4: 8192
-  // Terraform plans of ~60 K nodes fill 256 waves, one per CU, each walking 64 plans whose list lengths and
-  // filter outcomes differ from lane to lane -- the wave runs the union of their paths).  16 documents per
-  // wave quarter the divergence and give each CU four waves.  GG_LANE_DOCS overrides (A/B).
+  // Documents per lane batch: 64 (a wave's lanes, one tile each), or -- for a launch of few large documents
+  // (cfg4: 8192 Terraform plans of ~60 K nodes; at 64 per wave they fill 256 waves, one per CU, and one lane
+  // walks a whole plan's 2000-entry lists) -- L = 64 / G documents with G lanes each: the G lanes of a
+  // document run its tile in step and split every chunk of its filtered list fan-outs (coop_chunk), and the
+  // launch fills the machine's 16 waves per CU.  GG_LANE_GROUP sets G (1 turns the groups off), GG_LANE_DOCS
+  // sets L with one lane per document (the round-5 sparse batches; A/B).
   s->lane_docs = 64;
-  if (large_docs && (s->docs.ndocs() + 63) / 64 * s->progs.size() < (size_t)dev_ncu(s->device) * 4) s->lane_docs = 16;
-  if (const char* e = getenv("GG_LANE_DOCS")) s->lane_docs = (uint32_t)std::min(64, std::max(1, atoi(e)));
+  s->lane_group = 1;
+  {
+    const size_t fill = (size_t)dev_ncu(s->device) * 16;   // waves the lane kernel keeps resident
+    if (large_docs && (s->docs.ndocs() + 63) / 64 * s->progs.size() < fill) {
+      size_t L = 64;
+      while (L > 1 && (s->docs.ndocs() + L - 1) / L * s->progs.size() < fill) L >>= 1;
+      s->lane_docs = (uint32_t)L;
+      s->lane_group = (uint32_t)(64 / L);
+    }
+    if (const char* e = getenv("GG_LANE_GROUP")) {
+      uint32_t g = 1;
+      while (g < 64 && g * 2 <= (uint32_t)std::max(1, atoi(e))) g *= 2;
+      s->lane_group = g;
+      s->lane_docs = 64 / g;
+    }
+    if (const char* e = getenv("GG_LANE_DOCS")) { s->lane_docs = (uint32_t)std::min(64, std::max(1, atoi(e))); s->lane_group = 1; }
+  }
   size_t nbatches = (s->docs.ndocs() + s->lane_docs - 1) / s->lane_docs * s->progs.size();
   // wave mode: all tiles (mode 1) or only the lane kernel's overflow tiles (mode 0)
   size_t wave_slots = s->mode == 1 ? (size_t)dev_ncu(s->device) * 8 : (size_t)dev_ncu(s->device) * 2;
@@ -762,20 +780,29 @@ void session_upload(gg_session* s) {
   // budget unused while their tiles outgrow 64 KB (hundreds of records, long QR lists) and fall back to
   // the wave kernel one tile per wave: such launches get 256 KB lane heaps with 96 KB of record staging
   // while the heaps stay within kLaneHeapBudget
-  static constexpr size_t kLaneHeapBudget = (size_t)24 << 30;
+  // Lane groups: every lane of a document's group holds its own copy of the tile's state, so the 256 KB heaps
+  // are budgeted at 48 GB of the MI355X's 288 GB -- the resident waves are capped to fit (3072 = 12 per CU)
+  static constexpr size_t kLaneHeapBudget = (size_t)24 << 30, kGroupHeapBudget = (size_t)48 << 30;
   s->lane_heap_bytes = s->lane_heap_set ? s->lane_heap_set : 64u * 1024u;
   s->lane_recs_bytes = 24576;
-  if (!s->lane_heap_set && large_docs && s->lane_slots && (size_t)s->lane_slots * 64 * (256u << 10) <= kLaneHeapBudget) {
-    s->lane_heap_bytes = 256u << 10;
-    s->lane_recs_bytes = 2048u * (uint32_t)sizeof(Rec);
+  if (!s->lane_heap_set && large_docs && s->lane_slots) {
+    if (s->lane_group > 1) {
+      s->lane_heap_bytes = 256u << 10;
+      s->lane_recs_bytes = 2048u * (uint32_t)sizeof(Rec);
+      const size_t cap = kGroupHeapBudget / ((size_t)64 * s->lane_heap_bytes) & ~(size_t)7;
+      if (s->lane_slots > cap) s->lane_slots = (uint32_t)std::max<size_t>(cap, 8);
+    } else if ((size_t)s->lane_slots * 64 * (256u << 10) <= kLaneHeapBudget) {
+      s->lane_heap_bytes = 256u << 10;
+      s->lane_recs_bytes = 2048u * (uint32_t)sizeof(Rec);
+    }
   }
   s->dv->d_lane_heaps.alloc((size_t)s->lane_slots * 64 * s->lane_heap_bytes);
   s->dv->d_retry.alloc(std::max<size_t>(ntiles, 1));
   s->dv->d_retry2.alloc(std::max<size_t>(ntiles, 1));
   s->dv->d_tiles.alloc(std::max<size_t>(ntiles, 1));
   s->dv->d_rule_status.alloc(std::max<size_t>(ntiles * s->max_top, 1));
-  // direct record chunks (lane mode): rec_chunk slots per lane per batch, reserved by every lane batch of a
-  // launch.  GG_REC_CHUNK overrides (0: every record staged in the lane heap, the round-3 path); halved
+  // direct record chunks (lane mode): rec_chunk slots per document per batch (lane_docs documents), reserved
+  // by every lane batch of a launch.  GG_REC_CHUNK overrides (0: every record staged in the lane heap, the round-3 path); halved
   // until the reservations fit kMaxChunkBytes (<= 8 slots: off)
   s->rec_chunk = 0;
   size_t reserve = 0;
@@ -787,12 +814,13 @@ void session_upload(gg_session* s) {
     // few batches (large documents, hundreds of records per tile): chunks as large as 2 GB of
     // reservations allows, up to 1024 records per lane
     static constexpr size_t kSmallChunkBytes = (size_t)2 << 30;
-    if (large_docs && lane_batches && lane_batches * 64 * 32 * sizeof(Rec) < kSmallChunkBytes)
-      ch = std::min<size_t>(1024, kSmallChunkBytes / (lane_batches * 64 * sizeof(Rec)));
+    const size_t per = s->lane_docs;   // record columns per batch: its documents (eval_kernel.hip rbase)
+    if (large_docs && lane_batches && lane_batches * per * 32 * sizeof(Rec) < kSmallChunkBytes)
+      ch = std::min<size_t>(1024, kSmallChunkBytes / (lane_batches * per * sizeof(Rec)));
     if (getenv("GG_REC_CHUNK")) ch = (size_t)std::max(0, atoi(getenv("GG_REC_CHUNK")));
     static constexpr size_t kMaxChunkBytes = (size_t)24 << 30;
-    while (ch >= 8 && lane_batches * 64 * ch * sizeof(Rec) > kMaxChunkBytes) ch /= 2;
-    if (ch >= 8 && lane_batches * 64 * ch < 0xC0000000ull) { s->rec_chunk = (uint32_t)ch; reserve = lane_batches * 64 * ch; }
+    while (ch >= 8 && lane_batches * per * ch * sizeof(Rec) > kMaxChunkBytes) ch /= 2;
+    if (ch >= 8 && lane_batches * per * ch < 0xC0000000ull) { s->rec_chunk = (uint32_t)ch; reserve = lane_batches * per * ch; }
   }
   s->rec_cap = reserve + std::min<size_t>(std::max<size_t>(ntiles * 48, 4096), (size_t)96 * 1024 * 1024);
   s->rec_cap = std::min<size_t>(s->rec_cap, (size_t)0xFFFFFFF0u);
@@ -838,6 +866,7 @@ void session_launch(gg_session* s) {
   A.xcd_cursor = s->dv->d_counters.p + 16;
   A.lane_heaps = s->dv->d_lane_heaps.p; A.lane_heap_bytes = s->lane_heap_bytes; A.lane_recs_bytes = s->lane_recs_bytes;
   A.lane_docs = s->lane_docs;
+  A.lane_group = s->lane_group;
   A.stack_guard = dev_stack_guard(s->device);
   A.retry_list = s->mode == 1 ? nullptr : s->dv->d_retry.p;
   A.wave_frames_bytes = gg_session::kWaveFrames; A.wave_recs_bytes = gg_session::kWaveRecs;
@@ -919,7 +948,7 @@ uint32_t session_records_wanted(gg_session* s) {
   return nrec;
 }
 
-// Compacts every tile's records -- in place in their lane's direct chunk (TileOut.pad1 == 1) or contiguous
+// Compacts every tile's records -- in place in their lane's direct chunk (TileOut.pad1 = stride > 1) or contiguous
 // -- into one dense array in tile order and copies it to the host (s->recs), rewriting the host tiles'
 // rec_off to the dense offsets.  Only host writers read the dense array: the device reporter reads the
 // records where the evaluation left them (report_gpu.hip RecSeq), so a device-rendered report needs no
@@ -2014,6 +2043,7 @@ struct CallbackSink : ReportSink {
 }  // namespace
 
 namespace {
+bool first_load_error(const validate_input_t* docs, size_t from, size_t n, std::string& kind, std::string& msg);
 int32_t stream_single(int dev, const validate_input_t* docs, size_t n_docs, const validate_input_t* rules,
                       size_t n_rules, size_t chunk_docs, cfn_guard_write_fn write, void* ctx,
                       int32_t* exit_code, extern_err_t* err) {
@@ -2154,12 +2184,21 @@ int32_t stream_single(int dev, const validate_input_t* docs, size_t n_docs, cons
       }
     } join_reports{reps, turn};
     // the first failed chunk report in document order (joining every report before it), or -1
+    // the one-string call loads every data file before it evaluates or reports: a document after chunk j that
+    // does not load takes precedence over chunk j's evaluation or report error
+    auto later_load_error = [&](size_t j, std::string& k, std::string& m) {
+      return first_load_error(docs, std::min(n_docs, (j + 1) * chunk), n_docs, k, m);
+    };
     auto first_failure = [&](size_t upto) -> int32_t {
       for (size_t j = 0; j < upto; j++) {
         if (!reps[j]) continue;
         if (reps[j]->th.joinable()) reps[j]->th.join();
         if (!reps[j]->internal.empty()) return fail(-1, reps[j]->internal);
-        if (!reps[j]->ok) return fail(ffi_code(reps[j]->re.kind), error_display(reps[j]->re.kind, reps[j]->re.msg));
+        if (!reps[j]->ok) {
+          std::string lk, lm;
+          if (later_load_error(j, lk, lm)) return fail(ffi_code(lk), error_display(lk, lm));
+          return fail(ffi_code(reps[j]->re.kind), error_display(reps[j]->re.kind, reps[j]->re.msg));
+        }
       }
       if (sink.failed) return fail(-1, "the write callback failed");
       return 0;
@@ -2207,6 +2246,8 @@ int32_t stream_single(int dev, const validate_input_t* docs, size_t n_docs, cons
           for (auto& p : s->progs) progs.push_back(&p->prog);
           ReportError re;
           tile_error(s->docs, (uint32_t)(t / nf), *progs[t % nf], s->tiles[t], re);
+          std::string lk, lm;
+          if (later_load_error(k, lk, lm)) return fail(ffi_code(lk), error_display(lk, lm));
           return fail(ffi_code(re.kind), error_display(re.kind, re.msg));
         }
         if (s->tiles[t].status == ST_FAIL) anyfail = true;
@@ -2426,7 +2467,7 @@ int32_t cfn_guard_validate_batch_stream_devices(const validate_input_t* docs, si
       int state = 0;          // 0 pending, 1 ready, 2 failed
       ChainSink text;
       explicit Out(PinnedPool& p) : text(p) {}
-      bool anyfail = false;
+      bool anyfail = false, load_error = false;
       int32_t parse_code = 0;
       std::string kind, msg;
     };
@@ -2450,6 +2491,7 @@ int32_t cfn_guard_validate_batch_stream_devices(const validate_input_t* docs, si
           try {
             const size_t first = k * chunk, count = std::min(chunk, n_docs - first);
             std::unique_ptr<gg_session> ses = stream_chunk_session(devs[p], docs, n_docs, rules, n_rules, first, count, kind, msg);
+            o.load_error = !kind.empty();
             if (kind.empty()) {
               o.parse_code = ses->parse_errors.empty() ? 0 : 5;
               ReportError re;
@@ -2491,7 +2533,13 @@ int32_t cfn_guard_validate_batch_stream_devices(const validate_input_t* docs, si
         std::unique_lock<std::mutex> lk(mu);
         cv.wait(lk, [&] { return o.state != 0; });
       }
-      if (o.state == 2) return fail(ffi_code(o.kind), error_display(o.kind, o.msg));
+      if (o.state == 2) {
+        // an evaluation or report error yields to a later document that does not load (one-string precedence)
+        std::string lk, lm;
+        if (!o.load_error && o.kind != "Internal" && first_load_error(docs, std::min(n_docs, (k + 1) * chunk), n_docs, lk, lm))
+          return fail(ffi_code(lk), error_display(lk, lm));
+        return fail(ffi_code(o.kind), error_display(o.kind, o.msg));
+      }
       if (k == 0) { parse_code = o.parse_code; sink.write("[\n", 2); }
       anyfail = anyfail || o.anyfail;
       // the pinned blocks go to the callback as they are (no staging copy), then back to the pool; a
@@ -2513,6 +2561,388 @@ int32_t cfn_guard_validate_batch_stream_devices(const validate_input_t* docs, si
     if (sink.failed) return fail(-1, "the write callback failed");
     if (exit_code) *exit_code = anyfail ? 19 : parse_code;
     return 0;
+  } catch (std::exception& e) {
+    return fail(-1, e.what());
+  }
+}
+
+// ------------------------------------------------------- streamed, every format and -i ---
+// cfn_guard_validate_batch_stream_ex: the streamed entries with the whole structured contract of the
+// one-string call -- output format (structured.rs:122-129: JSON / YAML through serde, SARIF sarif.rs:29-53,
+// 127-160, JUnit xml.rs / reporters/mod.rs) and input parameters merged into every data file (validate.rs:317-350,
+// structured.rs:51-65) -- over a device list.  JSON without parameters runs the streamed JSON paths above.
+// Otherwise chunk k is loaded (host loader + merge when parameters are given, else the device loader),
+// evaluated and -- for JSON / YAML, whose documents' texts simply concatenate -- rendered on pipeline k % ndev
+// and written in order while later chunks run (host memory: two chunks' reports per device).  SARIF lists its
+// artifacts (the FAILed documents' names) before every result and JUnit its totals before every suite, so
+// those two hold every chunk's evaluated session on its device (≈20 GB of HBM per 1 M CFN templates, no report
+// text) until the last is evaluated; then the frame goes out and each chunk's results / suites follow in
+// order, each session released once written.  Errors: the one-string call's error precedence -- a data file
+// that does not load (in order) before a parameter-file error, a merge panic, an erroring tile or an aborting
+// report -- so on any other failure the documents after the failing chunk are load-checked first.  JSON /
+// YAML write the chunks before the failing one (the caller drops that prefix); SARIF / JUnit write nothing.
+namespace {
+// the first document of [from, n) the host loader rejects, scanned on the host threads
+bool first_load_error(const validate_input_t* docs, size_t from, size_t n, std::string& kind, std::string& msg) {
+  if (from >= n) return false;
+  const size_t nt = std::max<size_t>(1, std::min<size_t>(report_threads(), (n - from) / 256 + 1));
+  std::vector<size_t> at(nt, SIZE_MAX);
+  std::vector<LoadError> les(nt);
+  parallel_run(nt, [&](size_t w) {
+    const size_t a = from + (n - from) * w / nt, b = from + (n - from) * (w + 1) / nt;
+    for (size_t i = a; i < b; i++) {
+      DocBatch tmp;
+      const char* t = docs[i].content ? docs[i].content : "";
+      if (!load_document(tmp, t, strlen(t), docs[i].file_name ? docs[i].file_name : "", LOAD_LIBYAML, les[w])) { at[w] = i; return; }
+    }
+  });
+  for (size_t w = 0; w < nt; w++)
+    if (at[w] != SIZE_MAX) { kind = les[w].kind; msg = les[w].msg; return true; }
+  return false;
+}
+
+// stream_chunk_session with input parameters: documents on the host loader, each merged with them; a merge
+// panic is returned as the chunk's error (panic = true) unless a later document of the chunk does not load
+std::unique_ptr<gg_session> stream_chunk_session_params(int dev, const validate_input_t* docs, size_t n_docs,
+                                                        const validate_input_t* rules, size_t n_rules, const DocBatch* params,
+                                                        size_t first, size_t count, std::string& kind, std::string& msg,
+                                                        bool& panic) {
+  panic = false;
+  if (!params) return stream_chunk_session(dev, docs, n_docs, rules, n_rules, first, count, kind, msg);
+  std::unique_ptr<gg_session> ses(new gg_session());
+  ses->device = dev;
+  ses->defer_recs = true;
+  for (size_t i = 0; i < n_rules; i++) {
+    std::string perr;
+    const std::string name = rules[i].file_name ? rules[i].file_name : "";
+    if (!add_rules(ses.get(), rules[i].content ? rules[i].content : "", name, perr))
+      ses->parse_errors.push_back("Parsing error handling rule file = " + name + ", Error = " + error_display("ParseError", perr) + "\n---");
+  }
+  LoadError pan;
+  bool panicked = false;
+  for (size_t i = first; i < first + count; i++) {
+    LoadError le;
+    const char* t = docs[i].content ? docs[i].content : "";
+    if (!load_document(ses->docs, t, strlen(t), docs[i].file_name ? docs[i].file_name : "", LOAD_LIBYAML, le)) {
+      kind = le.kind; msg = le.msg;
+      return ses;
+    }
+    if (!panicked && !merge_params_last(ses->docs, params, pan)) panicked = true;
+  }
+  if (panicked) { kind = pan.kind; msg = pan.msg; panic = true; return ses; }
+  if (ses->progs.empty()) {
+    ses->tiles.clear(); ses->rule_status.clear(); ses->recs.clear(); ses->evaluated = true;
+  } else {
+    session_upload(ses.get());
+    session_run(ses.get(), true);
+  }
+  return ses;
+}
+
+// the first erroring tile of an evaluated chunk (false + re), and whether any rules file FAILed
+bool chunk_tiles(gg_session* s, ReportError& re, bool& anyfail) {
+  const size_t nf = s->progs.size(), nd = s->docs.ndocs();
+  for (size_t t = 0; t < nd * nf; t++) {
+    if (s->tiles[t].err) {
+      ensure_host_arena(s);
+      std::vector<const Program*> progs;
+      for (auto& p : s->progs) progs.push_back(&p->prog);
+      tile_error(s->docs, (uint32_t)(t / nf), *progs[t % nf], s->tiles[t], re);
+      return false;
+    }
+    if (s->tiles[t].status == ST_FAIL) anyfail = true;
+  }
+  return true;
+}
+
+int32_t stream_format(const std::vector<int>& devs, const validate_input_t* docs, size_t n_docs, const validate_input_t* rules,
+                      size_t n_rules, const validate_input_t* params, size_t n_params, int32_t fmt, size_t chunk_docs,
+                      cfn_guard_write_fn write, void* ctx, int32_t* exit_code, extern_err_t* err) {
+  auto fail = [&](int32_t code, const std::string& msg) { set_err(err, code, msg); if (exit_code) *exit_code = -1; return -1; };
+  try {
+    std::unique_ptr<DocBatch> pbatch;
+    LoadError pe;
+    if (!load_params(params, n_params, pbatch, pe)) {
+      std::string k, m;
+      if (first_load_error(docs, 0, n_docs, k, m)) return fail(ffi_code(k), error_display(k, m));
+      return fail(ffi_code(pe.kind), error_display(pe.kind, pe.msg));
+    }
+    const bool hold = fmt == OUT_SARIF || fmt == OUT_JUNIT;
+    const size_t ndev = devs.size();
+    const size_t chunk = chunk_docs ? chunk_docs : (ndev > 1 ? (size_t)16384 : (size_t)262144);
+    const size_t nchunks = (n_docs + chunk - 1) / chunk;
+    PinnedPool pool;
+    struct Out {
+      int state = 0;          // 0 pending, 1 ready, 2 failed
+      ChainSink text;
+      std::unique_ptr<gg_session> ses;   // SARIF / JUnit: the evaluated chunk, until it is written
+      explicit Out(PinnedPool& p) : text(p) {}
+      bool anyfail = false, load_error = false;
+      int32_t parse_code = 0;
+      std::string kind, msg;
+    };
+    std::vector<std::unique_ptr<Out>> outs(nchunks);
+    for (auto& o : outs) o.reset(new Out(pool));
+    std::mutex mu;
+    std::condition_variable cv;
+    size_t written = 0;
+    bool stop = false;
+    std::vector<std::thread> pipes;
+    for (size_t p = 0; p < std::min(ndev, nchunks); p++) {
+      pipes.emplace_back([&, p]() {
+        for (size_t k = p; k < nchunks; k += ndev) {
+          {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return stop || hold || k < 2 * ndev || written > k - 2 * ndev; });
+            if (stop) return;
+          }
+          Out& o = *outs[k];
+          std::string kind, msg;
+          bool load_error = false;
+          try {
+            HIPCHK(hipSetDevice(devs[p]));
+            const size_t first = k * chunk, count = std::min(chunk, n_docs - first);
+            bool panic = false;
+            std::unique_ptr<gg_session> ses =
+                stream_chunk_session_params(devs[p], docs, n_docs, rules, n_rules, pbatch.get(), first, count, kind, msg, panic);
+            load_error = !kind.empty() && !panic;
+            if (kind.empty()) {
+              o.parse_code = ses->parse_errors.empty() ? 0 : 5;
+              ReportError re;
+              if (fmt == OUT_JSON) {
+                if (!stream_chunk_report(ses.get(), k, o.text, re, o.anyfail)) { kind = re.kind; msg = re.msg; }
+              } else if (!chunk_tiles(ses.get(), re, o.anyfail)) {
+                kind = re.kind; msg = re.msg;
+              } else if (hold) {
+                o.ses = std::move(ses);
+              } else {
+                // YAML: a chunk's block-sequence items; the chunks' streams concatenate
+                std::string out;
+                int32_t code = 0;
+                if (!session_report(ses.get(), out, code, re, OUT_YAML)) { kind = re.kind; msg = re.msg; }
+                else o.text.write(out.data(), out.size());
+              }
+            }
+          } catch (std::exception& e) { kind = "Internal"; msg = e.what(); }
+          {
+            std::lock_guard<std::mutex> lk(mu);
+            o.kind = kind; o.msg = msg; o.load_error = load_error;
+            o.state = kind.empty() ? 1 : 2;
+          }
+          cv.notify_all();
+          if (!kind.empty()) return;
+        }
+      });
+    }
+    struct JoinAll {
+      std::vector<std::thread>& v; std::mutex& mu; std::condition_variable& cv; bool& stop;
+      ~JoinAll() { { std::lock_guard<std::mutex> lk(mu); stop = true; } cv.notify_all(); for (auto& t : v) if (t.joinable()) t.join(); }
+    } join{pipes, mu, cv, stop};
+    char* stage = (char*)pinned_get(DeviceBufs::kPinnedBytes, devs[0]);
+    if (!stage) throw std::runtime_error("pinned host staging: allocation failed");
+    struct StageFree { char* p; int d; ~StageFree() { pinned_put(p, DeviceBufs::kPinnedBytes, d); } } stage_free{stage, devs[0]};
+    CallbackSink sink(write, ctx, stage, DeviceBufs::kPinnedBytes);
+    auto wait_chunk = [&](size_t k) -> Out& {
+      Out& o = *outs[k];
+      std::unique_lock<std::mutex> lk(mu);
+      cv.wait(lk, [&] { return o.state != 0; });
+      return o;
+    };
+    // chunk k failed: a document after it that does not load takes precedence (unless k's error is one)
+    auto fail_chunk = [&](size_t k, Out& o) {
+      if (!o.load_error) {
+        std::string lk, lm;
+        if (o.kind != "Internal" && first_load_error(docs, std::min(n_docs, (k + 1) * chunk), n_docs, lk, lm))
+          return fail(ffi_code(lk), error_display(lk, lm));
+      }
+      return fail(ffi_code(o.kind), error_display(o.kind, o.msg));
+    };
+    int32_t parse_code = 0;
+    bool anyfail = false;
+    if (!n_docs) {
+      // no documents: the format's empty report (exit 5 when a rules file does not parse)
+      gg_session rs;
+      for (size_t i = 0; i < n_rules; i++) {
+        std::string perr;
+        if (!add_rules(&rs, rules[i].content ? rules[i].content : "", rules[i].file_name ? rules[i].file_name : "", perr))
+          rs.parse_errors.push_back(perr);
+      }
+      std::string out;
+      int32_t code = 0;
+      ReportError re;
+      if (!session_report(&rs, out, code, re, fmt)) return fail(ffi_code(re.kind), error_display(re.kind, re.msg));
+      sink.write(out.data(), out.size());
+      if (sink.failed) return fail(-1, "the write callback failed");
+      if (exit_code) *exit_code = code;
+      return 0;
+    }
+    if (!hold) {
+      for (size_t k = 0; k < nchunks; k++) {
+        Out& o = wait_chunk(k);
+        if (o.state == 2) return fail_chunk(k, o);
+        if (k == 0) { parse_code = o.parse_code; if (fmt == OUT_JSON) sink.write("[\n", 2); }
+        anyfail = anyfail || o.anyfail;
+        for (auto& b : o.text.blocks) {
+          if (!sink.failed && b.second && write(ctx, b.first, b.second) != 0) sink.failed = true;
+          pool.put(b.first);
+        }
+        o.text.blocks.clear();
+        sink.n += o.text.n;
+        if (sink.failed) return fail(-1, "the write callback failed");
+        {
+          std::lock_guard<std::mutex> lk(mu);
+          written = k + 1;
+        }
+        cv.notify_all();
+      }
+      if (fmt == OUT_JSON) sink.write("\n]", 2);
+    } else {
+      // every chunk evaluated (or the first failure, in order) before a byte is written
+      for (size_t k = 0; k < nchunks; k++) {
+        Out& o = wait_chunk(k);
+        if (o.state == 2) return fail_chunk(k, o);
+        anyfail = anyfail || o.anyfail;
+      }
+      parse_code = outs[0]->parse_code;
+      if (fmt == OUT_SARIF) {
+        // SarifReport::new (sarif.rs:29-53, 185-203): the FAILed documents' first-seen non-empty names
+        std::vector<std::string> art;
+        std::unordered_set<std::string> seen;
+        for (auto& op : outs) {
+          gg_session* s = op->ses.get();
+          const size_t nf = s->progs.size();
+          for (size_t d = 0; d < s->docs.ndocs(); d++) {
+            uint32_t status = ST_SKIP;
+            for (size_t f = 0; f < nf; f++) {
+              const uint32_t st = s->tiles[d * nf + f].status;   // Status::and (rules/mod.rs:122-133)
+              if (status == ST_FAIL) continue;
+              status = status == ST_PASS ? (st == ST_FAIL ? ST_FAIL : ST_PASS) : st;
+            }
+            if (status != ST_FAIL) continue;
+            const std::string& name = s->docs.names[d];
+            if (!name.empty() && seen.insert(name).second) art.push_back(name);
+          }
+        }
+        std::string head, tail;
+        sarif_frame(art, head, tail);
+        sink.write(head.data(), head.size());
+        // the results' first comma is dropped ("[\n        {" as serde's pretty printer writes it)
+        struct DropFirst : ReportSink {
+          ReportSink& in;
+          char* last = nullptr;
+          uint64_t n = 0;
+          explicit DropFirst(ReportSink& s) : in(s) {}
+          char* reserve(size_t k) override { return last = in.reserve(k); }
+          void commit(size_t k) override {
+            if (!k) return;
+            if (n == 0) { memmove(last, last + 1, k - 1); in.commit(k - 1); }
+            else in.commit(k);
+            n += k;
+          }
+          size_t max_piece() const override { return in.max_piece(); }
+          bool pinned() const override { return in.pinned(); }
+        } results(sink);
+        for (auto& op : outs) {
+          gg_session* s = op->ses.get();
+          ReportError re;
+          if (!s->progs.empty()) {
+            if (device_report_on(s) && s->fetched_on_device) {
+              if (!device_report_text(s, 0, s->docs.ndocs(), SIZE_MAX, results, re, nullptr, OUT_SARIF, kStreamPushBlocks))
+                return fail(ffi_code(re.kind), error_display(re.kind, re.msg));
+            } else {
+              ensure_host_arena(s);
+              std::vector<const Program*> progs;
+              for (auto& p : s->progs) progs.push_back(&p->prog);
+              const size_t nf = progs.size();
+              for (size_t d = 0; d < s->docs.ndocs(); d++) {
+                std::vector<TileResult> trs(nf);
+                std::vector<const TileResult*> tp(nf);
+                for (size_t f = 0; f < nf; f++) {
+                  trs[f] = tile_view(s->tiles.data(), s->rule_status.data(), s->max_top, s->recs.data(), d * nf + f);
+                  tp[f] = &trs[f];
+                }
+                std::string t;
+                if (!sarif_doc_results(s->docs, (uint32_t)d, progs, tp, t, re)) return fail(ffi_code(re.kind), error_display(re.kind, re.msg));
+                results.write(t.data(), t.size());
+              }
+            }
+          }
+          if (sink.failed) return fail(-1, "the write callback failed");
+          op->ses.reset();
+        }
+        if (results.n) sink.write("\n      ", 7);
+        sink.write(tail.data(), tail.size());
+      } else {
+        // JunitReporter (xml.rs:14-80): the totals -- one test per (data file, rules file), a failure per FAILed
+        // one -- then every chunk's test suites (its own report without the frame)
+        size_t tests = 0, failures = 0;
+        for (auto& op : outs) {
+          gg_session* s = op->ses.get();
+          const size_t nf = s->progs.size();
+          tests += s->docs.ndocs() * nf;
+          for (size_t t = 0; t < s->docs.ndocs() * nf; t++) failures += s->tiles[t].status == ST_FAIL;
+        }
+        const std::string head = "<?xml version=\"1.0\" encoding=\"UTF-8\"?>\n<testsuites name=\"cfn-guard validate report\" tests=\"" +
+                                 std::to_string(tests) + "\" failures=\"" + std::to_string(failures) + "\" errors=\"0\" time=\"0\">\n";
+        static const char kTail[] = "</testsuites>\n";
+        sink.write(head.data(), head.size());
+        for (auto& op : outs) {
+          std::string out;
+          int32_t code = 0;
+          ReportError re;
+          if (!session_report(op->ses.get(), out, code, re, OUT_JUNIT)) return fail(ffi_code(re.kind), error_display(re.kind, re.msg));
+          size_t a = out.find('\n');
+          a = a == std::string::npos ? out.size() : out.find('\n', a + 1);
+          a = a == std::string::npos ? out.size() : a + 1;
+          const size_t tl = sizeof(kTail) - 1;
+          const size_t b = out.size() >= a + tl && out.compare(out.size() - tl, tl, kTail) == 0 ? out.size() - tl : out.size();
+          if (b > a) sink.write(out.data() + a, b - a);
+          if (sink.failed) return fail(-1, "the write callback failed");
+          op->ses.reset();
+        }
+        sink.write(kTail, sizeof(kTail) - 1);
+      }
+    }
+    if (sink.failed) return fail(-1, "the write callback failed");
+    // exit code 19 on a FAIL; JUnit keeps 5 over 19 (reporters/mod.rs:97-103)
+    int32_t code = parse_code;
+    if (anyfail && !(fmt == OUT_JUNIT && parse_code == 5)) code = 19;
+    if (exit_code) *exit_code = code;
+    return 0;
+  } catch (std::exception& e) {
+    return fail(-1, e.what());
+  }
+}
+}  // namespace
+
+int32_t cfn_guard_validate_batch_stream_ex(const validate_input_t* docs, size_t n_docs, const validate_input_t* rules,
+                                           size_t n_rules, const validate_input_t* params, size_t n_params,
+                                           int32_t output_format, size_t chunk_docs, const int32_t* devices, size_t n_devices,
+                                           cfn_guard_write_fn write, void* ctx, int32_t* exit_code, extern_err_t* err) {
+  set_err(err, 0, "");
+  if (exit_code) *exit_code = 0;
+  auto fail = [&](int32_t code, const std::string& msg) { set_err(err, code, msg); if (exit_code) *exit_code = -1; return -1; };
+  if (!write) return fail(18, "IllegalArguments: no write callback");
+  if (output_format < OUT_JSON || output_format > OUT_JUNIT) return fail(18, "IllegalArguments: unknown output format");
+  try {
+    std::string why;
+    std::vector<int> devs;
+    if (devices) {
+      for (size_t i = 0; i < n_devices; i++) devs.push_back(devices[i]);
+      if (devs.empty()) return fail(-1, "IllegalArguments: an empty device list");
+      for (int d : devs)
+        if (!ensure_device(why, d)) return fail(-1, why);
+    } else {
+      int d = 0;
+      if (!ensure_device(why, -1, &d)) return fail(-1, why);
+      devs.push_back(d);
+    }
+    if (output_format == OUT_JSON && !n_params) {
+      if (devs.size() == 1) return stream_single(devs[0], docs, n_docs, rules, n_rules, chunk_docs, write, ctx, exit_code, err);
+      return cfn_guard_validate_batch_stream_devices(docs, n_docs, rules, n_rules, chunk_docs, devs.data(), devs.size(), write, ctx,
+                                                     exit_code, err);
+    }
+    return stream_format(devs, docs, n_docs, rules, n_rules, params, n_params, output_format, chunk_docs, write, ctx, exit_code, err);
   } catch (std::exception& e) {
     return fail(-1, e.what());
   }
@@ -3818,6 +4248,8 @@ int64_t gg_session_stat(gg_session* s, int32_t what) {
     }
     case 20: return (int64_t)s->mode;   // 0 lane mode (+ wave retry), 1 wave mode
     case 21: return (int64_t)s->parse_errors.size();   // rules files that did not parse (exit code 5)
+    case 22: return (int64_t)s->lane_group;   // lanes per document of the lane kernel (1: one lane per tile)
+    case 23: return (int64_t)s->lane_docs;    // documents per lane batch
     default: return -1;
   }
 }

@@ -335,6 +335,44 @@ struct Compiler {
     return (cid + 1) | 0x80000000u;
   }
 
+  // A filter conjunction that reads only the value it tests: access clauses over navigation steps (keys,
+  // indices, unnamed `*` / `[*]`, nested filters of the same kind) against literals or such queries -- no
+  // `%var` (lets are evaluated lazily and cached), rule references, functions, captures or map-key filters.
+  // Its evaluation for one value has no effect beyond its status (records are suppressed inside filters) and
+  // a possible error, so the lanes of a document's group may test a list's values at once (PPart.c bit 30,
+  // eval_recursive.inc coop_chunk).
+  bool coop_query(uint32_t qid, int depth) const {
+    if (depth > 16) return false;
+    const PQuery& q = queries[qid];
+    for (uint32_t i = 0; i < q.n; i++) {
+      const PPart& pp = parts[q.first + i];
+      const bool nav = pp.kind == P_THIS || pp.kind == P_KEY || pp.kind == P_KEY_INDEX || pp.kind == P_INDEX ||
+                       ((pp.kind == P_ALL_VALUES || pp.kind == P_ALL_INDICES) && pp.a == NONE);
+      if (nav) continue;
+      if (pp.kind == P_FILTER && pp.b == NONE && coop_conj(pp.a, depth + 1)) continue;
+      return false;
+    }
+    return true;
+  }
+  bool coop_conj(uint32_t cj, int depth) const {
+    if (depth > 16) return false;
+    const PRange2 C = conjs[cj];
+    for (uint32_t i = 0; i < C.n; i++) {
+      const PRange2 Di = disjs[disj_refs[C.first + i]];
+      for (uint32_t j = 0; j < Di.n; j++) {
+        const PClause& pc = clauses[clause_refs[Di.first + j]];
+        if (pc.kind != C_ACCESS) return false;
+        const uint32_t op = pc.flags & 15u, rk = (pc.flags >> 8) & 15u;
+        if (op < OP_EXISTS) {
+          if (rk == RHS_QUERY) { if (!coop_query(pc.b, depth + 1)) return false; }
+          else if (rk != RHS_LITERAL) return false;
+        }
+        if (!coop_query(pc.a, depth + 1)) return false;
+      }
+    }
+    return true;
+  }
+
   uint32_t query(const AccessQuery& q) {
     uint32_t qid = (uint32_t)queries.size();
     queries.push_back(PQuery{0, 0, q.match_all ? 1u : 0u, 0});
@@ -625,7 +663,10 @@ struct Compiler {
     for (size_t q = 0; q < queries.size(); q++)
       for (uint32_t i = 0; i < queries[q].n; i++) {
         PPart& pp = parts[queries[q].first + i];
-        if (pp.kind == P_FILTER) pp.c = fast_filter_clause(pp.a, query_block[q]);
+        if (pp.kind == P_FILTER) {
+          pp.c = fast_filter_clause(pp.a, query_block[q]);
+          if (pp.b == NONE && coop_conj(pp.a, 0)) pp.c |= 1u << 30;   // eval_core.inc COOP_FILTER
+        }
       }
     mark_root_vars();
     std::vector<uint32_t> blob(sizeof(ProgHeader) / 4 + 2, 0);

@@ -95,6 +95,8 @@ struct LaunchArgs {
   uint32_t rec_chunk;         // lane mode: record slots per lane reserved per batch (direct writes; 0: off)
   uint32_t lane_recs_bytes;   // lane mode: record staging bytes per lane (a multiple of 48; after the 4 KB frames)
   uint32_t lane_docs;         // lane mode: documents per batch (lanes 0 .. lane_docs-1 of a wave; 64 or fewer)
+  uint32_t lane_group;        // lane mode: lanes per document (1, or 64 / lane_docs: a document's lanes run its
+                              // tile in step and split its list fan-outs' filter tests, eval_core.inc coop_chunk)
   uint32_t stack_guard;       // lane-stack bytes past which a recursion step ends the tile with E_STACK
                               // (capi.cpp: the device's stack limit minus the deepest uncheck-ed call chain)
   unsigned long long* stats;   // stats build variant: [0,8) counters, [8] tiles, [9,18) cycles per category

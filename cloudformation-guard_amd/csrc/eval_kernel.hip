@@ -157,6 +157,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
   // a batch is lane_docs consecutive documents (64, or fewer for launches of few large documents: fewer
   // lanes of a wave diverge, and more waves share the CUs)
   const uint32_t L = A.lane_docs ? A.lane_docs : 64u;
+  // lanes per document: 1, or 64 / L -- the lanes of a document run its tile in step (identical state, one
+  // writer) and split its list fan-outs' filter tests (eval_recursive.inc coop_chunk)
+  const uint32_t G = A.lane_group ? A.lane_group : 1u;
+  const bool leader = (lane & (G - 1u)) == 0u;
   const uint32_t nchunks = (A.docs.ndocs + L - 1u) / L;
   const uint32_t xcd = blockIdx.x & 7u;
   const uint32_t c0 = (uint32_t)(((uint64_t)nchunks * xcd) / 8u), c1 = (uint32_t)(((uint64_t)nchunks * (xcd + 1u)) / 8u);
@@ -169,6 +173,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
     g_wave.heap = heap; g_wave.nodes = A.docs.nodes; g_wave.klen = A.docs.klen; g_wave.db = A.docs.bytes;
     g_wave.tix = A.docs.tix; g_wave.fcap = FRAMES_BYTES; g_wave.rcap = A.lane_recs_bytes; g_wave.type_key = A.docs.type_key;
     g_wave.recs = A.recs; g_wave.rchunk = A.rec_chunk; g_wave.sguard = A.stack_guard;
+    g_wave.rstride = L; g_wave.group = G;
   }
   __syncthreads();
   uint32_t staged = NONE;
@@ -194,8 +199,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
     if (b >= nbatches) break;
     const uint32_t file = b % A.nfiles, chunk = c0 + b / A.nfiles;
 #endif
-    const uint32_t pos = chunk * L + lane;
-    const bool active = lane < L && pos < A.docs.ndocs;
+    const uint32_t pos = chunk * L + lane / G;
+    const bool active = lane / G < L && pos < A.docs.ndocs;
     const uint32_t doc = (A.order && active) ? A.order[pos] : pos;
     if (file != staged) { P = stage_program(&A.progs[file], &g_prog, s_blob, A.lds_prog_words); staged = file; }
     const uint32_t tile = doc * A.nfiles + file;
@@ -203,19 +208,21 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
     if (P != &g_prog) {
       // the program did not fit the LDS window: lane mode reads it through LDS-typed pointers only,
       // so the whole batch goes to the wave kernel
-      if (active) A.retry_list[atomicAdd(A.retry_count, 1u)] = tile;
+      if (active && leader) A.retry_list[atomicAdd(A.retry_count, 1u)] = tile;
       continue;
     }
-    // the batch's direct record chunk: 64 lanes x rec_chunk slots, one atomic per wave (eval_core.inc
-    // rec_store); a reservation past the arena leaves the lanes without a chunk (their tiles then fail
-    // with E_RECORDS if they record anything, and the host re-runs with a larger arena)
+    // the batch's direct record chunk: L documents x rec_chunk slots (slot i of document d at base + L i + d),
+    // one atomic per wave (eval_core.inc rec_store); a reservation past the arena leaves the lanes without a
+    // chunk (their tiles then fail with E_RECORDS if they record anything, and the host re-runs with a larger
+    // arena)
     uint32_t rbase = NONE;
     if (A.rec_chunk) {
-      if (lane == 0) rbase = atomicAdd(A.rec_cursor, 64u * A.rec_chunk);
+      if (lane == 0) rbase = atomicAdd(A.rec_cursor, L * A.rec_chunk);
       rbase = __shfl(rbase, 0);
-      if ((uint64_t)rbase + 64ull * A.rec_chunk > A.rec_cap) rbase = NONE;
+      if ((uint64_t)rbase + (uint64_t)L * A.rec_chunk > A.rec_cap) rbase = NONE;
     }
-    c.rbase = rbase == NONE ? NONE : rbase + lane;
+    c.rbase = rbase == NONE ? NONE : rbase + lane / G;
+    c.mute = leader ? 0u : 1u;
     if (active) {
       tile_begin<true>(c, A, P, doc, heap, A.lane_heap_bytes, FRAMES_BYTES, A.lane_recs_bytes);
       c.syn_off = alloc_pers(c, 256 * 16);
@@ -230,19 +237,19 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
       for (uint32_t r = 0; r < P->n_top && !c.err; r++) {
         uint32_t st = run_rule(c, P->top_first + r);
         if (c.err) break;
-        rs[r] = (uint8_t)st;
+        if (leader) rs[r] = (uint8_t)st;
         if (st == ST_PASS) passes++; else if (st == ST_FAIL) fails++;
       }
       status = fails ? ST_FAIL : (passes ? ST_PASS : ST_SKIP);
       n = c.err ? 0 : c.nrec + c.naux;
       // records written into a chunk the arena could not hold: the tile is re-run after the host grows it
       if (n && A.rec_chunk && c.rbase == NONE) { c.err = E_RECORDS; n = 0; }
-      tile_stats(c, A);
+      if (leader) tile_stats(c, A);
     }
     // a tile whose records fit its chunk is published in place; the others (overflow, or no chunks) get a
     // contiguous range: wave-aggregated allocation, one atomic per wave
     const bool in_chunk = active && A.rec_chunk && c.rbase != NONE && n <= A.rec_chunk;
-    const uint32_t need = in_chunk ? 0u : n;
+    const uint32_t need = (in_chunk || !leader) ? 0u : n;
     uint32_t incl = need;
     for (uint32_t d = 1; d < 64; d <<= 1) {
       uint32_t v = __shfl_up(incl, d);
@@ -252,7 +259,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
     uint32_t base = 0;
     if (lane == 0 && total) base = atomicAdd(A.rec_cursor, total);
     base = __shfl(base, 0);
-    if (active) {
+    if (active && leader) {
       uint32_t off = base + incl - need;
       bool retry = c.err == E_HEAP || c.err == E_RECORDS || c.err == E_DEPTH;   // not E_STACK: wave frames are larger
       if (retry) A.retry_list[atomicAdd(A.retry_count, 1u)] = tile;
@@ -264,14 +271,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
       if (in_chunk && n) {
         // side records follow the tile's records in its chunk
         for (uint32_t i = 0; i < naux; i++) rec_store(c, nrec + i, stage_load(c, rec_slots(c) - 1 - i));
-        o.rec_off = c.rbase; o.pad1 = 1;   // slot k at rec_off + 64 k (session_fetch compacts)
+        o.rec_off = c.rbase; o.pad1 = L;   // slot k at rec_off + L k (session_fetch compacts)
       } else {
 #if GG_AB_NOREC != 1 && GG_AB_NOREC != 3   // diagnostic A/B only (2: staging off; 3: copy-out off)
         for (uint32_t i = 0; i < nrec; i++) A.recs[off + i] = rec_load(c, i);
 #endif
         for (uint32_t i = 0; i < naux; i++)
           A.recs[off + nrec + i] = stage_load(c, rec_slots(c) - 1 - i);
-        o.rec_off = n ? off : 0; o.pad1 = 0;
+        o.rec_off = n ? off : 0; o.pad1 = 1;   // contiguous
       }
       A.tiles[tile] = o;
     }
@@ -382,7 +389,7 @@ __global__ void __launch_bounds__(256) rule_count_kernel(const TileOut* tiles, c
 }
 
 // Record compaction (session_fetch, outside the evaluation): every tile's records -- in place in its
-// lane's direct chunk (TileOut.pad1 == 1: record k at rec_off + 64 k) or contiguous (pad1 == 0) -- are
+// lane's direct chunk (TileOut.pad1 = stride s > 1: record k at rec_off + s k) or contiguous (pad1 0 / 1) -- are
 // copied to dst[dense_off[t] ..), dense_off an exclusive scan of the tiles' record counts (rec_n + pad0),
 // so the host receives one dense array in tile order.  Three passes: per-block sums, a one-block scan of
 // the block sums, then per-block scan + copy.  The evaluation's buffers are only read (idempotent).
@@ -444,7 +451,7 @@ __global__ void __launch_bounds__(256) rec_compact_kernel(const TileOut* tiles, 
     if (i >= n) break;
     dense_off[i] = off;
     const TileOut t = tiles[i];
-    const uint32_t stride = t.pad1 == 1 ? 64u : 1u;
+    const uint32_t stride = t.pad1 > 1u ? t.pad1 : 1u;
     for (uint32_t r = 0; r < c[k]; r++) dst[off + r] = src[t.rec_off + (size_t)r * stride];
     off += c[k];
   }

@@ -484,7 +484,7 @@ RN void nc_reason(W& w, const Ctx& c, const Rec& rc) {
 // ------------------------------------------------------------------------------- records ---
 // one tile's ClauseReports (StreamWalker::items over its records), into the open not_compliant array
 // A tile's records as the evaluation left them: contiguous (stride 1), or in place in its lane's direct
-// record chunk (TileOut.pad1 == 1: record k at rec_off + 64 k, eval_kernel.hip) -- read where they are,
+// record chunk (TileOut.pad1 = stride s > 1: record k at rec_off + s k, eval_kernel.hip) -- read where they are,
 // so no compaction pass runs between the evaluation and the report
 struct RecSeq {
   const Rec* p;
@@ -928,7 +928,7 @@ RN void file_sarif(W& w, const RenderArgs& A, uint32_t doc) {
     const size_t t = (size_t)doc * nf + f;
     const TileOut to = A.tiles[t];
     Ctx c{&A, &A.progs[f], A.base[doc]};
-    tile_sarif(w, c, RecSeq{A.recs + to.rec_off, to.pad1 == 1 ? 64u : 1u}, to.rec_n, uri, urin);
+    tile_sarif(w, c, RecSeq{A.recs + to.rec_off, to.pad1 > 1u ? to.pad1 : 1u}, to.rec_n, uri, urin);
   }
 }
 
@@ -957,7 +957,7 @@ RN void file_report(W& w, const RenderArgs& A, uint32_t doc) {
     const size_t t = (size_t)doc * nf + f;
     const TileOut to = A.tiles[t];
     Ctx c{&A, &A.progs[f], A.base[doc]};
-    tile_items(w, c, RecSeq{A.recs + to.rec_off, to.pad1 == 1 ? 64u : 1u}, to.rec_n);
+    tile_items(w, c, RecSeq{A.recs + to.rec_off, to.pad1 > 1u ? to.pad1 : 1u}, to.rec_n);
   }
   close(w, ']');
   // the distinct top-level rule names that SKIPped / PASSed in any file, sorted (std::set)

@@ -67,6 +67,14 @@ def lib():
                                                               ctypes.c_size_t, WRITE_FN, ctypes.c_void_p,
                                                               ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ExternError)]
         L.cfn_guard_validate_batch_stream_devices.restype = ctypes.c_int32
+    if hasattr(L, "cfn_guard_validate_batch_stream_ex"):   # (round 6: formats and -i on the streamed entries)
+        L.cfn_guard_validate_batch_stream_ex.argtypes = [ctypes.POINTER(ValidateInput), ctypes.c_size_t,
+                                                         ctypes.POINTER(ValidateInput), ctypes.c_size_t,
+                                                         ctypes.POINTER(ValidateInput), ctypes.c_size_t, ctypes.c_int32,
+                                                         ctypes.c_size_t, ctypes.POINTER(ctypes.c_int32), ctypes.c_size_t,
+                                                         WRITE_FN, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32),
+                                                         ctypes.POINTER(ExternError)]
+        L.cfn_guard_validate_batch_stream_ex.restype = ctypes.c_int32
     L.gg_synth_texts.argtypes = [ctypes.c_uint64, ctypes.c_size_t, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]
     L.gg_synth_texts.restype = ctypes.c_void_p
     L.gg_texts_inputs.argtypes = [ctypes.c_void_p]
@@ -348,7 +356,7 @@ WRITE_FN = ctypes.CFUNCTYPE(ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ct
 
 
 def validate_structured_stream(rules, data, write=None, chunk_docs=0, inputs=None, n_docs=None, count_only=False,
-                               devices=False):
+                               devices=False, output="json", params=None):
     """cfn_guard_validate_batch_stream: the JSON report of validate_structured streamed to write(bytes) in
     document order, the documents evaluated in chunks of chunk_docs (0: 262144) on two alternating sessions.
     Returns (text or None, exit_code): the text when write is None (collected), else None.  Raises GuardError on
@@ -357,7 +365,9 @@ def validate_structured_stream(rules, data, write=None, chunk_docs=0, inputs=Non
     library's pinned staging) and only its length is taken -- write(n) gets byte counts (measurement); "native":
     the library's counting callback (gg_count_write) takes them, write(total) is called once at the end.
     devices: a list of HIP ordinals (or None: every visible device) for cfn_guard_validate_batch_stream_devices --
-    chunk k on devices[k % len(devices)], the same bytes; False (default): the one-device entry."""
+    chunk k on devices[k % len(devices)], the same bytes; False (default): the one-device entry.
+    output ("json", "yaml", "sarif", "junit") / params ([(name, text)], validate -i): through
+    cfn_guard_validate_batch_stream_ex, the one-string call's bytes in every format."""
     R = (ValidateInput * max(1, len(rules)))(*[ValidateInput(_b(t), _b(n)) for n, t in rules])
     if inputs is None:
         inputs = (ValidateInput * max(1, len(data)))(*[ValidateInput(_b(t), _b(n)) for n, t in data])
@@ -381,7 +391,15 @@ def validate_structured_stream(rules, data, write=None, chunk_docs=0, inputs=Non
         cbf = WRITE_FN(cb)
     code = ctypes.c_int32(0)
     err = ExternError()
-    if devices is False:
+    if output != "json" or params:
+        P = (ValidateInput * max(1, len(params or [])))(*[ValidateInput(_b(t), _b(n)) for n, t in (params or [])])
+        if devices is None:
+            devices = list(range(lib().gg_device_available()))
+        dv = (ctypes.c_int32 * max(1, len(devices or [])))(*(devices or []))
+        lib().cfn_guard_validate_batch_stream_ex(inputs, n_docs, R, len(rules), P, len(params or []), OUTPUT_FORMATS[output],
+                                                 chunk_docs, dv if devices else None, len(devices or []), cbf, ctx,
+                                                 ctypes.byref(code), ctypes.byref(err))
+    elif devices is False:
         lib().cfn_guard_validate_batch_stream(inputs, n_docs, R, len(rules), chunk_docs, cbf, ctx, ctypes.byref(code),
                                               ctypes.byref(err))
     else:
@@ -768,7 +786,7 @@ class Session:
     STAT = {"ndocs": 0, "nfiles": 1, "nodes": 2, "bytes": 3, "fail": 4, "pass": 5, "skip": 6, "errors": 7,
             "records": 8, "arena_bytes": 9, "first_error": 10, "record_bytes": 11, "record_cap": 12,
             "max_top": 13, "slots": 14, "heap_bytes": 15, "retried": 16, "lane_slots": 17, "mode": 20,
-            "parse_errors": 21}
+            "parse_errors": 21, "lane_group": 22, "lane_docs": 23}
 
     def exit_code(self, output="json"):
         """the structured run's exit code over the evaluated documents, as the report would set it:

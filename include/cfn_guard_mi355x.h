@@ -101,6 +101,23 @@ int32_t cfn_guard_validate_batch_stream_devices(const validate_input_t *docs, si
                                                 const validate_input_t *rules, size_t n_rules, size_t chunk_docs,
                                                 const int32_t *devices, size_t n_devices, cfn_guard_write_fn write,
                                                 void *ctx, int32_t *exit_code, extern_err_t *err);
+/* The streamed entries with the one-string call's whole structured contract (cfn_guard_validate_batch_params /
+ * _devices: `validate --structured -o json|yaml|sarif|junit [-i <params>]*`, structured.rs:99-133,
+ * validate.rs:317-350): output_format CFN_GUARD_OUTPUT_* (JSON, YAML, SARIF, JUNIT), params merged into every
+ * data file, chunks of chunk_docs documents (0: 262144 on one device, 16384 per chunk over several) on
+ * devices[k % n_devices] (NULL: the process default device).  The bytes `write` receives are the one-string
+ * call's, in document order.  JSON and YAML write each chunk while later ones run (two chunks' reports per
+ * device in host memory); SARIF and JUnit put their frame -- the FAILed documents' artifacts, the test totals --
+ * before every result, so they keep every chunk's evaluated results on its device until the last chunk is
+ * evaluated (about 20 GB of HBM per million CloudFormation templates, no report text), then write.  Errors follow
+ * the one-string call's precedence; JSON / YAML may have written the chunks before the failing one (a prefix to
+ * drop), SARIF / JUnit write nothing before an error.  JSON without params is cfn_guard_validate_batch_stream
+ * (one device) / _stream_devices. */
+int32_t cfn_guard_validate_batch_stream_ex(const validate_input_t *docs, size_t n_docs, const validate_input_t *rules,
+                                           size_t n_rules, const validate_input_t *params, size_t n_params,
+                                           int32_t output_format, size_t chunk_docs, const int32_t *devices,
+                                           size_t n_devices, cfn_guard_write_fn write, void *ctx, int32_t *exit_code,
+                                           extern_err_t *err);
 /* synthetic corpora as validate inputs (bench.py): format 0 JSON (synth.cfn_doc), 1 block-style YAML */
 typedef struct gg_texts gg_texts;
 gg_texts *gg_synth_texts(uint64_t first, size_t n, int32_t n_resources, int32_t format, int32_t nthreads);

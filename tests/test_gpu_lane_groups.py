@@ -1,0 +1,109 @@
+"""Lane groups: G lanes per document run its tile in step and split every chunk
+of its filtered list fan-outs -- the reference's per-element Filter (eval_context.rs:723-828) and
+check_and_delegate over map values (:268-313) -- merging the verdicts with shuffles (eval_recursive.inc
+coop_chunk).  Whatever G, the bytes equal the oracle's and the one-lane-per-tile kernel's; an error raised
+inside a cooperatively tested filter surfaces as the reference raises it."""
+import json
+import os
+
+import pytest
+
+import guard_amd
+import synth
+from guard_oracle import validate_structured as oracle_validate
+from rulepack import rule_pack
+
+pytestmark = pytest.mark.gpu
+
+
+def _report(rules, docs, group, prefix="g", output="json"):
+    old = os.environ.get("GG_LANE_GROUP")
+    if group is None:
+        os.environ.pop("GG_LANE_GROUP", None)
+    else:
+        os.environ["GG_LANE_GROUP"] = str(group)
+    try:
+        s = guard_amd.Session()
+        try:
+            for name, text in rules:
+                s.add_rules(text, name)
+            s.add_docs(docs, ["%s-%d.json" % (prefix, i) for i in range(len(docs))])
+            s.eval(1)
+            g = s.stat(s.STAT["lane_group"])
+            return s.report(output), g
+        finally:
+            s.close()
+    finally:
+        if old is None:
+            os.environ.pop("GG_LANE_GROUP", None)
+        else:
+            os.environ["GG_LANE_GROUP"] = old
+
+
+@pytest.mark.parametrize("group", [2, 16, 64])
+def test_terraform_plans_every_group_size_vs_oracle(group):
+    rules = rule_pack("cfg4")
+    docs = synth.tf_corpus(9, start=300, n_resources=150) + synth.tf_corpus(2, start=900, n_resources=700)
+    data = [("g-%d.json" % i, d) for i, d in enumerate(docs)]
+    exp, ecode, _ = oracle_validate(rules, data)
+    (out, code), g = _report(rules, docs, group)
+    assert g == group
+    assert (out, code) == (exp, ecode)
+
+
+def test_full_size_plans_pick_lane_groups():
+    """a launch of few large plans selects lane groups by itself (capi.cpp session_upload)"""
+    rules = rule_pack("cfg4")
+    docs = synth.tf_corpus(3, start=40, n_resources=2000)
+    data = [("g-%d.json" % i, d) for i, d in enumerate(docs)]
+    exp, ecode, _ = oracle_validate(rules, data)
+    (out, code), g = _report(rules, docs, None)
+    assert g > 1
+    assert (out, code) == (exp, ecode)
+    assert _report(rules, docs, 1)[0] == (exp, ecode)
+
+
+@pytest.mark.parametrize("group", [4, 32])
+def test_cfn_templates_in_lane_groups(group):
+    """groups on CloudFormation templates (map fan-outs, type blocks, fast filters) and the cfg3 pack"""
+    for pack, docs in (("cfg2", synth.cfn_corpus(40, start=11, n_resources=20)),
+                       ("cfg3", synth.cfn_corpus(20, start=77, n_resources=30))):
+        rules = rule_pack(pack)
+        base, _ = _report(rules, docs, 1)
+        (out, code), g = _report(rules, docs, group)
+        assert g == group
+        assert (out, code) == base, pack
+
+
+def test_formats_in_lane_groups():
+    rules = rule_pack("cfg4")
+    docs = synth.tf_corpus(4, start=5, n_resources=90)
+    for fmt in ("yaml", "sarif", "junit"):
+        assert _report(rules, docs, 8, output=fmt)[0] == _report(rules, docs, 1, output=fmt)[0], fmt
+
+
+RAISING = """let picked = items[ size empty ]
+rule r when %picked !empty {
+    %picked.name exists
+}
+"""
+
+
+def test_error_inside_a_cooperative_filter():
+    """`empty` on an integer raises inside the filter (eval.rs:251-262): the chunk goes back to the
+    sequential tests, which raise the reference's error for the first such element in order"""
+    items = [{"name": "a%d" % k, "size": ([] if k % 5 else "s")} for k in range(150)]
+    items[97]["size"] = 7   # the first element whose test raises
+    items[140]["size"] = 9
+    doc = json.dumps({"items": items})
+    rules = [("raise.guard", RAISING)]
+    data = [("g-0.json", doc)]
+    try:
+        oracle_validate(rules, data, raise_errors=True)
+        raise AssertionError("the oracle did not abort")
+    except Exception as e:   # guard_oracle.GuardError
+        want = getattr(e, "display", lambda: str(e))()
+    for group in (1, 16, 64):
+        with pytest.raises(guard_amd.GuardError) as g:
+            _report(rules, [doc], group)
+        assert g.value.message == want, group

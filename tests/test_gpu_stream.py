@@ -163,3 +163,64 @@ def test_stream_devices_errors_and_empty():
         guard_amd.validate_structured_stream(rule_pack("cfg2"), data, write=write, chunk_docs=5, devices=[0, 0])
     with pytest.raises(guard_amd.GuardError):
         guard_amd.validate_structured_stream(rules, data, chunk_docs=5, devices=[])
+
+
+# ---- round 6: cfn_guard_validate_batch_stream_ex -- every structured format and -i on the streamed entries
+def _mixed_corpus(n_json, n_yaml, start):
+    docs = synth.cfn_corpus(n_json, start=start, n_resources=8) + synth.cfn_yaml_corpus(n_yaml, start=start + 3, n_resources=5)
+    return [("f%d.%s" % (i, "json" if i < n_json else "yaml"), d) for i, d in enumerate(docs)]
+
+
+@pytest.mark.parametrize("output", ["yaml", "sarif", "junit", "json"])
+@pytest.mark.parametrize("chunk", [1, 9, 0])
+def test_stream_every_format_equals_one_string_and_oracle(output, chunk):
+    rules = rule_pack("cfg2")
+    data = _mixed_corpus(50, 14, 120)
+    one = guard_amd.validate_structured(rules, data, output=output)
+    params = [("p.yaml", "Extra:\n  Note: x\n")] if output == "json" else None   # json: the -i path of the entry
+    if params:
+        one = guard_amd.validate_structured(rules, data, output=output, params=params)
+    got = guard_amd.validate_structured_stream(rules, data, chunk_docs=chunk, output=output, params=params)
+    assert got == one
+    exp, ecode, _ = oracle_validate(rules, data, output=output, params=params)
+    assert got == (exp, ecode)
+
+
+@pytest.mark.parametrize("output", ["yaml", "sarif", "junit"])
+def test_stream_formats_with_params_and_device_list(output):
+    rules = rule_pack("cfg2") + [("p.guard", "rule uses_param { Extra.Note == 'x' }")]
+    data = _mixed_corpus(30, 6, 7)
+    params = [("p1.yaml", "Extra:\n  Note: x\n"), ("p2.json", '{"Other": 1}')]
+    one = guard_amd.validate_structured(rules, data, output=output, params=params)
+    assert guard_amd.validate_structured_stream(rules, data, chunk_docs=8, output=output, params=params) == one
+    assert guard_amd.validate_structured_stream(rules, data, chunk_docs=5, output=output, params=params, devices=[0, 0]) == one
+
+
+@pytest.mark.parametrize("output", ["yaml", "sarif", "junit", "json"])
+def test_stream_formats_empty_parse_error_and_errors(output):
+    rules = rule_pack("cfg2") + [("broken.guard", "rule r { Resources.*.Properties.X == }")]
+    assert guard_amd.validate_structured_stream(rules, [], chunk_docs=4, output=output) == \
+        guard_amd.validate_structured(rules, [], output=output)
+    data = _mixed_corpus(20, 4, 55)
+    assert guard_amd.validate_structured_stream(rules, data, chunk_docs=6, output=output) == \
+        guard_amd.validate_structured(rules, data, output=output)
+    # an evaluation error in a later chunk and a load error after it: the one-string call's error (the load error)
+    bad_rules = [("t.guard", "rule r { Resources.*.Properties.Port empty }")]
+    docs = [d for _, d in _mixed_corpus(24, 0, 3)]
+    docs[9] = json.dumps({"Resources": {"b": {"Type": "AWS::S3::Bucket", "Properties": {"Port": 8080}}}})
+    docs[20] = '{"Resources": '   # does not load
+    bad = [("e%d.json" % i, d) for i, d in enumerate(docs)]
+    with pytest.raises(guard_amd.GuardError) as g1:
+        guard_amd.validate_structured(bad_rules, bad, output=output)
+    seen = []
+    with pytest.raises(guard_amd.GuardError) as g2:
+        guard_amd.validate_structured_stream(bad_rules, bad, write=seen.append, chunk_docs=5, output=output)
+    assert (g1.value.code, g1.value.message) == (g2.value.code, g2.value.message)
+    if output in ("sarif", "junit"):
+        assert not seen   # SARIF / JUnit write nothing before an error
+    # a parameter file that does not load, with every data file loading: the parameter error
+    with pytest.raises(guard_amd.GuardError) as g3:
+        guard_amd.validate_structured(rules, data, output=output, params=[("bad.yaml", "a: [")])
+    with pytest.raises(guard_amd.GuardError) as g4:
+        guard_amd.validate_structured_stream(rules, data, output=output, params=[("bad.yaml", "a: [")], chunk_docs=7)
+    assert (g3.value.code, g3.value.message) == (g4.value.code, g4.value.message)
