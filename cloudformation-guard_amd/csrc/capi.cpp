@@ -866,7 +866,8 @@ void session_launch(gg_session* s) {
   A.xcd_cursor = s->dv->d_counters.p + 16;
   A.lane_heaps = s->dv->d_lane_heaps.p; A.lane_heap_bytes = s->lane_heap_bytes; A.lane_recs_bytes = s->lane_recs_bytes;
   A.lane_docs = s->lane_docs;
-  A.lane_group = s->lane_group;
+  // bit 16: no split walks (GG_SPLIT_WALK=0, A/B)
+  A.lane_group = s->lane_group | ((getenv("GG_SPLIT_WALK") && atoi(getenv("GG_SPLIT_WALK")) == 0) ? (1u << 16) : 0u);
   A.stack_guard = dev_stack_guard(s->device);
   A.retry_list = s->mode == 1 ? nullptr : s->dv->d_retry.p;
   A.wave_frames_bytes = gg_session::kWaveFrames; A.wave_recs_bytes = gg_session::kWaveRecs;

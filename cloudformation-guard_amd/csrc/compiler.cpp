@@ -668,6 +668,19 @@ struct Compiler {
           if (pp.b == NONE && coop_conj(pp.a, 0)) pp.c |= 1u << 30;   // eval_core.inc COOP_FILTER
         }
       }
+    // PQuery.pad = 1: a walk of the query does nothing but produce results -- no named `*` / `[*]` / filter
+    // (captures into the root scope), no `%var` key, no map-key filter (its records join the clause's) -- so
+    // the lanes of a document's group may split its first fan-out (eval_recursive.inc split_merge)
+    for (size_t q = 0; q < queries.size(); q++) {
+      bool ok = true;
+      for (uint32_t i = 0; i < queries[q].n && ok; i++) {
+        const PPart& pp = parts[queries[q].first + i];
+        if ((pp.kind == P_ALL_VALUES || pp.kind == P_ALL_INDICES) && pp.a != NONE) ok = false;
+        if (pp.kind == P_FILTER && pp.b != NONE) ok = false;
+        if (pp.kind == P_KEY_VAR || pp.kind == P_MAP_KEY_FILTER) ok = false;
+      }
+      queries[q].pad = ok ? 1u : 0u;
+    }
     mark_root_vars();
     std::vector<uint32_t> blob(sizeof(ProgHeader) / 4 + 2, 0);
     ProgHeader& h = P.hdr;

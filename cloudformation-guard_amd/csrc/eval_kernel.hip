@@ -120,7 +120,7 @@ __device__ __attribute__((always_inline)) inline void tile_begin(CtxT& c, const 
   if constexpr (LANE) tile_ptrs_lane(c, A, doc);
   else tile_ptrs_wave(c, A, P, doc, heap, frames_bytes, recs_bytes);
   c.tmp = frames_bytes + recs_bytes; c.pers = heap_bytes; c.nframes = 0; c.nrec = 0;
-  c.err = 0; c.err_a = 0; c.err_b = 0; c.suppress = 0; c.rec_created = 0; c.depth = 0; c.nsyn = 0;
+  c.err = 0; c.err_a = 0; c.err_b = 0; c.suppress = 0; c.rec_created = 0; c.split = 0; c.nsyn = 0;
   c.ffok = NONE; c.naux = 0;
 #ifdef GG_STATS
   for (int i = 0; i < 8; i++) { c.st[i] = 0; c.tdep[i] = 0; }
@@ -159,7 +159,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
   const uint32_t L = A.lane_docs ? A.lane_docs : 64u;
   // lanes per document: 1, or 64 / L -- the lanes of a document run its tile in step (identical state, one
   // writer) and split its list fan-outs' filter tests (eval_recursive.inc coop_chunk)
-  const uint32_t G = A.lane_group ? A.lane_group : 1u;
+  const uint32_t G = (A.lane_group & 0xFFFFu) ? (A.lane_group & 0xFFFFu) : 1u;
   const bool leader = (lane & (G - 1u)) == 0u;
   const uint32_t nchunks = (A.docs.ndocs + L - 1u) / L;
   const uint32_t xcd = blockIdx.x & 7u;
@@ -173,7 +173,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GG_LANE
     g_wave.heap = heap; g_wave.nodes = A.docs.nodes; g_wave.klen = A.docs.klen; g_wave.db = A.docs.bytes;
     g_wave.tix = A.docs.tix; g_wave.fcap = FRAMES_BYTES; g_wave.rcap = A.lane_recs_bytes; g_wave.type_key = A.docs.type_key;
     g_wave.recs = A.recs; g_wave.rchunk = A.rec_chunk; g_wave.sguard = A.stack_guard;
-    g_wave.rstride = L; g_wave.group = G;
+    g_wave.rstride = L; g_wave.group = G; g_wave.split_on = (A.lane_group >> 16) ? 0u : 1u;
   }
   __syncthreads();
   uint32_t staged = NONE;
