@@ -789,7 +789,9 @@ void session_upload(gg_session* s) {
     if (s->lane_group > 1) {
       s->lane_heap_bytes = 256u << 10;
       s->lane_recs_bytes = 2048u * (uint32_t)sizeof(Rec);
-      const size_t cap = kGroupHeapBudget / ((size_t)64 * s->lane_heap_bytes) & ~(size_t)7;
+      size_t budget = kGroupHeapBudget;
+      if (const char* e = getenv("GG_GROUP_HEAP_GB")) budget = (size_t)std::max(1, atoi(e)) << 30;
+      const size_t cap = budget / ((size_t)64 * s->lane_heap_bytes) & ~(size_t)7;
       if (s->lane_slots > cap) s->lane_slots = (uint32_t)std::max<size_t>(cap, 8);
     } else if ((size_t)s->lane_slots * 64 * (256u << 10) <= kLaneHeapBudget) {
       s->lane_heap_bytes = 256u << 10;

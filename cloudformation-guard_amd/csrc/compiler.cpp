@@ -681,6 +681,12 @@ struct Compiler {
       }
       queries[q].pad = ok ? 1u : 0u;
     }
+    // PClause.c = 1 on a block clause whose block (no lets of its own) is such a conjunction: the evaluation of
+    // the block for one value reads only that value and produces only its records and status, so the lanes of a
+    // document's group may evaluate the values at once and merge their records in value order
+    // (eval_recursive.inc split_block)
+    for (auto& pc : clauses)
+      if (pc.kind == C_BLOCK && blocks[pc.b].nlets == 0 && coop_conj(blocks[pc.b].conj, 0)) pc.c = 1;
     mark_root_vars();
     std::vector<uint32_t> blob(sizeof(ProgHeader) / 4 + 2, 0);
     ProgHeader& h = P.hdr;

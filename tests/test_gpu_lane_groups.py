@@ -107,3 +107,84 @@ def test_error_inside_a_cooperative_filter():
         with pytest.raises(guard_amd.GuardError) as g:
             _report(rules, [doc], group)
         assert g.value.message == want, group
+
+
+BLOCKS = """rule values_block {
+    items[*] {
+        v == 1
+        w exists
+        tags[*] != 'bad'
+    }
+}
+rule filtered_block_or {
+    items[ kind == 'a' ] {
+        v == 1 or w == 2
+    }
+}
+rule missing_values_block {
+    Resources.*.Properties {
+        Name exists
+    }
+}
+rule nested_block {
+    items[*] {
+        tags[*] { this != 'bad' }
+    }
+}
+"""
+
+
+def _block_doc(n, seed):
+    r = seed
+    items, res = [], {}
+    for k in range(n):
+        r = (r * 1103515245 + 12345) & 0x7FFFFFFF
+        it = {"kind": "ab"[r % 2], "v": (r >> 3) % 2, "tags": ["ok", "bad"][: 1 + (r >> 5) % 2]}
+        if (r >> 7) % 3:
+            it["w"] = (r >> 9) % 3
+        items.append(it)
+        res["r%d" % k] = {"Type": "T"} if (r >> 11) % 4 == 0 else {"Type": "T", "Properties": {"Name": "x"} if (r >> 13) % 2 else {}}
+    return json.dumps({"items": items, "Resources": res})
+
+
+@pytest.mark.parametrize("n", [5, 150, 700, 3000])
+def test_split_blocks_vs_oracle(n):
+    """block clauses over a document's values evaluated by the lane group at once (eval_recursive.inc split_block):
+    the reference's records in value order -- failing clauses, missing block values, disjunctions, nested blocks --
+    and, past the record staging (n = 3000), the wave kernel's retry, for every group size"""
+    rules = [("blocks.guard", BLOCKS)]
+    docs = [_block_doc(n, 17 + n), _block_doc(n // 2 + 1, 5 + n)]
+    data = [("g-%d.json" % i, d) for i, d in enumerate(docs)]
+    exp, ecode, _ = oracle_validate(rules, data)
+    for group in (1, 16, 64):
+        (out, code), g = _report(rules, docs, group)
+        assert g == group
+        assert (out, code) == (exp, ecode), group
+
+
+RAISING_BLOCK = """rule r {
+    items[*] {
+        name exists
+        size empty
+    }
+}
+"""
+
+
+def test_error_inside_a_split_block():
+    """an error raised by one value of a split block: the sequential loop runs again and raises the reference's
+    error for the first such value"""
+    items = [{"name": "a%d" % k, "size": []} for k in range(150)]
+    items[61]["size"] = 7
+    items[120]["size"] = 9
+    doc = json.dumps({"items": items})
+    rules = [("raise.guard", RAISING_BLOCK)]
+    try:
+        oracle_validate(rules, [("g-0.json", doc)], raise_errors=True)
+        raise AssertionError("the oracle did not abort")
+    except Exception as e:   # guard_oracle.GuardError
+        want = getattr(e, "display", lambda: str(e))()
+    for group in (1, 16, 64):
+        with pytest.raises(guard_amd.GuardError) as g:
+            _report(rules, [doc], group)
+        assert g.value.message == want, group
