@@ -39,8 +39,11 @@ def main():
         corpus = synth.tf_bench_corpus(n) if pack == "cfg4" else synth.config_corpus(n)
     names = ["d-%d.json" % i for i in range(n)]
     out = {}
-    groups = [int(g) for g in os.environ.get("GROUPS", "16").split(",")]
-    for fname, text in rulepack.rule_pack(pack):
+    groups = [int(g) for g in os.environ.get("GSIZES", "16").split(",")]
+    files = rulepack.rule_pack(pack)
+    if os.environ.get("EXTRA"):   # a guard file of variant rules (lets first), each rule timed on its own
+        files = [(os.path.basename(os.environ["EXTRA"]), open(os.environ["EXTRA"]).read())]
+    for fname, text in files:
         lets, rules = split_rules(text)
         variants = [("(whole file)", text)] + [(re.match(r"rule (\w+)", r).group(1), "\n".join(lets) + "\n" + r + "\n")
                                               for r in rules]
