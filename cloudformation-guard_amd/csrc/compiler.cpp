@@ -373,6 +373,34 @@ struct Compiler {
     return true;
   }
 
+  // A filter conjunction the device tests for one value without the evaluator (PPart.c bit 29, eval_core.inc
+  // quick_conj): every clause an access clause that cannot raise (error_free_clause), over a path of plain keys
+  // optionally ending in an unnamed `[*]` / `*`, compared with one literal or checked by a unary operator.
+  // Records are suppressed inside filters, so its status is all the test needs.
+  bool quick_conj(uint32_t cj) const {
+    const PRange2 C = conjs[cj];
+    if (C.n < 1) return false;
+    for (uint32_t i = 0; i < C.n; i++) {
+      const PRange2 Di = disjs[disj_refs[C.first + i]];
+      for (uint32_t j = 0; j < Di.n; j++) {
+        const uint32_t cid = clause_refs[Di.first + j];
+        const PClause& pc = clauses[cid];
+        if (pc.kind != C_ACCESS || !error_free_clause(cid)) return false;
+        const uint32_t op = pc.flags & 15u, rk = (pc.flags >> 8) & 15u;
+        if (op < OP_EXISTS && rk != RHS_LITERAL) return false;
+        const PQuery& q = queries[pc.a];
+        if (q.n < 1) return false;
+        for (uint32_t k = 0; k < q.n; k++) {
+          const PPart& pp = parts[q.first + k];
+          if (pp.kind == P_THIS || pp.kind == P_KEY) continue;
+          if ((pp.kind == P_ALL_VALUES || pp.kind == P_ALL_INDICES) && pp.a == NONE && k + 1 == q.n) continue;
+          return false;
+        }
+      }
+    }
+    return true;
+  }
+
   uint32_t query(const AccessQuery& q) {
     uint32_t qid = (uint32_t)queries.size();
     queries.push_back(PQuery{0, 0, q.match_all ? 1u : 0u, 0});
@@ -666,6 +694,7 @@ struct Compiler {
         if (pp.kind == P_FILTER) {
           pp.c = fast_filter_clause(pp.a, query_block[q]);
           if (pp.b == NONE && coop_conj(pp.a, 0)) pp.c |= 1u << 30;   // eval_core.inc COOP_FILTER
+          if (pp.b == NONE && quick_conj(pp.a)) pp.c |= 1u << 29;     // eval_core.inc QUICK_FILTER
         }
       }
     // PQuery.pad = 1: a walk of the query does nothing but produce results -- no named `*` / `[*]` / filter
