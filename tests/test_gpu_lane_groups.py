@@ -188,3 +188,31 @@ def test_error_inside_a_split_block():
         with pytest.raises(guard_amd.GuardError) as g:
             _report(rules, [doc], group)
         assert g.value.message == want, group
+
+
+COMPARES = """rule eq_values { items[*].v == 1 }
+rule ne_lists { items[*].tags != 'bad' }
+rule exists_values { items[*].w exists }
+rule in_values { items[*].kind in ['a', 'c'] }
+rule in_lists { items[*].tags in ['ok'] }
+rule gt_values { items[*].v > 0 }
+rule regex_values { items[*].name == /^n[0-4]/ }
+rule some_values { some items[*].w == 2 }
+rule not_in_values { items[*].kind not in ['b'] }
+rule empty_values { items[*].tags !empty }
+"""
+
+
+@pytest.mark.parametrize("n", [40, 700, 3000])
+def test_split_comparisons_vs_oracle(n):
+    """an access clause's comparison over a long value list shared out by the lane group (eval_recursive.inc
+    split_compare): unresolved values' records first, then each value's comparison, in value order -- equal to
+    the oracle for every group size, past the record staging too (n = 3000)"""
+    rules = [("compares.guard", COMPARES)]
+    docs = [_block_doc(n, 31 + n), _block_doc(n // 3 + 1, 3 + n)]
+    data = [("g-%d.json" % i, d) for i, d in enumerate(docs)]
+    exp, ecode, _ = oracle_validate(rules, data)
+    for group in (1, 16, 64):
+        (out, code), g = _report(rules, docs, group)
+        assert g == group
+        assert (out, code) == (exp, ecode), group
