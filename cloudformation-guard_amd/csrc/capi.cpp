@@ -738,6 +738,16 @@ void session_upload(gg_session* s) {
     if (w > gg_session::kMaxLdsProgWords) w = p->prog.hdr.off_dfa;
     if (w <= gg_session::kMaxLdsProgWords) s->lds_prog_words = std::max(s->lds_prog_words, (w + 3u) & ~3u);
   }
+  // A session whose programs need the NFA simulation (a regex past the DFA limits) evaluates in the wave kernel:
+  // the lane kernel's NFA variant gave wrong verdicts for a program of three or more NFA-simulated regexes in some
+  // builds of round 6 (tests/test_gpu_parity.py test_nfa_regex_pack_vs_oracle) while the wave kernel's matched the
+  // oracle in every build; the cause is not found.  GG_NFA_LANES=1 keeps the lane kernel (A/B).
+  {
+    bool nfa = false;
+    for (auto& p : s->progs)
+      for (auto& r : p->prog.regex) nfa |= r.nfa;
+    if (nfa && s->mode == 0 && !(getenv("GG_NFA_LANES") && atoi(getenv("GG_NFA_LANES")))) s->mode = 1;
+  }
   size_t ntiles = s->docs.ndocs() * s->progs.size();
   const bool large_docs = s->docs.ndocs() && arena_nodes(s) / s->docs.ndocs() > 4096;
   // Documents per lane batch: 64 (a wave's lanes, one tile each), or -- for a launch of few large documents

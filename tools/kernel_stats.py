@@ -27,13 +27,19 @@ if PACK == "micro":
     FILES = [(k + ".guard", v) for k, v in CASES.items()]
 else:
     FILES = rulepack.rule_pack(PACK)
+if os.environ.get("EXTRA"):   # each rule of a variants file on its own (lets first), as tools/rule_split_timing.py
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import re  # noqa: E402
+    from rule_split_timing import split_rules  # noqa: E402
+    pre, rs = split_rules(open(os.environ["EXTRA"]).read())
+    FILES = [(re.match(r"rule (\w+)", r).group(1) + ".guard", "\n".join(pre) + "\n" + r + "\n") for r in rs]
 corpus = None
 if PACK == "cfg5":
     import synth  # noqa: E402
     corpus = synth.config_corpus(ndocs, start=0)
 elif PACK == "cfg4":
     import synth  # noqa: E402
-    corpus = synth.tf_bench_corpus(ndocs, start=0)
+    corpus = synth.tf_corpus(ndocs, n_resources=int(os.environ["SIZE"])) if os.environ.get("SIZE") else synth.tf_bench_corpus(ndocs, start=0)
 for name, text in FILES:
     s = guard_amd.Session()
     s.add_rules(text, name)
