@@ -775,6 +775,29 @@ void session_upload(gg_session* s) {
     if (const char* e = getenv("GG_LANE_DOCS")) { s->lane_docs = (uint32_t)std::min(64, std::max(1, atoi(e))); s->lane_group = 1; }
   }
   size_t nbatches = (s->docs.ndocs() + s->lane_docs - 1) / s->lane_docs * s->progs.size();
+  // Lane groups (few large documents, no shape order): documents ordered by arena size inside each XCD's share
+  // of the L-document chunks (the kernel's c0 / c1 split), largest first.  A batch's L documents are then of
+  // similar size, so its lane groups' loops run similar trip counts, and every XCD queue hands out its largest
+  // plans first (longest-first scheduling: the launch does not end on a 2000-resource plan started last).
+  // GG_SIZE_ORDER=0 keeps load order.  Results do not depend on the order (tiles stay indexed by document).
+  if (s->lane_group > 1 && !s->has_order && s->mode != 1 && s->docs.ndocs() > s->lane_docs &&
+      !(getenv("GG_SIZE_ORDER") && atoi(getenv("GG_SIZE_ORDER")) == 0)) {
+    const DocBatch& D = s->docs;
+    const size_t nd = D.ndocs(), L = s->lane_docs, nchunks = (nd + L - 1) / L, total = arena_nodes(s);
+    std::vector<uint32_t> ord(nd);
+    std::vector<uint64_t> size(nd);
+    for (size_t d = 0; d < nd; d++) {
+      ord[d] = (uint32_t)d;
+      size[d] = (d + 1 < nd ? (uint64_t)D.base[d + 1] : (uint64_t)total) - (uint64_t)D.base[d];
+    }
+    for (size_t x = 0; x < 8; x++) {
+      const size_t lo = std::min(nd, nchunks * x / 8 * L), hi = std::min(nd, nchunks * (x + 1) / 8 * L);
+      std::stable_sort(ord.begin() + lo, ord.begin() + hi, [&](uint32_t a, uint32_t b) { return size[a] > size[b]; });
+    }
+    s->dv->d_order.upload(ord.data(), nd, st);
+    HIPCHK(hipStreamSynchronize(st));   // ord dies at the end of this scope
+    s->has_order = true;
+  }
   // wave mode: all tiles (mode 1) or only the lane kernel's overflow tiles (mode 0)
   size_t wave_slots = s->mode == 1 ? (size_t)dev_ncu(s->device) * 8 : (size_t)dev_ncu(s->device) * 2;
   uint32_t slots = (uint32_t)std::min<size_t>(std::max<size_t>(ntiles, 1), wave_slots);

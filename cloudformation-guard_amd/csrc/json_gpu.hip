@@ -141,15 +141,35 @@ struct Text {
   }
   // the window offset of document byte i (after plain_run(i) loaded its window)
   __device__ uint32_t woff(uint64_t i) const { return (uint32_t)((base + i) & 15ull); }
+  // YAML plain scalars (yaml_gpu.inc scan_plain): bit 7 set where the byte is not an ordinary plain-scalar
+  // byte -- a space or control byte, ':', '#', DEL, a non-ASCII byte, and in flow context , [ ] { } (the
+  // lowest flagged byte is exact; a borrow can only flag a later byte too, which shortens a run)
+  __device__ static uint32_t eq_bytes(uint32_t x, uint32_t rep) { const uint32_t v = x ^ rep; return (v - 0x01010101u) & ~v; }
+  template <bool FLOW>
+  __device__ static uint32_t yplain_special(uint32_t x) {
+    uint32_t m = eq_bytes(x, 0x3A3A3A3Au) | eq_bytes(x, 0x23232323u) | eq_bytes(x, 0x7F7F7F7Fu) | ((x - 0x21212121u) & ~x) | x;
+    if (FLOW)
+      m |= eq_bytes(x, 0x2C2C2C2Cu) | eq_bytes(x, 0x5B5B5B5Bu) | eq_bytes(x, 0x5D5D5D5Du) | eq_bytes(x, 0x7B7B7B7Bu) |
+           eq_bytes(x, 0x7D7D7D7Du);
+    return m & 0x80808080u;
+  }
+  // bit 7 set where the byte is not a space (exact per byte: no borrows)
+  __device__ static uint32_t not_space(uint32_t x) {
+    const uint32_t v = x ^ 0x20202020u;
+    return (((v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | v) & 0x80808080u;
+  }
   // the number of plain printable ASCII bytes from i to the first special byte, the end of i's
   // 16-byte block or the end of the document (0 when byte i is special)
-  __device__ uint32_t plain_run(uint64_t i) {
+  __device__ uint32_t plain_run(uint64_t i) { return run_of(i, [](uint32_t x) { return special(x); }); }
+  // the same for the bytes SP flags (yplain_special, not_space)
+  template <typename SP>
+  __device__ __attribute__((always_inline)) uint32_t run_of(uint64_t i, SP&& sp) {
     if (i >= n) return 0;
     const uint64_t g = base + i, a = g & ~15ull;
     if (a != wb) { w = *(const uint4*)(s + a); wb = a; }
     const uint32_t k = (uint32_t)(g - a);
-    uint64_t lo = (uint64_t)special(w.x) | ((uint64_t)special(w.y) << 32);
-    uint64_t hi = (uint64_t)special(w.z) | ((uint64_t)special(w.w) << 32);
+    uint64_t lo = (uint64_t)sp(w.x) | ((uint64_t)sp(w.y) << 32);
+    uint64_t hi = (uint64_t)sp(w.z) | ((uint64_t)sp(w.w) << 32);
     if (k < 8) lo &= ~0ull << (8u * k);
     else { lo = 0; hi &= ~0ull << (8u * (k - 8u)); }
     const uint32_t first = lo ? (uint32_t)__builtin_ctzll(lo) >> 3 : (hi ? 8u + ((uint32_t)__builtin_ctzll(hi) >> 3) : 16u);

@@ -82,6 +82,27 @@ def test_formats_in_lane_groups():
         assert _report(rules, docs, 8, output=fmt)[0] == _report(rules, docs, 1, output=fmt)[0], fmt
 
 
+def test_size_order_does_not_change_the_report():
+    """lane-group launches evaluate documents largest first inside each XCD's share (capi.cpp session_upload,
+    GG_SIZE_ORDER); the report stays in document order and equals load order's and the oracle's"""
+    rules = rule_pack("cfg4")
+    sizes = [40, 260, 90, 700, 15, 330, 120, 520, 60, 210, 410, 25, 150, 95, 380, 45, 600, 70]
+    docs = [synth.tf_corpus(1, start=31 + i, n_resources=n)[0] for i, n in enumerate(sizes)]
+    data = [("g-%d.json" % i, d) for i, d in enumerate(docs)]
+    exp = oracle_validate(rules, data)[:2]
+    old = os.environ.get("GG_SIZE_ORDER")
+    try:
+        os.environ["GG_SIZE_ORDER"] = "0"
+        unsorted = _report(rules, docs, 16)[0]
+    finally:
+        if old is None:
+            os.environ.pop("GG_SIZE_ORDER", None)
+        else:
+            os.environ["GG_SIZE_ORDER"] = old
+    assert _report(rules, docs, 16)[0] == exp
+    assert unsorted == exp
+
+
 RAISING = """let picked = items[ size empty ]
 rule r when %picked !empty {
     %picked.name exists
