@@ -24,7 +24,10 @@ profiles/pmc_<round>.json exists for the same workload, else nul
 cpu_baseline: the CPU oracle (oracle/guard_oracle, a pure-Python restatement of the reference
 evaluator -- NOT the reference binary, which cannot be built here) run on a bounded sample of the
 same documents x the same rule pack, in one process per core on the host cores of this box:
-`value` end to end (load + evaluate + structured report), `eval_only_value` evaluation alone.
+`value` end to end (load + evaluate + structured report), `eval_only_value` evaluation alone.  The sample
+doubles as a full-size parity check: its per-tile statuses and its structured JSON report (every record,
+message and value, digested per core's document range) must equal the ones the GPU session produced for
+the same documents inside the full-size launch (`statuses_equal`, `reports_equal`).
 
 e2e (N = 1): the whole job a `validate --structured` user pays for, on the same workload -- load
 (synthetic text generated on host threads, then parsed by the MI355X JSON / YAML loader,
@@ -122,11 +125,21 @@ def _oracle_worker(args):
     from guard_oracle.parser import parse_rules
     rules = rulepack.rule_pack(workload)
     docs = _workload_docs(workload, first, n, n_resources)
-    names = ["synthetic-%d.json" % (first + i) for i in range(n)]
+    # the bench session's document names (bench.py main), so the reports compare byte for byte
+    prefix = {"cfg4": "plan", "cfg5": "snapshot"}.get(workload, "synthetic")
+    names = ["%s-%d.json" % (prefix, first + i) for i in range(n)]
+    outs = []
     t = time.time()
     for name, d in zip(names, docs):
-        validate_structured(rules, [(name, d)])
+        outs.append(validate_structured(rules, [(name, d)]))
     t_e2e = time.time() - t
+    # the structured JSON report of the whole range, joined from the one-document reports (the serde pretty
+    # layout: each document's object indented by 2 inside one array), with its exit code
+    import hashlib
+    joined = "[\n" + ",\n".join(o[0][2:-2] for o in outs) + "\n]"
+    codes = [o[1] for o in outs]
+    rcode = -1 if -1 in codes else (19 if 19 in codes else 0)
+    report = (first, n, hashlib.sha256(joined.encode()).hexdigest(), len(joined), rcode)
     parsed = [load_document(d, name) for name, d in zip(names, docs)]
     prs = [parse_rules(text, rn) for rn, text in rules]
     code = {E.PASS: 0, E.FAIL: 1, E.SKIP: 2}   # guard_types.h ST_PASS / ST_FAIL / ST_SKIP
@@ -139,7 +152,7 @@ def _oracle_worker(args):
             except E.GuardError:
                 st.append(3)   # an erroring tile (gg_session_tile_status)
     t_eval = time.time() - t
-    return t_e2e, t_eval, n * len(rules), first, bytes(st)
+    return t_e2e, t_eval, n * len(rules), first, bytes(st), report
 
 
 def cpu_baseline(workload, n_resources, per_core):
@@ -157,7 +170,7 @@ def cpu_baseline(workload, n_resources, per_core):
     # per-(document, rules file) statuses of the sample, tile order: the GPU's are checked against them
     statuses = b"".join(r[4] for r in sorted(res, key=lambda r: r[3]))
     return {"value": round(evals / busy, 2), "unit": "evals/s", "cores": cores, "kind": "port",
-            "_statuses": statuses,
+            "_statuses": statuses, "_reports": [r[5] for r in sorted(res, key=lambda r: r[3])],
             "eval_only_value": round(evals / busy_eval, 2), "host": host_info(),
             "sample": "%d %s documents x %d rules files (%d evals) through the Python restatement of the reference "
                       "(oracle/guard_oracle, not the reference binary), one process per core; value = load + evaluate + "
@@ -391,8 +404,26 @@ def main():
         if bad:
             cpu["first_mismatch_tile"] = bad[0]
             log("CPU/GPU status MISMATCH at %d of %d tiles (first: tile %d)" % (len(bad), len(exp), bad[0]))
+        # and their structured JSON reports (records, messages, values: every byte), rendered from the
+        # full-size session's results for the same document ranges
+        reps = cpu.pop("_reports", [])
+        if args.format == "json" and reps and args.workload in ("cfg2", "cfg3", "cfg4", "cfg5"):
+            import hashlib
+            t0 = time.time()
+            mism = []
+            for (f0, n, digest, nbytes, code) in reps:
+                txt, gcode = sess.report_range("json", f0, n)
+                if gcode != code or len(txt) != nbytes or hashlib.sha256(txt.encode()).hexdigest() != digest:
+                    mism.append(f0)
+            cpu["reports_checked_docs"] = sum(r[1] for r in reps)
+            cpu["reports_equal"] = not mism
+            cpu["reports_check_s"] = round(time.time() - t0, 2)
+            if mism:
+                cpu["first_report_mismatch_range"] = mism[0]
+                log("CPU/GPU report MISMATCH in %d of %d document ranges (first at document %d)" % (len(mism), len(reps), mism[0]))
     elif cpu is not None:
         cpu.pop("_statuses", None)
+        cpu.pop("_reports", None)
     tally_sum = int(counts.sum().item())   # the all-reduced tensor: every rank's last-step tallies
     n_fail, n_pass, n_skip, n_err = sess.stat(4), sess.stat(5), sess.stat(6), sess.stat(7)
 

@@ -153,6 +153,11 @@ struct Text {
            eq_bytes(x, 0x7D7D7D7Du);
     return m & 0x80808080u;
   }
+  // comments: bit 7 set where the byte is not printable ASCII (a control byte -- the tab and the line break
+  // included --, DEL or a non-ASCII byte)
+  __device__ static uint32_t not_printable(uint32_t x) {
+    return (eq_bytes(x, 0x7F7F7F7Fu) | ((x - 0x20202020u) & ~x) | x) & 0x80808080u;
+  }
   // bit 7 set where the byte is not a space (exact per byte: no borrows)
   __device__ static uint32_t not_space(uint32_t x) {
     const uint32_t v = x ^ 0x20202020u;
