@@ -173,12 +173,20 @@ struct DBuf {
   void alloc(size_t count) {
     n = count;
     if (count <= cap && p) return;
-    // a growing buffer may still be read by work queued on its session's stream: hipFree waits for it
+    // a growing buffer may still be read by work queued on its session's stream: hipFree waits for it --
+    // for the whole device, so a pooled set growing in a streamed batch waited for the other chunk's report
+    // (chunk 3's upload 2.8 s instead of 50 ms, 7.7-9.3 s per 1 M templates against 5.1-5.3 s when no set grew,
+    // profiles/r06zf_stream_*).  Growth is made rare: a buffer of 1 MB or more asks for 1/8 headroom (the next
+    // chunk's arena is a few percent larger or smaller), and the capacity is the cache's whole size class.
     dev_free_sync(p);
     p = nullptr;
     n = count;
-    cap = count;
-    if (count) HIPCHK(dev_alloc(&p, count * sizeof(T)));
+    cap = 0;
+    if (count) {
+      const size_t want = count * sizeof(T) >= ((size_t)1 << 20) ? count + count / 8 : count;
+      HIPCHK(dev_alloc(&p, want * sizeof(T)));
+      cap = std::max(want, dev_cache_class(want * sizeof(T)) / sizeof(T));
+    }
   }
   // alloc with headroom: a growing buffer is reallocated rarely (hipFree synchronises the whole device,
   // which would serialise the device reporter's overlapped render and copy-out)
@@ -2116,6 +2124,8 @@ int32_t stream_single(int dev, const validate_input_t* docs, size_t n_docs, cons
     // GG_STREAM_SERIAL=1 (diagnostic): a chunk loads only after the previous one is reported
     const bool serial = getenv("GG_STREAM_SERIAL") != nullptr;
     size_t reported = 0;
+    // chunk j's session has been torn down (its buffer set is back in the pool): chunk j + 2 uploads into it
+    std::vector<char> torn(nchunks, 0);
     std::thread producer([&]() {
       for (size_t k = 0; k < nchunks; k++) {
         Slot& sl = slot[k & 1];
@@ -2152,6 +2162,13 @@ int32_t stream_single(int dev, const validate_input_t* docs, size_t n_docs, cons
             if (ses->progs.empty()) {
               ses->tiles.clear(); ses->rule_status.clear(); ses->recs.clear(); ses->evaluated = true;
             } else {
+              // the load ran alongside chunk k - 2's teardown; the upload takes that chunk's buffer set (a new set
+              // would allocate ~25 GB afresh: chunk 3's upload took 3.8 s instead of 40 ms when it raced the
+              // teardown, profiles/r06zj_stream_load_trace.log)
+              if (k >= 2) {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return torn[k - 2] || stop; });
+              }
               session_upload(ses.get());
               mark("uploaded", k);
               session_run(ses.get(), true);
@@ -2338,6 +2355,11 @@ int32_t stream_single(int dev, const validate_input_t* docs, size_t n_docs, cons
         }
         cv.notify_all();
         done.reset();
+        {
+          std::lock_guard<std::mutex> lk(mu);
+          torn[k] = 1;
+        }
+        cv.notify_all();
         mark("torn down", k);
       });
     }

@@ -9,12 +9,16 @@
 // is handed out again only once that event has completed -- the ordering hipFree enforced device-wide,
 // enforced per block.  dev_alloc takes a cached block of the same size class whose fence (if any) has
 // passed before calling hipMalloc.  A hipMalloc that fails empties the device's list and tries once more.
-// GG_DEV_CACHE_GB bounds the bytes a device's list holds (default 16; 0 turns the cache off).  Memory held
+// GG_DEV_CACHE_GB bounds the bytes a device's list holds (default 48; 0 turns the cache off).  Memory held
 // here is invisible to the HIP runtime and to torch's allocator in the same process, so the default stays
-// well under the 288 GB of one MI355X.
+// well under the 288 GB of one MI355X -- but above one streamed chunk's buffer set (262 144 templates: ~25 GB
+// of lane heaps, record arena and arena columns): with 16 GB the rest of every torn-down set went to hipFree,
+// which waits for the device to go idle (the other chunk's report), and the next chunk hipMalloc'd it again.
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <map>
 #include <mutex>
@@ -35,7 +39,7 @@ struct DevCache {
   DevCache() {
     const char* e = getenv("GG_DEV_CACHE_GB");
     // the cap is parsed as a double and scaled before the conversion (GG_DEV_CACHE_GB=0.5 is 512 MB)
-    const double gb = e ? atof(e) : 16.0;
+    const double gb = e ? atof(e) : 48.0;
     cap = gb > 0 ? (size_t)(gb * (double)(1ull << 30)) : 0;
   }
 };
@@ -85,21 +89,40 @@ inline hipError_t dev_alloc(void** out, size_t bytes) {
   {
     std::lock_guard<std::mutex> lk(C.mu);
     auto& fl = C.free_list[dev];
-    for (auto it = fl.lower_bound(c); it != fl.end() && it->first == c; ++it) {
+    // the smallest cached block of this class or up to 1.5 x larger: a streamed batch's last, smaller chunk
+    // (or any chunk whose counts land a class lower) takes the previous chunk's blocks instead of hipMalloc'ing
+    // ~20 GB afresh (2.2-3.8 s, profiles/r06zk_stream_trace.log); the block keeps its own class
+    for (auto it = fl.lower_bound(c); it != fl.end() && it->first <= c + c / 2; ++it) {
       // a fenced block is taken only once the work queued before its dev_free_on has completed
       if (it->second.fence) {
         if (hipEventQuery(it->second.fence) != hipSuccess) { (void)hipGetLastError(); continue; }
         C.spare_events[dev].push_back(it->second.fence);
       }
+      const size_t have = it->first;
       *out = it->second.p;
-      C.held[dev] -= c;
+      C.held[dev] -= have;
       fl.erase(it);
-      C.live[*out] = {dev, c};
+      C.live[*out] = {dev, have};
       return hipSuccess;
     }
   }
   void* p = nullptr;
+  // GG_ALLOC_TRACE=<MB>: every cache miss of at least that size on stderr, with the hipMalloc's wall time
+  static const long trace_mb = getenv("GG_ALLOC_TRACE") ? atol(getenv("GG_ALLOC_TRACE")) : -1;
+  const auto t0 = std::chrono::steady_clock::now();
   hipError_t e = hipMalloc(&p, c);
+  if (trace_mb >= 0 && c >= ((size_t)trace_mb << 20)) {
+    size_t cached = 0, near = 0;
+    {
+      std::lock_guard<std::mutex> lk(C.mu);
+      cached = C.held[dev];
+      auto it = C.free_list[dev].lower_bound(c / 2);
+      if (it != C.free_list[dev].end()) near = it->first;
+    }
+    fprintf(stderr, "[alloc] miss %zu MB on device %d: hipMalloc %.1f ms (cache holds %zu MB, next class >= half: %zu MB)\n",
+            c >> 20, dev, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(),
+            cached >> 20, near >> 20);
+  }
   if (e != hipSuccess) {
     (void)hipGetLastError();
     dev_cache_flush(dev);

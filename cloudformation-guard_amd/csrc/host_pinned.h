@@ -90,7 +90,8 @@ inline void pinned_free(void* p) {
 // blocks here and give them back at the end of the call instead of unpinning them (pinning 256 MB costs
 // ~0.1 s, and the report copy-out of the sessions after a call that unpinned its staging was measured at
 // half the rate, profiles/r05x_report_ab.log).  At most GG_PINNED_CACHE_GB per device stay cached (default
-// 1: the one-device stream's 256 MB staging plus a device-list stream's working set of 64 MB blocks); page-
+// 2: the one-device stream's 256 MB staging, the device loader's two 64 MB bounce buffers per load, and a
+// device-list stream's working set of 64 MB blocks); page-
 // locked memory is invisible to the rest of the host, so gg_device_cache_release hands it back too
 // (pinned_cache_flush).
 struct PinnedCache {
@@ -100,7 +101,7 @@ struct PinnedCache {
   std::unordered_map<int, size_t> cached;                  // device -> bytes in `free`
   PinnedCache() {
     const char* e = getenv("GG_PINNED_CACHE_GB");
-    const double gb = e ? atof(e) : 1.0;
+    const double gb = e ? atof(e) : 2.0;
     cap = gb > 0 ? (size_t)(gb * (double)(1ull << 30)) : 0;
   }
   static PinnedCache& get() { static PinnedCache* c = new PinnedCache; return *c; }

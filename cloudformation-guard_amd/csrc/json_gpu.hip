@@ -721,6 +721,15 @@ uint32_t grid_for(uint64_t items, uint32_t block) {
 // Host <-> device transfers of the loader's bulk arrays through two pinned bounce buffers: the
 // DMA of one chunk overlaps the host threads' copy of the other (hipMemcpy from / to pageable
 // memory stages through the runtime at a few GB/s, single threaded).
+// one copy stream per device for every load's staging, created on first use and kept for the process
+inline hipStream_t staging_stream(int dev) {
+  static std::mutex mu;
+  static hipStream_t st[64] = {};
+  if (dev < 0 || dev >= 64) dev = 0;
+  std::lock_guard<std::mutex> lk(mu);
+  if (!st[dev]) JCHK(hipStreamCreateWithFlags(&st[dev], hipStreamNonBlocking));
+  return st[dev];
+}
 struct Staging {
   static constexpr size_t kChunk = 64ull << 20;
   void* pin[2] = {nullptr, nullptr};
@@ -731,15 +740,20 @@ struct Staging {
     int dev = 0;
     JCHK(hipGetDevice(&dev));
     for (int i = 0; i < 2; i++)
-      if (!(pin[i] = pinned_alloc(kChunk, dev))) throw std::runtime_error("pinned host staging: allocation failed");
-    JCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+      if (!(pin[i] = pinned_get(kChunk, dev))) throw std::runtime_error("pinned host staging: allocation failed");
+    s = staging_stream(dev);
     JCHK(hipEventCreateWithFlags(&ev[0], hipEventDisableTiming));
     JCHK(hipEventCreateWithFlags(&ev[1], hipEventDisableTiming));
     threads = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
   }
   ~Staging() {
-    if (s) { hipStreamSynchronize(s); hipStreamDestroy(s); }
-    for (int i = 0; i < 2; i++) { pinned_free(pin[i]); if (ev[i]) hipEventDestroy(ev[i]); }
+    if (s) hipStreamSynchronize(s);   // the stream stays (staging_stream): no create / destroy per load
+    // back to the process-wide pinned cache: a streamed batch loads a chunk while another chunk's report runs,
+    // and unpinning (hipHostUnregister) at the end of every load stalled it behind that report
+    // (profiles/r06zi_stream_load_trace.log: 64-540 ms between the index and the loader's return)
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    for (int i = 0; i < 2; i++) { pinned_put(pin[i], kChunk, dev); if (ev[i]) hipEventDestroy(ev[i]); }
   }
   // fn(t, nthreads) on `threads` host threads
   template <typename F>
