@@ -241,6 +241,8 @@ def main():
     ap.add_argument("--e2e-stream", type=int, default=262144,
                     help="also time the streamed batch entry (cfn_guard_validate_batch_stream) over the same synthetic "
                          "texts with this many documents per chunk (0: off; cfg2/cfg3 at N=1 only)")
+    ap.add_argument("--e2e-stream-runs", type=int, default=2,
+                    help="runs of the streamed JSON leg (a child process each); the line reports the fastest and lists all")
     ap.add_argument("--e2e-devices-docs", type=int, default=262144,
                     help="also time the streamed batch entry over every visible device (cfn_guard_validate_batch_stream_"
                          "devices) with this many synthetic documents per device (0: off; cfg2/cfg3 at N=1 only)")
@@ -301,11 +303,21 @@ def main():
         if args.e2e_devices_docs:
             legs.append(("devices", args.e2e_devices_docs, args.e2e_stream, 1, "json"))
         for key, nd, chunk, ndev, output in legs:
-            log("e2e stream leg %s: %d documents in chunks of %d (a process of its own)" % (key, nd, chunk))
-            try:
-                early[key] = _stream_leg(args.workload, first, nd, args.resources, args.format, chunk, ndev, lthreads, output)
-            except Exception as e:   # the leg is reported as failed; the line still prints
-                early[key] = {"error": str(e)[-500:]}
+            # the JSON leg runs --e2e-stream-runs times (a process each) and reports the fastest with every run's
+            # wall clock: the same leg took 5.0-12.8 s on one box from run to run (profiles/r06zk_*, r06zm_*)
+            runs = max(1, args.e2e_stream_runs) if key == "json" else 1
+            for r in range(runs):
+                log("e2e stream leg %s (run %d/%d): %d documents in chunks of %d (a process of its own)"
+                    % (key, r + 1, runs, nd, chunk))
+                try:
+                    leg = _stream_leg(args.workload, first, nd, args.resources, args.format, chunk, ndev, lthreads, output)
+                except Exception as e:   # the leg is reported as failed; the line still prints
+                    early[key] = {"error": str(e)[-500:]}
+                    break
+                all_s = early.get(key, {}).get("runs_s", []) + [round(leg["seconds"], 3)]
+                if key not in early or leg["seconds"] < early[key]["seconds"]:
+                    early[key] = leg
+                early[key]["runs_s"] = all_s
     texts = None
     t_gen = 0.0
     if args.workload in ("cfg4", "cfg5"):
@@ -558,11 +570,12 @@ def main():
         e2e_stream = {"value": round(ntiles / t_stream, 1), "unit": "evals/s", "seconds": round(t_stream, 3),
                       "chunk_docs": args.e2e_stream, "report_bytes": nbytes[0],
                       "report_GBps": round(nbytes[0] / t_stream / 1e9, 3), "exit_code": st_code,
-                      "gen_s": round(t_gen_s, 3),
+                      "gen_s": round(t_gen_s, 3), "runs_s": leg.get("runs_s"),
                       "note": "cfn_guard_validate_batch_stream (the C ABI batch entry, JSON) in a process of its own over "
                               "the same synthetic texts resident in host memory: load + upload + evaluation + fetch + "
                               "device-rendered report to host memory (shader copy-out), chunked and overlapped, counted "
-                              "by the library's native callback; text generation (gen_s) not included"}
+                              "by the library's native callback; text generation (gen_s) not included; the fastest of "
+                              "runs_s (one process each, before the bench process touches the GPU)"}
 
     e2e_stream_sarif = None
     if (rank == 0 and world == 1 and not args.no_e2e and args.e2e_stream and args.e2e_sarif
